@@ -1,0 +1,119 @@
+/* siddhi_amd — MI355X-native pattern/sequence matching engine, C ABI (the drop-in boundary).
+ *
+ * Each entry point replaces one reference API (paths relative to
+ * modules/siddhi-core/src/main/java/org/wso2/siddhi/core/):
+ *   sm_manager_create / destroy     SiddhiManager()                         SiddhiManager.java:56
+ *   sm_app_create                   SiddhiManager.createSiddhiAppRuntime    SiddhiManager.java:73
+ *   sm_app_input_handler            SiddhiAppRuntime.getInputHandler        SiddhiAppRuntime.java:337
+ *   sm_input_send                   InputHandler.send(long, Object[])       stream/input/InputHandler.java:53
+ *   sm_input_send_columns           InputHandler.send(Event[])              stream/input/InputHandler.java:65 (columnar)
+ *   sm_app_add_stream_callback      SiddhiAppRuntime.addCallback(String, StreamCallback)  :243
+ *   sm_app_add_query_callback       SiddhiAppRuntime.addCallback(String, QueryCallback)   :254
+ *   sm_app_start / sm_app_shutdown  SiddhiAppRuntime.start / shutdown       :353 / :396
+ *   sm_app_advance_time             @app:playback heartbeat (EventTimeBasedMillisTimestampGenerator.java:99)
+ *   sm_app_process_device_batch     StreamJunction.sendData over a device-resident columnar batch (no Java
+ *                                   counterpart: the bulk entry a JNI/Panama receiver would call)
+ *
+ * Threading / delivery: an app handle is single-owner (calls are serialised internally). Events are
+ * staged on send and processed on the GPU at sm_app_flush (also at shutdown and when the staging buffer
+ * fills); callbacks run on the calling thread at that point, in the reference's emission order. Event
+ * arrays passed to callbacks are valid only during the callback. Errors never cross the ABI as exceptions:
+ * every call returns a status and sm_last_error() holds the thread-local message.
+ */
+#ifndef SIDDHI_AMD_H
+#define SIDDHI_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  SM_OK = 0,
+  SM_E_PARSE = 1,        /* SiddhiParserException */
+  SM_E_VALIDATION = 2,   /* SiddhiAppValidationException / SiddhiAppCreationException */
+  SM_E_UNSUPPORTED = 3,  /* construct outside the hot-path subset */
+  SM_E_TYPE = 4,         /* value type does not match the stream definition (ClassCastException) */
+  SM_E_DEVICE = 5,       /* HIP error */
+  SM_E_RUNTIME = 6,      /* runtime failure (reference NullPointerException paths, capacity) */
+  SM_E_ARG = 7
+};
+
+enum { SM_INT = 0, SM_LONG = 1, SM_FLOAT = 2, SM_DOUBLE = 3, SM_STRING = 4, SM_BOOL = 5 };
+
+typedef struct sm_value {
+  int32_t type;
+  int32_t is_null;
+  int64_t i;     /* INT / LONG / BOOL */
+  double d;      /* FLOAT / DOUBLE */
+  const char* s; /* STRING */
+} sm_value;
+
+typedef struct sm_event {
+  int64_t timestamp;
+  const sm_value* data;
+  int32_t n;
+} sm_event;
+
+typedef struct sm_manager sm_manager;
+typedef struct sm_app sm_app;
+typedef struct sm_input sm_input;
+
+typedef void (*sm_stream_callback)(void* user, const sm_event* events, size_t n);
+typedef void (*sm_query_callback)(void* user, int64_t timestamp, const sm_event* in_events, size_t n_in,
+                                  const sm_event* removed_events, size_t n_removed);
+
+const char* sm_last_error(void);
+const char* sm_version(void);
+
+int sm_manager_create(sm_manager** out);
+void sm_manager_destroy(sm_manager* m);
+
+int sm_app_create(sm_manager* m, const char* siddhiql, sm_app** out);
+void sm_app_destroy(sm_app* app);
+int sm_app_start(sm_app* app);
+int sm_app_flush(sm_app* app);
+int sm_app_shutdown(sm_app* app);
+
+int sm_app_input_handler(sm_app* app, const char* stream_id, sm_input** out);
+int sm_input_send(sm_input* in, int64_t timestamp, const sm_value* row, size_t n);
+/* n events of the handler's stream; cols[k] = host column of attribute k (int32 / int64 / float / double /
+ * uint8 for BOOL / const char* for STRING); null_flags may be NULL or hold per-attribute uint8 arrays. */
+int sm_input_send_columns(sm_input* in, size_t n, const int64_t* timestamps, const void* const* cols,
+                          const uint8_t* const* null_flags);
+
+/* attribute types (SM_INT …) of a stream: writes up to cap entries, returns the count in *n */
+int sm_app_stream_schema(sm_app* app, const char* stream_id, int32_t* types, size_t cap, size_t* n);
+
+int sm_app_advance_time(sm_app* app, int64_t timestamp);
+/* wall-clock scheduler emulation: fire every due timer at its scheduled time up to `timestamp` */
+int sm_app_advance_wallclock(sm_app* app, int64_t timestamp);
+
+int sm_app_add_stream_callback(sm_app* app, const char* stream_id, sm_stream_callback cb, void* user);
+int sm_app_add_query_callback(sm_app* app, const char* query_name, sm_query_callback cb, void* user);
+
+/* Parity/diagnostics: collect every output as JSON
+ * {"streams": {"<id>": [[ts, [values], [refs]], ...]}, "queries": {"<name>": [[ts, [[values]...]], ...]}}
+ * where refs are the global arrival ordinals of the events at the select list's variable positions. */
+int sm_app_set_collect(sm_app* app, int collect);
+size_t sm_app_dump_outputs(sm_app* app, char* buf, size_t len);
+
+/* Options (before the first flush): "heap_words" (per-key partial-match arena, words per semispace),
+ * "batch_events" (auto-flush threshold). */
+int sm_app_set_option(sm_app* app, const char* key, int64_t value);
+
+/* Device-resident batch of ONE stream (columns already in HBM, hipStream given as void*): every record is
+ * processed as a fresh stream segment for the fast-path queries (every e1 -> e2 within T), producing match
+ * tuples that stay on the device. `ordinals` (int64, may be NULL = base + index) gives each event's global
+ * arrival ordinal (multi-GPU shards keep the ordinals of the unsharded stream). */
+int sm_app_process_device_batch(sm_app* app, const char* stream_id, size_t n, const int64_t* d_timestamps,
+                                const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
+                                void* hip_stream);
+/* Match tuples of the last device batch for a query: n pairs (e1, e2) of ordinals relative to the batch's
+ * ordinal_base, uint32[2*n] in device memory, in reference output order (e2 ordinal, then e1 ordinal). */
+int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** d_pairs, size_t* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,198 @@
+"""siddhi_amd — MI355X-native Siddhi pattern/sequence matching, Python host mirror of the reference API.
+
+Mirrors the reference's user-facing classes (modules/siddhi-core/src/main/java/org/wso2/siddhi/core/):
+  SiddhiManager.createSiddhiAppRuntime (SiddhiManager.java:73)
+  SiddhiAppRuntime.getInputHandler / addCallback / start / shutdown (SiddhiAppRuntime.java:243-396)
+  InputHandler.send(Object[]) / send(long, Object[]) / send(Event) / send(Event[]) (InputHandler.java:47-65)
+  StreamCallback.receive(Event[]) (StreamCallback.java:101), QueryCallback.receive(long, Event[], Event[])
+  (QueryCallback.java:105), Event(timestamp, data) (core/event/Event.java)
+over the C ABI of libsiddhi_amd.so. Differences from the reference: events are processed on the GPU when the
+runtime flushes (flush(), shutdown(), or when the staging buffer fills), so callbacks fire at those points —
+in the reference's order — instead of inside send().
+"""
+import ctypes
+import time
+
+from . import _lib
+from ._lib import (OperationNotSupportedException, SiddhiAppCreationException, SiddhiAppValidationException,
+                   SiddhiDeviceError, SiddhiError, SiddhiParserException, SiddhiTypeError, check, lib)
+
+__all__ = ["SiddhiManager", "SiddhiAppRuntime", "InputHandler", "Event", "StreamCallback", "QueryCallback",
+           "SiddhiError", "SiddhiParserException", "SiddhiAppValidationException", "SiddhiAppCreationException",
+           "OperationNotSupportedException", "SiddhiTypeError", "SiddhiDeviceError"]
+
+
+class Event:
+    """core/event/Event.java"""
+
+    def __init__(self, timestamp=-1, data=None, is_expired=False):
+        self.timestamp = timestamp
+        self.data = list(data) if data is not None else []
+        self.is_expired = is_expired
+
+    def getData(self):
+        return self.data
+
+    def getTimestamp(self):
+        return self.timestamp
+
+    def isExpired(self):
+        return self.is_expired
+
+    def __repr__(self):
+        return f"Event{{timestamp={self.timestamp}, data={self.data}, isExpired={self.is_expired}}}"
+
+
+class StreamCallback:
+    """Subclass and override receive(events)."""
+
+    def receive(self, events):
+        raise NotImplementedError
+
+
+class QueryCallback:
+    """Subclass and override receive(timestamp, in_events, remove_events)."""
+
+    def receive(self, timestamp, in_events, remove_events):
+        raise NotImplementedError
+
+
+def _py_value(v):
+    if v.is_null:
+        return None
+    t = v.type
+    if t in (2, 3):
+        return v.d
+    if t == 4:
+        return v.s.decode() if v.s is not None else None
+    if t == 5:
+        return bool(v.i)
+    return v.i
+
+
+def _events(ptr, n):
+    out = []
+    for k in range(n):
+        e = ptr[k]
+        out.append(Event(e.timestamp, [_py_value(e.data[j]) for j in range(e.n)]))
+    return out
+
+
+class InputHandler:
+    def __init__(self, runtime, stream_id, handle, types):
+        self._rt = runtime
+        self.stream_id = stream_id
+        self._h = handle
+        self._types = types
+
+    def _row(self, data):
+        if len(data) != len(self._types):
+            raise SiddhiTypeError(f"stream {self.stream_id} expects {len(self._types)} attributes")
+        arr = (_lib.SmValue * max(len(data), 1))()
+        keep = []
+        for k, (v, t) in enumerate(zip(data, self._types)):
+            arr[k].type = t
+            if v is None:
+                arr[k].is_null = 1
+            elif t == 4:
+                b = str(v).encode()
+                keep.append(b)
+                arr[k].s = b
+            elif t in (2, 3):
+                arr[k].d = float(v)
+            elif t == 5:
+                arr[k].i = 1 if v else 0
+            else:
+                arr[k].i = int(v)
+        return arr, keep
+
+    def send(self, *args):
+        """send(data) | send(timestamp, data) | send(Event) | send([Event, ...])"""
+        if len(args) == 2:
+            ts, data = args
+            self._send(int(ts), data)
+        elif isinstance(args[0], Event):
+            self._send(args[0].timestamp, args[0].data)
+        elif args[0] and isinstance(args[0][0], Event):
+            for e in args[0]:
+                self._send(e.timestamp, e.data)
+        else:
+            self._send(int(time.time() * 1000), args[0])
+
+    def _send(self, ts, data):
+        arr, keep = self._row(data)
+        check(lib().sm_input_send(self._h, ts, arr, len(data)))
+
+
+class SiddhiAppRuntime:
+    def __init__(self, handle):
+        self._h = handle
+        self._cbs = []  # keep ctypes trampolines alive
+        self._inputs = {}
+
+    def getInputHandler(self, stream_id):
+        if stream_id not in self._inputs:
+            h = ctypes.c_void_p()
+            check(lib().sm_app_input_handler(self._h, stream_id.encode(), ctypes.byref(h)))
+            self._inputs[stream_id] = InputHandler(self, stream_id, h, self.stream_schema(stream_id))
+        return self._inputs[stream_id]
+
+    def stream_schema(self, stream_id):
+        types = (ctypes.c_int32 * 64)()
+        n = ctypes.c_size_t()
+        check(lib().sm_app_stream_schema(self._h, stream_id.encode(), types, 64, ctypes.byref(n)))
+        return [types[k] for k in range(n.value)]
+
+    def addCallback(self, name, callback):
+        if isinstance(callback, StreamCallback):
+            def tramp(user, evs, n, cb=callback):
+                cb.receive(_events(evs, n))
+            f = _lib.STREAM_CB(tramp)
+            check(lib().sm_app_add_stream_callback(self._h, name.encode(), f, None))
+        elif isinstance(callback, QueryCallback):
+            def tramp(user, ts, ins, nin, rm, nrm, cb=callback):
+                cb.receive(ts, _events(ins, nin) if nin else None, _events(rm, nrm) if nrm else None)
+            f = _lib.QUERY_CB(tramp)
+            check(lib().sm_app_add_query_callback(self._h, name.encode(), f, None))
+        else:
+            raise TypeError("callback must be a StreamCallback or QueryCallback")
+        self._cbs.append(f)
+
+    def start(self):
+        check(lib().sm_app_start(self._h))
+
+    def flush(self):
+        check(lib().sm_app_flush(self._h))
+
+    def shutdown(self):
+        if self._h:
+            check(lib().sm_app_shutdown(self._h))
+            lib().sm_app_destroy(self._h)
+            self._h = None
+
+    def advance_time(self, ts):
+        check(lib().sm_app_advance_time(self._h, int(ts)))
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().sm_app_destroy(self._h)
+        except Exception:
+            pass
+
+
+class SiddhiManager:
+    def __init__(self):
+        h = ctypes.c_void_p()
+        check(lib().sm_manager_create(ctypes.byref(h)))
+        self._h = h
+
+    def createSiddhiAppRuntime(self, siddhi_app):
+        h = ctypes.c_void_p()
+        check(lib().sm_app_create(self._h, siddhi_app.encode(), ctypes.byref(h)))
+        return SiddhiAppRuntime(h)
+
+    def shutdown(self):
+        if self._h:
+            lib().sm_manager_destroy(self._h)
+            self._h = None

@@ -1,0 +1,51 @@
+// Device batch descriptors shared by the runtime (host) and the NFA / filter / fast-path kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../plan.h"
+
+namespace sm {
+
+constexpr int kMaxAttrs = 48;
+constexpr int NFA_START = -3;  // ev_stream marker: SiddhiAppRuntime.start()
+constexpr int NFA_TICK = -1;   // playback heartbeat (clock advance without an event)
+constexpr int NFA_WALL = -2;   // wall-clock emulation tick
+
+enum : int32_t { NFA_ERR_ARENA = 1, NFA_ERR_TIMERS = 2, NFA_ERR_OUTPUT = 4, NFA_ERR_NPE = 8 };
+
+struct NfaStream {
+  int32_t nattr;
+  int32_t types[kMaxAttrs];
+  const void* cols[kMaxAttrs];
+  const uint8_t* nulls[kMaxAttrs];  // null flags per attribute or nullptr
+};
+
+struct NfaBatch {
+  // app batch (all records in arrival order)
+  const int32_t* ev_stream;  // stream index or NFA_* marker
+  const int64_t* ev_row;     // row within the stream's columns
+  const int64_t* ev_ts;
+  const int64_t* ev_clock;   // playback clock after the record's sendData
+  int64_t ordinal_base;      // global ordinal of record 0
+  const NfaStream* streams;
+  // advance points (playback listener firings / wall ticks), ascending position
+  const int64_t* adv_pos;
+  const int64_t* adv_clock;
+  const int64_t* adv_wall;   // wall tick target, -1 for playback points
+  int64_t nadv;
+  int64_t clock_in;          // clock before the batch
+  // this query's records grouped by key slot: key_pos[key_off[k] .. key_off[k+1]) ascending
+  const int64_t* key_off;
+  const int64_t* key_pos;
+  int32_t create_all;        // non-partitioned: the single lane exists from app creation
+  // output
+  void* out;
+  uint32_t* out_count;
+  uint32_t out_cap;
+  uint32_t out_stride;
+};
+
+void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int32_t nkeys,
+                int32_t* err_dev, hipStream_t s);
+
+}  // namespace sm

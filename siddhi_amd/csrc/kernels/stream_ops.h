@@ -1,0 +1,39 @@
+// Host entry points of the column-scan / key-grouping kernels (stream_ops.hip).
+#pragma once
+#include "nfa.h"
+#include "primitives.h"
+
+namespace sm {
+
+struct KeyProg {  // partition key expression of one stream (device copy)
+  int32_t stream, len, type, pad;
+  const Instr* code;
+  const DVal* consts;
+};
+
+// Device key → slot table (open addressing) with slot → key inverse; slots are per-key state indices.
+struct KeyTable {
+  int64_t* tkeys = nullptr;
+  int32_t* tslots = nullptr;  // slot + 1, 0 = empty
+  uint64_t mask = 0;
+  int64_t cap = 0;
+  int64_t* slot_keys = nullptr;
+  int64_t slot_cap = 0;
+  int32_t nslots = 0;
+  void reserve(int64_t total_slots, hipStream_t s);
+  void release();
+};
+
+// FilterProcessor over rows [0, n) of one stream; writes matching row indices (ascending), returns the count.
+int64_t filter_rows(const NfaStream* st_dev, int64_t n, const Instr* code, int len, const DVal* consts,
+                    int64_t* out_rows, Scratch& sc, hipStream_t s);
+void project_rows(const NfaStream* st_dev, const int64_t* rows, int64_t nm, const int64_t* row_pos,
+                  const int64_t* ev_ts, int64_t ordinal_base, const char* blob_dev, int32_t query_order, char* out,
+                  uint32_t stride, hipStream_t s);
+int64_t select_records(const int32_t* ev_stream, int64_t n, uint64_t stream_mask, bool with_start, int64_t* out_pos,
+                       Scratch& sc, hipStream_t s);
+int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* ev_stream, const int64_t* ev_row,
+                     const NfaStream* streams_dev, const KeyProg* progs_dev, int nprogs, int64_t** key_pos_out,
+                     int64_t** key_off_out, Scratch& sc, hipStream_t s);
+
+}  // namespace sm

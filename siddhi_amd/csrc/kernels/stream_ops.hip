@@ -1,0 +1,550 @@
+// Column-scan kernels for gfx950:
+//   * filter (FilterProcessor.process, core/query/processor/filter/FilterProcessor.java:50-62) as a two-pass
+//     ordered stream compaction: pass 1 evaluates the predicate per row and keeps one wave64 ballot word per
+//     64 rows plus a per-block count; an exclusive scan of the counts gives each block its output offset;
+//     pass 2 expands the ballot words into row indices (popcount prefix within the word).
+//   * projection of matched rows (QuerySelector.processNoGroupBy :124-167) into output records
+//   * partition-key evaluation (ValuePartitionExecutor.execute :34-40) and the device key table
+//     (PartitionRuntime.cloneIfNotExist :256 — key → per-key state slot)
+#include "expr.h"
+#include "nfa.h"
+#include "stream_ops.h"
+
+namespace sm {
+
+namespace {
+
+constexpr int kFThreads = 256;
+constexpr int kFIters = 8;  // 64-row groups per wave → tile = 256 threads × 8 = 2048 rows per block
+
+struct ColLoader {
+  const NfaStream* st;
+  int64_t row;
+  __device__ StackVal var(const Instr& in) const {
+    StackVal v;
+    v.i = 0;
+    v.d = 0;
+    v.null = 0;
+    int a = in.a;
+    if (st->nulls[a] && st->nulls[a][row]) {
+      v.null = 1;
+      return v;
+    }
+    switch (st->types[a]) {
+      case T_INT: v.i = ((const int32_t*)st->cols[a])[row]; break;
+      case T_LONG: v.i = ((const int64_t*)st->cols[a])[row]; break;
+      case T_FLOAT: v.d = (double)((const float*)st->cols[a])[row]; break;
+      case T_DOUBLE: v.d = ((const double*)st->cols[a])[row]; break;
+      case T_STRING: v.i = ((const int32_t*)st->cols[a])[row]; v.null = v.i < 0; break;
+      default: v.i = ((const uint8_t*)st->cols[a])[row]; break;
+    }
+    return v;
+  }
+};
+
+__global__ __launch_bounds__(kFThreads) void filter_mask_kernel(const NfaStream* __restrict__ st, int64_t n,
+                                                                const Instr* __restrict__ code, int len,
+                                                                const DVal* __restrict__ consts,
+                                                                uint64_t* __restrict__ masks,
+                                                                uint32_t* __restrict__ block_counts) {
+  __shared__ uint32_t wsum[kFThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kFThreads * kFIters;
+  uint32_t cnt = 0;
+  for (int it = 0; it < kFIters; ++it) {
+    int64_t group = (tile >> 6) + (int64_t)it * (kFThreads / 64) + w;  // 64-row group index
+    int64_t row = group * 64 + lane;
+    bool pass = false;
+    if (row < n) {
+      if (len == 0) pass = true;
+      else {
+        ColLoader ld{st, row};
+        pass = truthy(eval_prog(code, len, consts, ld));
+      }
+    }
+    uint64_t m = __ballot(pass);
+    if (lane == 0 && group * 64 < n) masks[group] = m;
+    cnt += (uint32_t)__popcll(m);
+  }
+  if (lane == 0) wsum[w] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int k = 0; k < kFThreads / 64; ++k) s += wsum[k];
+    block_counts[blockIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(kFThreads) void filter_write_kernel(const uint64_t* __restrict__ masks, int64_t n,
+                                                                 const uint32_t* __restrict__ block_offsets,
+                                                                 int64_t* __restrict__ out_rows) {
+  __shared__ uint32_t wbase[kFThreads / 64][kFIters];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kFThreads * kFIters;
+  // per-(iteration, wave) popcounts in group order: group = it * 4 + w
+  for (int it = 0; it < kFIters; ++it) {
+    int64_t group = (tile >> 6) + (int64_t)it * (kFThreads / 64) + w;
+    uint64_t m = (group * 64 < n) ? masks[group] : 0ull;
+    if (lane == 0) wbase[w][it] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = block_offsets[blockIdx.x];
+    for (int it = 0; it < kFIters; ++it)
+      for (int k = 0; k < kFThreads / 64; ++k) {
+        uint32_t c = wbase[k][it];
+        wbase[k][it] = acc;
+        acc += c;
+      }
+  }
+  __syncthreads();
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int it = 0; it < kFIters; ++it) {
+    int64_t group = (tile >> 6) + (int64_t)it * (kFThreads / 64) + w;
+    if (group * 64 >= n) break;
+    uint64_t m = masks[group];
+    if ((m >> lane) & 1ull) out_rows[wbase[w][it] + __popcll(m & lt)] = group * 64 + lane;
+  }
+}
+
+__global__ void project_kernel(const NfaStream* __restrict__ st, const int64_t* __restrict__ rows, int64_t nm,
+                               const int64_t* __restrict__ row_pos, const int64_t* __restrict__ ev_ts,
+                               int64_t ordinal_base, const char* __restrict__ blob, int32_t query_order, char* out,
+                               uint32_t stride) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nm) return;
+  const DQuery* q = (const DQuery*)blob;
+  const Instr* code = (const Instr*)(blob + q->off_code);
+  const DVal* consts = (const DVal*)(blob + q->off_const);
+  const int32_t* sel = (const int32_t*)(blob + q->off_sel);
+  int64_t row = rows[i];
+  int64_t p = row_pos[row];
+  OutRec* o = (OutRec*)(out + (size_t)i * stride);
+  o->pos = p;
+  o->time = 0;
+  o->create = -1;
+  o->ts = ev_ts[p];
+  o->phase = 1;
+  o->query = query_order;
+  o->sched = -1;
+  o->seq = 0;
+  o->key = 0;
+  DVal* vals = (DVal*)((char*)o + sizeof(OutRec));
+  ColLoader ld{st, row};
+  for (int k = 0; k < q->nsel; ++k) {
+    StackVal v = eval_prog(code + sel[3 * k], sel[3 * k + 1], consts, ld);
+    if (sel[3 * k + 2] == T_FLOAT || sel[3 * k + 2] == T_DOUBLE) vals[k].d = v.d;
+    else vals[k].i = v.i;
+    vals[k].null = v.null;
+    vals[k].pad = 0;
+  }
+  int64_t* rf = (int64_t*)(vals + q->nsel);
+  for (int k = 0; k < q->nrefs; ++k) rf[k] = ordinal_base + p;
+}
+
+// records of the query's streams (+ START markers when `with_start`), as positions
+__global__ void select_records_kernel(const int32_t* __restrict__ ev_stream, int64_t n, uint32_t stream_mask_lo,
+                                      uint32_t stream_mask_hi, int with_start, uint8_t* __restrict__ flag) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int s = ev_stream[i];
+  bool f;
+  if (s == NFA_START) f = with_start;
+  else if (s < 0) f = false;
+  else f = (s < 32) ? ((stream_mask_lo >> s) & 1u) : ((stream_mask_hi >> (s - 32)) & 1u);
+  flag[i] = f;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+// partition key per selected record; invalid (null key / other stream) → valid = 0
+__global__ void key_eval_kernel(const int64_t* __restrict__ pos, int64_t n, const int32_t* __restrict__ ev_stream,
+                                const int64_t* __restrict__ ev_row, const NfaStream* __restrict__ streams,
+                                const KeyProg* __restrict__ progs, int nprogs, int64_t* __restrict__ keys,
+                                uint8_t* __restrict__ valid) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t p = pos[i];
+  int s = ev_stream[p];
+  keys[i] = 0;
+  valid[i] = 0;
+  for (int k = 0; k < nprogs; ++k) {
+    if (progs[k].stream != s) continue;
+    ColLoader ld{&streams[s], ev_row[p]};
+    StackVal v = eval_prog(progs[k].code, progs[k].len, progs[k].consts, ld);
+    if (v.null) return;
+    int64_t key;
+    if (progs[k].type == T_FLOAT || progs[k].type == T_DOUBLE) {
+      double d = v.d;
+      if (d != d) d = __longlong_as_double(0x7ff8000000000000ll);  // String.valueOf(NaN) == "NaN" for every NaN
+      key = __double_as_longlong(d);
+    } else {
+      key = v.i;
+    }
+    keys[i] = key;
+    valid[i] = 1;
+    return;
+  }
+}
+
+__global__ void table_lookup_kernel(const int64_t* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t n,
+                                    const int64_t* __restrict__ tkeys, const int32_t* __restrict__ tslots,
+                                    uint64_t mask, int32_t* __restrict__ slot_out, uint32_t* __restrict__ nmissing) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (valid && !valid[i]) {
+    slot_out[i] = -2;
+    return;
+  }
+  int64_t k = keys[i];
+  uint64_t h = mix64((uint64_t)k) & mask;
+  for (;;) {
+    int32_t s = tslots[h];
+    if (s == 0) {
+      slot_out[i] = -1;
+      atomicAdd(nmissing, 1u);
+      return;
+    }
+    if (tkeys[h] == k) {
+      slot_out[i] = s - 1;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__global__ void table_insert_kernel(const int64_t* __restrict__ keys, const int32_t* __restrict__ slots, int64_t n,
+                                    int64_t* __restrict__ tkeys, int32_t* __restrict__ tslots, uint64_t mask) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t k = keys[i];
+  uint64_t h = mix64((uint64_t)k) & mask;
+  for (;;) {
+    if (atomicCAS(&tslots[h], 0, slots[i] + 1) == 0) {
+      tkeys[h] = k;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__global__ void minmax_kernel(const int64_t* __restrict__ keys, int64_t n, unsigned long long* __restrict__ mm) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // order-preserving map int64 → uint64
+  uint64_t lo = ~0ull, hi = 0;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t u = (uint64_t)keys[i] ^ 0x8000000000000000ull;
+    lo = u < lo ? u : lo;
+    hi = u > hi ? u : hi;
+  }
+  atomicMin(&mm[0], (unsigned long long)lo);
+  atomicMax(&mm[1], (unsigned long long)hi);
+}
+
+__global__ void rebase_keys_kernel(const int64_t* __restrict__ keys, int64_t n, uint64_t lo, uint64_t* __restrict__ out,
+                                   uint32_t* __restrict__ idx) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = ((uint64_t)keys[i] ^ 0x8000000000000000ull) - lo;
+  idx[i] = (uint32_t)i;
+}
+
+// after sorting (rebased key, idx): run starts get a new slot id; every entry learns its run's slot
+__global__ void run_start_kernel(const uint64_t* __restrict__ sk, int64_t n, uint32_t* __restrict__ flag) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  flag[i] = (i == 0 || sk[i] != sk[i - 1]) ? 1u : 0u;
+}
+
+__global__ void assign_new_slots_kernel(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sidx,
+                                        const uint32_t* __restrict__ run_excl, int64_t n, int32_t base,
+                                        const int64_t* __restrict__ keys_of_missing,
+                                        const uint32_t* __restrict__ missing_map, int32_t* __restrict__ slot_out,
+                                        int64_t* __restrict__ new_keys, int32_t* __restrict__ new_slots,
+                                        int64_t* __restrict__ slot_keys) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool start = (i == 0 || sk[i] != sk[i - 1]);
+  uint32_t run = run_excl[i] + (start ? 1u : 0u) - 1u;  // inclusive count - 1
+  int32_t slot = base + (int32_t)run;
+  uint32_t m = sidx[i];  // index into the missing list
+  slot_out[missing_map[m]] = slot;
+  if (start) {
+    new_keys[run] = keys_of_missing[m];
+    new_slots[run] = slot;
+    slot_keys[slot] = keys_of_missing[m];
+  }
+}
+
+template <typename T>
+__global__ void compact_flag_kernel(const uint8_t* __restrict__ flag, const uint32_t* __restrict__ excl, int64_t n,
+                                    T* __restrict__ out_idx) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (flag[i]) out_idx[excl[i]] = (T)i;
+}
+
+__global__ void u8_to_u32_kernel(const uint8_t* __restrict__ f, int64_t n, uint32_t* __restrict__ o) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) o[i] = f[i];
+}
+
+__global__ void missing_flags_kernel(const int32_t* __restrict__ slot, int64_t n, uint8_t* __restrict__ f) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = slot[i] == -1;
+}
+
+__global__ void gather_i64_kernel(const int64_t* __restrict__ src, const uint32_t* __restrict__ idx, int64_t n,
+                                  int64_t* __restrict__ dst) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+
+__global__ void slot_to_u32_kernel(const int32_t* __restrict__ slot, int64_t n, uint32_t* __restrict__ key,
+                                   uint32_t* __restrict__ idx) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    key[i] = (uint32_t)slot[i];
+    idx[i] = (uint32_t)i;
+  }
+}
+
+__global__ void count_slots_kernel(const uint32_t* __restrict__ sorted_slot, int64_t n, uint32_t* __restrict__ counts) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&counts[sorted_slot[i]], 1u);
+}
+
+__global__ void u32_to_i64_kernel(const uint32_t* __restrict__ a, int64_t n, int64_t* __restrict__ o) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) o[i] = a[i];
+}
+
+__global__ void count_valid_slots_kernel(const uint32_t* __restrict__ sk, int64_t n, uint32_t nslots,
+                                         uint32_t* __restrict__ counts) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && sk[i] < nslots) atomicAdd(&counts[sk[i]], 1u);
+}
+
+__global__ void gather_pos_kernel(const int64_t* __restrict__ pos, const uint32_t* __restrict__ si, int64_t n,
+                                  int64_t* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = pos[si[i]];
+}
+
+__global__ void rehash_kernel(const int64_t* __restrict__ slot_keys, int64_t nslots, int64_t* __restrict__ tkeys,
+                              int32_t* __restrict__ tslots, uint64_t mask) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots) return;
+  int64_t k = slot_keys[i];
+  uint64_t h = mix64((uint64_t)k) & mask;
+  for (;;) {
+    if (atomicCAS(&tslots[h], 0, (int32_t)i + 1) == 0) {
+      tkeys[h] = k;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+inline dim3 grid_for(int64_t n, int t = 256) { return dim3((unsigned)((n + t - 1) / t)); }
+
+}  // namespace
+
+void KeyTable::release() {
+  if (tkeys) (void)hipFree(tkeys);
+  if (tslots) (void)hipFree(tslots);
+  if (slot_keys) (void)hipFree(slot_keys);
+  tkeys = nullptr;
+  tslots = nullptr;
+  slot_keys = nullptr;
+  cap = 0;
+  slot_cap = 0;
+  nslots = 0;
+}
+
+void KeyTable::reserve(int64_t total, hipStream_t s) {
+  if (total > INT32_MAX - 1) throw std::runtime_error("too many partition keys");
+  if (total > slot_cap) {
+    int64_t nc = std::max<int64_t>(1024, slot_cap);
+    while (nc < total) nc *= 2;
+    int64_t* nk = nullptr;
+    SM_HIP(hipMalloc(&nk, nc * 8));
+    if (slot_keys && nslots) SM_HIP(hipMemcpyAsync(nk, slot_keys, (size_t)nslots * 8, hipMemcpyDeviceToDevice, s));
+    SM_HIP(hipStreamSynchronize(s));
+    if (slot_keys) SM_HIP(hipFree(slot_keys));
+    slot_keys = nk;
+    slot_cap = nc;
+  }
+  if (total * 2 > cap) {
+    int64_t nc = std::max<int64_t>(2048, cap);
+    while (nc < total * 2) nc *= 2;
+    if (tkeys) SM_HIP(hipFree(tkeys));
+    if (tslots) SM_HIP(hipFree(tslots));
+    SM_HIP(hipMalloc(&tkeys, nc * 8));
+    SM_HIP(hipMalloc(&tslots, nc * 4));
+    SM_HIP(hipMemsetAsync(tslots, 0, nc * 4, s));
+    cap = nc;
+    mask = (uint64_t)nc - 1;
+    if (nslots > 0)
+      hipLaunchKernelGGL(rehash_kernel, grid_for(nslots), dim3(256), 0, s, slot_keys, (int64_t)nslots, tkeys, tslots,
+                         mask);
+  }
+}
+
+int64_t filter_rows(const NfaStream* st_dev, int64_t n, const Instr* code, int len, const DVal* consts,
+                    int64_t* out_rows, Scratch& sc, hipStream_t s) {
+  if (n == 0) return 0;
+  size_t mark = sc.used;
+  int64_t ngroups = (n + 63) / 64;
+  int64_t tile = (int64_t)kFThreads * kFIters;
+  int64_t nblocks = (n + tile - 1) / tile;
+  uint64_t* masks = (uint64_t*)sc.take(ngroups * 8);
+  uint32_t* counts = (uint32_t*)sc.take((nblocks + 1) * 4);
+  uint32_t* total = (uint32_t*)sc.take(4);
+  hipLaunchKernelGGL(filter_mask_kernel, dim3((unsigned)nblocks), dim3(kFThreads), 0, s, st_dev, n, code, len, consts,
+                     masks, counts);
+  exclusive_scan_u32(counts, nblocks, sc, s, total);
+  hipLaunchKernelGGL(filter_write_kernel, dim3((unsigned)nblocks), dim3(kFThreads), 0, s, masks, n, counts, out_rows);
+  uint32_t h = 0;
+  SM_HIP(hipMemcpyAsync(&h, total, 4, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+  return h;
+}
+
+void project_rows(const NfaStream* st_dev, const int64_t* rows, int64_t nm, const int64_t* row_pos,
+                  const int64_t* ev_ts, int64_t ordinal_base, const char* blob_dev, int32_t query_order, char* out,
+                  uint32_t stride, hipStream_t s) {
+  if (nm == 0) return;
+  hipLaunchKernelGGL(project_kernel, grid_for(nm), dim3(256), 0, s, st_dev, rows, nm, row_pos, ev_ts, ordinal_base,
+                     blob_dev, query_order, out, stride);
+}
+
+int64_t select_records(const int32_t* ev_stream, int64_t n, uint64_t stream_mask, bool with_start, int64_t* out_pos,
+                       Scratch& sc, hipStream_t s) {
+  if (n == 0) return 0;
+  size_t mark = sc.used;
+  uint8_t* flag = (uint8_t*)sc.take(n);
+  uint32_t* ex = (uint32_t*)sc.take(n * 4);
+  uint32_t* total = (uint32_t*)sc.take(4);
+  hipLaunchKernelGGL(select_records_kernel, grid_for(n), dim3(256), 0, s, ev_stream, n, (uint32_t)stream_mask,
+                     (uint32_t)(stream_mask >> 32), (int)with_start, flag);
+  hipLaunchKernelGGL(u8_to_u32_kernel, grid_for(n), dim3(256), 0, s, flag, n, ex);
+  exclusive_scan_u32(ex, n, sc, s, total);
+  hipLaunchKernelGGL(compact_flag_kernel<int64_t>, grid_for(n), dim3(256), 0, s, flag, ex, n, out_pos);
+  uint32_t h = 0;
+  SM_HIP(hipMemcpyAsync(&h, total, 4, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+  return h;
+}
+
+// Group a query's records by partition key. Returns the number of valid records; key_pos / key_off (CSR over
+// all `*nslots` slots) are written into buffers from `sc` (valid until the caller releases the scratch).
+int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* ev_stream, const int64_t* ev_row,
+                     const NfaStream* streams_dev, const KeyProg* progs_dev, int nprogs, int64_t** key_pos_out,
+                     int64_t** key_off_out, Scratch& sc, hipStream_t s) {
+  int64_t* keys = (int64_t*)sc.take(std::max<int64_t>(n, 1) * 8);
+  uint8_t* valid = (uint8_t*)sc.take(std::max<int64_t>(n, 1));
+  int32_t* slot = (int32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
+  uint32_t* nmiss = (uint32_t*)sc.take(4);
+  if (n > 0)
+    hipLaunchKernelGGL(key_eval_kernel, grid_for(n), dim3(256), 0, s, pos, n, ev_stream, ev_row, streams_dev, progs_dev,
+                       nprogs, keys, valid);
+  SM_HIP(hipMemsetAsync(nmiss, 0, 4, s));
+  if (n > 0)
+    hipLaunchKernelGGL(table_lookup_kernel, grid_for(n), dim3(256), 0, s, keys, valid, n, T.tkeys, T.tslots, T.mask,
+                       slot, nmiss);
+  uint32_t hm = 0;
+  SM_HIP(hipMemcpyAsync(&hm, nmiss, 4, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  if (hm > 0) {
+    // new keys: compact, sort by key (stable → first occurrence first), one new slot per distinct key
+    size_t mark = sc.used;
+    uint8_t* f = (uint8_t*)sc.take(n);
+    uint32_t* ex = (uint32_t*)sc.take(n * 4);
+    hipLaunchKernelGGL(missing_flags_kernel, grid_for(n), dim3(256), 0, s, slot, n, f);
+    hipLaunchKernelGGL(u8_to_u32_kernel, grid_for(n), dim3(256), 0, s, f, n, ex);
+    exclusive_scan_u32(ex, n, sc, s);
+    uint32_t* miss = (uint32_t*)sc.take(hm * 4);
+    hipLaunchKernelGGL(compact_flag_kernel<uint32_t>, grid_for(n), dim3(256), 0, s, f, ex, n, miss);
+    int64_t* mkeys = (int64_t*)sc.take(hm * 8);
+    hipLaunchKernelGGL(gather_i64_kernel, grid_for(hm), dim3(256), 0, s, keys, miss, (int64_t)hm, mkeys);
+    unsigned long long* mm = (unsigned long long*)sc.take(16);
+    unsigned long long init[2] = {~0ull, 0ull};
+    SM_HIP(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(minmax_kernel, dim3(std::min<int64_t>(1024, (hm + 255) / 256)), dim3(256), 0, s, mkeys,
+                       (int64_t)hm, mm);
+    unsigned long long hmm[2];
+    SM_HIP(hipMemcpyAsync(hmm, mm, 16, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    uint64_t span = hmm[1] - hmm[0];
+    int bits = 0;
+    while (bits < 64 && (span >> bits) != 0) ++bits;
+    uint64_t* sk = (uint64_t*)sc.take(hm * 8);
+    uint64_t* sk2 = (uint64_t*)sc.take(hm * 8);
+    uint32_t* si = (uint32_t*)sc.take(hm * 4);
+    uint32_t* si2 = (uint32_t*)sc.take(hm * 4);
+    hipLaunchKernelGGL(rebase_keys_kernel, grid_for(hm), dim3(256), 0, s, mkeys, (int64_t)hm, (uint64_t)hmm[0], sk, si);
+    bool alt = radix_sort_pairs<uint64_t>(sk, sk2, si, si2, hm, 0, bits, sc, s);
+    if (alt) {
+      std::swap(sk, sk2);
+      std::swap(si, si2);
+    }
+    uint32_t* runs = (uint32_t*)sc.take(hm * 4);
+    uint32_t* nruns = (uint32_t*)sc.take(4);
+    hipLaunchKernelGGL(run_start_kernel, grid_for(hm), dim3(256), 0, s, sk, (int64_t)hm, runs);
+    exclusive_scan_u32(runs, hm, sc, s, nruns);
+    uint32_t hr = 0;
+    SM_HIP(hipMemcpyAsync(&hr, nruns, 4, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    T.reserve((int64_t)T.nslots + hr, s);
+    int64_t* nk = (int64_t*)sc.take(hr * 8);
+    int32_t* ns = (int32_t*)sc.take(hr * 4);
+    hipLaunchKernelGGL(assign_new_slots_kernel, grid_for(hm), dim3(256), 0, s, sk, si, runs, (int64_t)hm, T.nslots,
+                       mkeys, miss, slot, nk, ns, T.slot_keys);
+    hipLaunchKernelGGL(table_insert_kernel, grid_for(hr), dim3(256), 0, s, nk, ns, (int64_t)hr, T.tkeys, T.tslots,
+                       T.mask);
+    T.nslots += hr;
+    sc.used = mark;
+  }
+  // stable group by slot: sort (slot, record index) pairs; invalid records (-2) sort last and are dropped
+  uint32_t* sk = (uint32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
+  uint32_t* sk2 = (uint32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
+  uint32_t* si = (uint32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
+  uint32_t* si2 = (uint32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
+  if (n > 0) hipLaunchKernelGGL(slot_to_u32_kernel, grid_for(n), dim3(256), 0, s, slot, n, sk, si);
+  int bits = 0;
+  while (bits < 32 && ((uint64_t)0xffffffffu >> bits) != 0 && (((uint64_t)T.nslots + 1) >> bits) != 0) ++bits;
+  bits = 32;  // -2 (invalid) maps to 0xfffffffe: keep all 32 bits so invalid records sort last
+  bool alt = radix_sort_pairs<uint32_t>(sk, sk2, si, si2, n, 0, bits, sc, s);
+  if (alt) {
+    std::swap(sk, sk2);
+    std::swap(si, si2);
+  }
+  int64_t* key_off = (int64_t*)sc.take(((int64_t)T.nslots + 2) * 8);
+  uint32_t* counts = (uint32_t*)sc.take(((int64_t)T.nslots + 2) * 4);
+  uint32_t* total = (uint32_t*)sc.take(4);
+  SM_HIP(hipMemsetAsync(counts, 0, ((int64_t)T.nslots + 2) * 4, s));
+  if (n > 0) hipLaunchKernelGGL(count_valid_slots_kernel, grid_for(n), dim3(256), 0, s, sk, n, (uint32_t)T.nslots, counts);
+  exclusive_scan_u32(counts, (int64_t)T.nslots + 1, sc, s, total);
+  hipLaunchKernelGGL(u32_to_i64_kernel, grid_for((int64_t)T.nslots + 1), dim3(256), 0, s, counts,
+                     (int64_t)T.nslots + 1, key_off);
+  uint32_t hv = 0;
+  SM_HIP(hipMemcpyAsync(&hv, total, 4, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  int64_t* key_pos = (int64_t*)sc.take(std::max<int64_t>(hv, 1) * 8);
+  if (hv > 0) hipLaunchKernelGGL(gather_pos_kernel, grid_for(hv), dim3(256), 0, s, pos, si, (int64_t)hv, key_pos);
+  *key_pos_out = key_pos;
+  *key_off_out = key_off;
+  return hv;
+}
+
+}  // namespace sm

@@ -1,0 +1,925 @@
+// Host runtime + C ABI (include/siddhi_amd.h): SiddhiManager / SiddhiAppRuntime / InputHandler /
+// callbacks restated over a batched device pipeline.
+//
+// send() stages events into per-stream host columns (the StreamJunction.sendData path,
+// core/stream/StreamJunction.java:232); flush() uploads the batch once and runs every query on the GPU:
+//   single-stream queries  → filter scan + projection kernels (stream_ops.hip)
+//   pattern / sequence     → key grouping (stream_ops.hip) + NFA interpreter (nfa.hip)
+// Outputs of all queries are ordered as the reference emits them (trigger position, timer phase, listener
+// order, query order, emission order) and delivered to StreamCallback / QueryCallback on the calling thread.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/siddhi_amd.h"
+#include "compiler.h"
+#include "kernels/fastpath.h"
+#include "kernels/nfa.h"
+#include "kernels/primitives.h"
+#include "kernels/stream_ops.h"
+#include "siddhiql/ast.h"
+
+namespace sm {
+namespace {
+
+thread_local std::string g_err;
+
+struct DeviceError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct TypeError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+int width_of(int t) {
+  switch (t) {
+    case T_INT: return 4;
+    case T_LONG: return 8;
+    case T_FLOAT: return 4;
+    case T_DOUBLE: return 8;
+    case T_STRING: return 4;
+    default: return 1;
+  }
+}
+
+// growable device buffer
+struct DBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void* ensure(size_t bytes) {
+    if (bytes > cap) {
+      if (p) SM_HIP(hipFree(p));
+      size_t c = std::max<size_t>(bytes, cap * 2);
+      c = std::max<size_t>(c, 256);
+      SM_HIP(hipMalloc(&p, c));
+      cap = c;
+    }
+    return p;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  ~DBuf() { release(); }
+};
+
+struct StreamStage {
+  const sql::StreamDef* def;
+  std::vector<std::vector<uint8_t>> cols;
+  std::vector<std::vector<uint8_t>> nulls;
+  std::vector<bool> any_null;
+  std::vector<int64_t> row_pos;
+  int64_t rows = 0;
+  // device copies for the current flush
+  std::vector<DBuf> dcols, dnulls;
+  DBuf drow_pos;
+  void clear() {
+    for (auto& c : cols) c.clear();
+    for (auto& c : nulls) c.clear();
+    std::fill(any_null.begin(), any_null.end(), false);
+    row_pos.clear();
+    rows = 0;
+  }
+};
+
+struct HostOut {
+  OutRec r;
+  std::vector<DVal> vals;
+  std::vector<int64_t> refs;
+  int qidx;
+};
+
+struct Callback {
+  sm_stream_callback scb = nullptr;
+  sm_query_callback qcb = nullptr;
+  void* user = nullptr;
+};
+
+struct QueryRt {
+  CompiledQuery cq;
+  DBuf blob;
+  // state queries
+  KeyTable keys;
+  DBuf ks, heap;
+  int64_t state_slots = 0;  // slots with allocated per-key state
+  DBuf out;
+  DBuf keyprogs;             // KeyProg array (device)
+  std::vector<DBuf> keycode; // code / consts backing the key programs
+  int nkeyprogs = 0;
+  const CompiledPartition* part = nullptr;
+  // device batch results
+  DBuf dev_pairs;
+  int64_t dev_n = 0;
+};
+
+}  // namespace
+}  // namespace sm
+
+struct sm_manager {
+  int dummy = 0;
+};
+
+struct sm_input {
+  struct sm_app* app;
+  int stream;
+};
+
+struct sm_app {
+  std::mutex mu;
+  sql::App ast;
+  sm::Dict dict;
+  std::vector<sm::StreamStage> streams;
+  std::vector<std::unique_ptr<sm::QueryRt>> queries;  // app order
+  std::vector<sm::CompiledPartition> parts;
+  std::vector<std::unique_ptr<sm_input>> inputs;
+  std::map<std::string, std::vector<sm::Callback>> stream_cbs, query_cbs;
+  // batch staging
+  std::vector<int32_t> ev_stream;
+  std::vector<int64_t> ev_row, ev_ts, ev_clock;
+  std::vector<int64_t> adv_pos, adv_clock, adv_wall;
+  int64_t ordinal_base = 0;
+  int64_t clock = 0;          // playback clock (EventTimeBasedMillisTimestampGenerator.lastEventTimestamp)
+  int64_t clock_batch_in = 0;
+  bool started = false;
+  bool shut = false;
+  int64_t batch_events = 1 << 20;
+  int32_t heap_half = 1024;
+  bool collect = false;
+  std::map<std::string, std::vector<std::string>> collected_streams;  // JSON fragments
+  std::map<std::string, std::vector<std::string>> collected_queries;
+  hipStream_t stream = nullptr;
+  sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_adv_pos, d_adv_clock, d_adv_wall, d_streams, d_err, d_count,
+      d_keyoff, scratch;
+  sm::Scratch sc;
+};
+
+namespace sm {
+namespace {
+
+void set_error(const std::string& m) { g_err = m; }
+
+int status_of(const std::exception& e) {
+  if (dynamic_cast<const sql::ParseError*>(&e)) return SM_E_PARSE;
+  if (dynamic_cast<const sql::ValidationError*>(&e)) return SM_E_VALIDATION;
+  if (dynamic_cast<const sql::UnsupportedError*>(&e)) return SM_E_UNSUPPORTED;
+  if (dynamic_cast<const TypeError*>(&e)) return SM_E_TYPE;
+  std::string w = e.what();
+  if (w.rfind("HIP error", 0) == 0) return SM_E_DEVICE;
+  return SM_E_RUNTIME;
+}
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return SM_OK;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return status_of(e);
+  }
+}
+
+void ensure_scratch(sm_app* a, size_t bytes) {
+  if (a->sc.cap < bytes || !a->sc.base) {
+    a->scratch.ensure(bytes);
+    a->sc.base = (char*)a->scratch.p;
+    a->sc.cap = a->scratch.cap;
+  }
+  a->sc.used = 0;
+}
+
+void build_app(sm_app* a) {
+  a->streams.resize(a->ast.streams.size());
+  for (size_t i = 0; i < a->ast.streams.size(); ++i) {
+    StreamStage& st = a->streams[i];
+    st.def = &a->ast.streams[i];
+    size_t na = st.def->attrs.size();
+    if (na > (size_t)kMaxAttrs) throw sql::UnsupportedError("stream has too many attributes");
+    st.cols.resize(na);
+    st.nulls.resize(na);
+    st.any_null.assign(na, false);
+    st.dcols.resize(na);
+    st.dnulls.resize(na);
+  }
+  for (auto& p : a->ast.partitions) a->parts.push_back(compile_partition(a->ast, p, a->dict));
+  for (size_t o = 0; o < a->ast.order.size(); ++o) {
+    auto [pi, qi] = a->ast.order[o];
+    const sql::Query& qd = pi < 0 ? a->ast.queries[qi] : a->ast.partitions[pi].queries[qi];
+    auto q = std::make_unique<QueryRt>();
+    q->cq = compile_query(a->ast, qd, (int)o, pi, a->dict);
+    if (pi >= 0) {
+      q->part = &a->parts[pi];
+      for (int s : q->cq.streams)
+        if (std::find(q->part->streams.begin(), q->part->streams.end(), s) == q->part->streams.end())
+          throw sql::UnsupportedError("non-partitioned stream '" + a->ast.streams[s].id +
+                                      "' inside a partition is not supported");
+      if (q->cq.hdr.kind == 0) throw sql::UnsupportedError("single-stream queries inside a partition are not supported");
+    }
+    a->queries.push_back(std::move(q));
+  }
+}
+
+void upload_app(sm_app* a) {
+  SM_HIP(hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking));
+  for (auto& q : a->queries) {
+    q->blob.ensure(q->cq.blob.size());
+    SM_HIP(hipMemcpyAsync(q->blob.p, q->cq.blob.data(), q->cq.blob.size(), hipMemcpyHostToDevice, a->stream));
+    if (q->part) {
+      // key programs of the partition's streams
+      const CompiledPartition& cp = *q->part;
+      std::vector<KeyProg> kps(cp.streams.size());
+      q->keycode.resize(cp.streams.size() * 2);
+      for (size_t k = 0; k < cp.streams.size(); ++k) {
+        size_t cb = std::max<size_t>(cp.key_code[k].size() * sizeof(Instr), 16);
+        size_t kb = std::max<size_t>(cp.key_consts[k].size() * sizeof(DVal), 16);
+        q->keycode[2 * k].ensure(cb);
+        q->keycode[2 * k + 1].ensure(kb);
+        if (!cp.key_code[k].empty())
+          SM_HIP(hipMemcpyAsync(q->keycode[2 * k].p, cp.key_code[k].data(), cp.key_code[k].size() * sizeof(Instr),
+                                hipMemcpyHostToDevice, a->stream));
+        if (!cp.key_consts[k].empty())
+          SM_HIP(hipMemcpyAsync(q->keycode[2 * k + 1].p, cp.key_consts[k].data(),
+                                cp.key_consts[k].size() * sizeof(DVal), hipMemcpyHostToDevice, a->stream));
+        kps[k].stream = cp.streams[k];
+        kps[k].len = (int)cp.key_code[k].size();
+        kps[k].type = cp.key_type[k];
+        kps[k].code = (const Instr*)q->keycode[2 * k].p;
+        kps[k].consts = (const DVal*)q->keycode[2 * k + 1].p;
+      }
+      q->keyprogs.ensure(kps.size() * sizeof(KeyProg));
+      SM_HIP(hipMemcpyAsync(q->keyprogs.p, kps.data(), kps.size() * sizeof(KeyProg), hipMemcpyHostToDevice, a->stream));
+      q->nkeyprogs = (int)kps.size();
+      q->keys.reserve(1, a->stream);
+    }
+  }
+  SM_HIP(hipStreamSynchronize(a->stream));
+}
+
+// ---- JSON (parity dump) in the same shape as the oracle's
+void json_val(std::ostringstream& o, const sm_app* a, const DVal& v, int t) {
+  if (v.null) {
+    o << "null";
+    return;
+  }
+  switch (t) {
+    case T_INT:
+    case T_LONG: o << v.i; break;
+    case T_BOOL: o << (v.i ? "true" : "false"); break;
+    case T_FLOAT:
+    case T_DOUBLE: {
+      if (std::isnan(v.d)) { o << "\"NaN\""; break; }
+      if (std::isinf(v.d)) { o << (v.d > 0 ? "\"Infinity\"" : "\"-Infinity\""); break; }
+      char b[64];
+      auto r = std::to_chars(b, b + 64, v.d);
+      std::string s(b, r.ptr);
+      if (s.find_first_of(".eE") == std::string::npos) s += ".0";
+      o << s;
+      break;
+    }
+    default: {
+      if (v.i < 0 || v.i >= (int64_t)a->dict.strs.size()) {
+        o << "null";
+        break;
+      }
+      o << '"';
+      for (char c : a->dict.strs[v.i]) {
+        if (c == '"' || c == '\\') o << '\\' << c;
+        else if ((unsigned char)c < 0x20) {
+          char b[8];
+          snprintf(b, 8, "\\u%04x", c);
+          o << b;
+        } else o << c;
+      }
+      o << '"';
+    }
+  }
+}
+
+void to_sm_values(const sm_app* a, const HostOut& h, const CompiledQuery& cq, std::vector<sm_value>& out) {
+  out.resize(h.vals.size());
+  for (size_t k = 0; k < h.vals.size(); ++k) {
+    sm_value& v = out[k];
+    int t = cq.sel_types[k];
+    v.type = t;
+    v.is_null = h.vals[k].null;
+    v.i = 0;
+    v.d = 0;
+    v.s = nullptr;
+    if (v.is_null) continue;
+    if (t == T_FLOAT || t == T_DOUBLE) v.d = h.vals[k].d;
+    else if (t == T_STRING) {
+      int64_t id = h.vals[k].i;
+      if (id < 0 || id >= (int64_t)a->dict.strs.size()) v.is_null = 1;
+      else v.s = a->dict.strs[id].c_str();
+    } else v.i = h.vals[k].i;
+  }
+}
+
+void deliver(sm_app* a, std::vector<HostOut>& outs) {
+  std::stable_sort(outs.begin(), outs.end(), [](const HostOut& x, const HostOut& y) {
+    if (x.r.pos != y.r.pos) return x.r.pos < y.r.pos;
+    if (x.r.phase != y.r.phase) return x.r.phase < y.r.phase;
+    if (x.r.phase == 0) {
+      if (x.r.time != y.r.time) return x.r.time < y.r.time;
+      int gx = x.r.create >= 0, gy = y.r.create >= 0;  // non-partitioned listeners registered first
+      if (gx != gy) return gx < gy;
+      if (x.r.create != y.r.create) return x.r.create < y.r.create;
+      if (x.r.query != y.r.query) return x.r.query < y.r.query;
+      if (x.r.sched != y.r.sched) return x.r.sched < y.r.sched;
+      return x.r.seq < y.r.seq;
+    }
+    if (x.r.query != y.r.query) return x.r.query < y.r.query;
+    return x.r.seq < y.r.seq;
+  });
+  std::vector<sm_value> vals;
+  for (auto& h : outs) {
+    const CompiledQuery& cq = a->queries[h.qidx]->cq;
+    to_sm_values(a, h, cq, vals);
+    sm_event ev{h.r.ts, vals.data(), (int32_t)vals.size()};
+    if (a->collect) {
+      std::ostringstream o;
+      o << "[" << h.r.ts << ",[";
+      for (size_t k = 0; k < h.vals.size(); ++k) {
+        if (k) o << ",";
+        json_val(o, a, h.vals[k], cq.sel_types[k]);
+      }
+      o << "],[";
+      for (size_t k = 0; k < h.refs.size(); ++k) {
+        if (k) o << ",";
+        o << h.refs[k];
+      }
+      o << "]]";
+      std::string ev_json = o.str();
+      a->collected_streams[cq.insert_into].push_back(ev_json);
+      if (cq.partition < 0) {
+        std::ostringstream q;
+        q << "[" << h.r.ts << ",[[";
+        for (size_t k = 0; k < h.vals.size(); ++k) {
+          if (k) q << ",";
+          json_val(q, a, h.vals[k], cq.sel_types[k]);
+        }
+        q << "]]]";
+        a->collected_queries[cq.name].push_back(q.str());
+      }
+    }
+    auto it = a->stream_cbs.find(cq.insert_into);
+    if (it != a->stream_cbs.end())
+      for (auto& cb : it->second)
+        if (cb.scb) cb.scb(cb.user, &ev, 1);
+    if (cq.partition < 0) {  // partition clones do not inherit QueryCallbacks (PartitionRuntime)
+      auto qt = a->query_cbs.find(cq.name);
+      if (qt != a->query_cbs.end())
+        for (auto& cb : qt->second)
+          if (cb.qcb) cb.qcb(cb.user, h.r.ts, &ev, 1, nullptr, 0);
+    }
+  }
+}
+
+void read_outputs(sm_app* a, int qidx, const void* dev, int64_t n, std::vector<HostOut>& outs) {
+  if (n <= 0) return;
+  const CompiledQuery& cq = a->queries[qidx]->cq;
+  size_t stride = sizeof(OutRec) + cq.hdr.nsel * sizeof(DVal) + cq.hdr.nrefs * sizeof(int64_t);
+  std::vector<char> host((size_t)n * stride);
+  SM_HIP(hipMemcpyAsync(host.data(), dev, host.size(), hipMemcpyDeviceToHost, a->stream));
+  SM_HIP(hipStreamSynchronize(a->stream));
+  for (int64_t k = 0; k < n; ++k) {
+    const char* b = host.data() + (size_t)k * stride;
+    HostOut h;
+    memcpy(&h.r, b, sizeof(OutRec));
+    h.vals.resize(cq.hdr.nsel);
+    memcpy(h.vals.data(), b + sizeof(OutRec), cq.hdr.nsel * sizeof(DVal));
+    h.refs.resize(cq.hdr.nrefs);
+    memcpy(h.refs.data(), b + sizeof(OutRec) + cq.hdr.nsel * sizeof(DVal), cq.hdr.nrefs * sizeof(int64_t));
+    h.qidx = qidx;
+    outs.push_back(std::move(h));
+  }
+}
+
+void ensure_state(sm_app* a, QueryRt& q, int64_t nkeys) {
+  if (nkeys <= q.state_slots) return;
+  int64_t cap = std::max<int64_t>(nkeys, q.state_slots * 2);
+  cap = std::max<int64_t>(cap, 16);
+  const DQuery& h = q.cq.hdr;
+  size_t ks_bytes = (size_t)cap * h.ks_words * 8;
+  size_t heap_words = 2 * (size_t)a->heap_half + 64;
+  size_t heap_bytes = (size_t)cap * heap_words * 8;
+  void *nks = nullptr, *nheap = nullptr;
+  SM_HIP(hipMalloc(&nks, ks_bytes));
+  SM_HIP(hipMalloc(&nheap, heap_bytes));
+  SM_HIP(hipMemsetAsync(nks, 0, ks_bytes, a->stream));
+  if (q.state_slots > 0) {
+    SM_HIP(hipMemcpyAsync(nks, q.ks.p, (size_t)q.state_slots * h.ks_words * 8, hipMemcpyDeviceToDevice, a->stream));
+    SM_HIP(hipMemcpyAsync(nheap, q.heap.p, (size_t)q.state_slots * heap_words * 8, hipMemcpyDeviceToDevice, a->stream));
+  }
+  SM_HIP(hipStreamSynchronize(a->stream));
+  q.ks.release();
+  q.heap.release();
+  q.ks.p = nks;
+  q.ks.cap = ks_bytes;
+  q.heap.p = nheap;
+  q.heap.cap = heap_bytes;
+  q.state_slots = cap;
+}
+
+template <typename T>
+void upload(sm_app* a, DBuf& d, const std::vector<T>& v) {
+  d.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
+  if (!v.empty()) SM_HIP(hipMemcpyAsync(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, a->stream));
+}
+
+void flush(sm_app* a) {
+  const int64_t N = (int64_t)a->ev_stream.size();
+  if (N == 0) return;
+  // ---- upload the batch
+  std::vector<NfaStream> nst(a->streams.size());
+  for (size_t s = 0; s < a->streams.size(); ++s) {
+    StreamStage& st = a->streams[s];
+    NfaStream& d = nst[s];
+    memset(&d, 0, sizeof(d));
+    d.nattr = (int)st.def->attrs.size();
+    for (int k = 0; k < d.nattr; ++k) {
+      d.types[k] = (int)st.def->attrs[k].type;
+      upload(a, st.dcols[k], st.cols[k]);
+      d.cols[k] = st.dcols[k].p;
+      if (st.any_null[k]) {
+        upload(a, st.dnulls[k], st.nulls[k]);
+        d.nulls[k] = (const uint8_t*)st.dnulls[k].p;
+      }
+    }
+    upload(a, st.drow_pos, st.row_pos);
+  }
+  upload(a, a->d_streams, nst);
+  upload(a, a->d_ev_stream, a->ev_stream);
+  upload(a, a->d_ev_row, a->ev_row);
+  upload(a, a->d_ev_ts, a->ev_ts);
+  upload(a, a->d_ev_clock, a->ev_clock);
+  upload(a, a->d_adv_pos, a->adv_pos);
+  upload(a, a->d_adv_clock, a->adv_clock);
+  upload(a, a->d_adv_wall, a->adv_wall);
+  a->d_err.ensure(16);
+  a->d_count.ensure(16);
+  ensure_scratch(a, (size_t)N * 96 + (64 << 20));
+  std::vector<HostOut> outs;
+  for (size_t qi = 0; qi < a->queries.size(); ++qi) {
+    QueryRt& q = *a->queries[qi];
+    const DQuery& h = q.cq.hdr;
+    a->sc.used = 0;
+    size_t stride = sizeof(OutRec) + h.nsel * sizeof(DVal) + h.nrefs * sizeof(int64_t);
+    if (h.kind == 0) {
+      StreamStage& st = a->streams[h.stream];
+      if (st.rows == 0) continue;
+      const NfaStream* sd = (const NfaStream*)a->d_streams.p + h.stream;
+      int64_t* rows = (int64_t*)a->sc.take(st.rows * 8);
+      const char* blob = (const char*)q.blob.p;
+      const DQuery* hd = &h;
+      int64_t nm = filter_rows(sd, st.rows, (const Instr*)(blob + hd->off_code) + h.filt_off, h.filt_len,
+                               (const DVal*)(blob + hd->off_const), rows, a->sc, a->stream);
+      q.out.ensure(std::max<size_t>((size_t)nm * stride, 16));
+      project_rows(sd, rows, nm, (const int64_t*)st.drow_pos.p, (const int64_t*)a->d_ev_ts.p, a->ordinal_base, blob,
+                   h.query_order, (char*)q.out.p, (uint32_t)stride, a->stream);
+      read_outputs(a, (int)qi, q.out.p, nm, outs);
+      continue;
+    }
+    // ---- pattern / sequence query
+    uint64_t mask = 0;
+    for (int s : q.cq.streams) mask |= (1ull << s);
+    bool partitioned = h.partitioned;
+    int64_t* pos = (int64_t*)a->sc.take(N * 8);
+    int64_t nq = select_records((const int32_t*)a->d_ev_stream.p, N, mask, !partitioned, pos, a->sc, a->stream);
+    int64_t* key_pos = pos;
+    int64_t* key_off = nullptr;
+    int64_t nkeys = 1;
+    if (partitioned) {
+      int64_t nv = group_by_key(q.keys, pos, nq, (const int32_t*)a->d_ev_stream.p, (const int64_t*)a->d_ev_row.p,
+                                (const NfaStream*)a->d_streams.p, (const KeyProg*)q.keyprogs.p, q.nkeyprogs, &key_pos,
+                                &key_off, a->sc, a->stream);
+      nq = nv;
+      nkeys = q.keys.nslots;
+    } else {
+      key_off = (int64_t*)a->sc.take(16);
+      int64_t ho[2] = {0, nq};
+      SM_HIP(hipMemcpyAsync(key_off, ho, 16, hipMemcpyHostToDevice, a->stream));
+    }
+    if (nkeys == 0) continue;
+    ensure_state(a, q, nkeys);
+    int64_t cap = std::max<int64_t>(4096, 8 * nq + 1024);
+    q.out.ensure((size_t)cap * stride);
+    NfaBatch b{};
+    b.ev_stream = (const int32_t*)a->d_ev_stream.p;
+    b.ev_row = (const int64_t*)a->d_ev_row.p;
+    b.ev_ts = (const int64_t*)a->d_ev_ts.p;
+    b.ev_clock = (const int64_t*)a->d_ev_clock.p;
+    b.ordinal_base = a->ordinal_base;
+    b.streams = (const NfaStream*)a->d_streams.p;
+    b.adv_pos = (const int64_t*)a->d_adv_pos.p;
+    b.adv_clock = (const int64_t*)a->d_adv_clock.p;
+    b.adv_wall = (const int64_t*)a->d_adv_wall.p;
+    b.nadv = (int64_t)a->adv_pos.size();
+    b.clock_in = a->clock_batch_in;
+    b.key_off = key_off;
+    b.key_pos = key_pos;
+    b.create_all = !partitioned;
+    b.out = q.out.p;
+    b.out_count = (uint32_t*)a->d_count.p;
+    b.out_cap = (uint32_t)cap;
+    b.out_stride = (uint32_t)stride;
+    SM_HIP(hipMemsetAsync(a->d_count.p, 0, 4, a->stream));
+    SM_HIP(hipMemsetAsync(a->d_err.p, 0, 4, a->stream));
+    launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, (int32_t)nkeys,
+               (int32_t*)a->d_err.p, a->stream);
+    SM_HIP(hipGetLastError());
+    uint32_t hc = 0;
+    int32_t he = 0;
+    SM_HIP(hipMemcpyAsync(&hc, a->d_count.p, 4, hipMemcpyDeviceToHost, a->stream));
+    SM_HIP(hipMemcpyAsync(&he, a->d_err.p, 4, hipMemcpyDeviceToHost, a->stream));
+    SM_HIP(hipStreamSynchronize(a->stream));
+    if (he) {
+      std::string why;
+      if (he & NFA_ERR_ARENA) why += " per-key partial-match arena exhausted (raise option heap_words);";
+      if (he & NFA_ERR_TIMERS) why += " timer queue full;";
+      if (he & NFA_ERR_OUTPUT) why += " output buffer full;";
+      if (he & NFA_ERR_NPE) why += " NullPointerException/IllegalStateException path of the reference;";
+      throw std::runtime_error("query '" + q.cq.name + "':" + why);
+    }
+    read_outputs(a, (int)qi, q.out.p, std::min<int64_t>(hc, cap), outs);
+  }
+  // ---- batch done
+  a->ordinal_base += N;
+  a->clock_batch_in = a->clock;
+  a->ev_stream.clear();
+  a->ev_row.clear();
+  a->ev_ts.clear();
+  a->ev_clock.clear();
+  a->adv_pos.clear();
+  a->adv_clock.clear();
+  a->adv_wall.clear();
+  for (auto& st : a->streams) st.clear();
+  deliver(a, outs);
+}
+
+// StreamJunction.sendData :232-237: the playback clock advances (and listeners fire) only when ts >= clock
+void stage_record(sm_app* a, int32_t stream, int64_t row, int64_t ts, int wall) {
+  int64_t p = (int64_t)a->ev_stream.size();
+  a->ev_stream.push_back(stream);
+  a->ev_row.push_back(row);
+  a->ev_ts.push_back(ts);
+  if (a->ast.playback && stream != NFA_START) {
+    if (ts >= a->clock) {
+      a->clock = ts;
+      a->adv_pos.push_back(p);
+      a->adv_clock.push_back(ts);
+      a->adv_wall.push_back(wall ? ts : -1);
+    }
+  }
+  a->ev_clock.push_back(a->clock);
+}
+
+void maybe_autoflush(sm_app* a) {
+  if ((int64_t)a->ev_stream.size() >= a->batch_events) flush(a);
+}
+
+void put_value(StreamStage& st, int k, const sm_value& v, sm_app* a) {
+  int t = (int)st.def->attrs[k].type;
+  auto& col = st.cols[k];
+  size_t w = width_of(t);
+  size_t off = col.size();
+  col.resize(off + w);
+  uint8_t* dst = col.data() + off;
+  bool isnull = v.is_null != 0;
+  if (!isnull && v.type != t) throw TypeError("value type does not match attribute '" + st.def->attrs[k].name + "'");
+  switch (t) {
+    case T_INT: { int32_t x = isnull ? 0 : (int32_t)v.i; memcpy(dst, &x, 4); break; }
+    case T_LONG: { int64_t x = isnull ? 0 : v.i; memcpy(dst, &x, 8); break; }
+    case T_FLOAT: { float x = isnull ? 0.f : (float)v.d; memcpy(dst, &x, 4); break; }
+    case T_DOUBLE: { double x = isnull ? 0.0 : v.d; memcpy(dst, &x, 8); break; }
+    case T_STRING: { int32_t x = isnull ? -1 : a->dict.intern(v.s ? v.s : ""); memcpy(dst, &x, 4); break; }
+    default: { uint8_t x = isnull ? 0 : (v.i ? 1 : 0); *dst = x; break; }
+  }
+  if (isnull || st.any_null[k]) {
+    if (!st.any_null[k]) {
+      st.any_null[k] = true;
+      st.nulls[k].assign(st.rows, 0);
+    }
+    st.nulls[k].push_back(isnull ? 1 : 0);
+  }
+}
+
+std::string dump_json(sm_app* a) {
+  std::ostringstream o;
+  o << "{\"streams\":{";
+  bool first = true;
+  for (auto& kv : a->collected_streams) {
+    if (!first) o << ",";
+    first = false;
+    o << "\"" << kv.first << "\":[";
+    for (size_t k = 0; k < kv.second.size(); ++k) o << (k ? "," : "") << kv.second[k];
+    o << "]";
+  }
+  o << "},\"queries\":{";
+  first = true;
+  for (auto& kv : a->collected_queries) {
+    if (!first) o << ",";
+    first = false;
+    o << "\"" << kv.first << "\":[";
+    for (size_t k = 0; k < kv.second.size(); ++k) o << (k ? "," : "") << kv.second[k];
+    o << "]";
+  }
+  o << "}}";
+  return o.str();
+}
+
+}  // namespace
+}  // namespace sm
+
+using namespace sm;
+
+extern "C" {
+
+const char* sm_last_error(void) { return sm::g_err.c_str(); }
+const char* sm_version(void) { return "siddhi_amd 0.1 (gfx950)"; }
+
+int sm_manager_create(sm_manager** out) {
+  *out = new sm_manager();
+  return SM_OK;
+}
+void sm_manager_destroy(sm_manager* m) { delete m; }
+
+int sm_app_create(sm_manager* m, const char* siddhiql, sm_app** out) {
+  (void)m;
+  *out = nullptr;
+  auto a = std::make_unique<sm_app>();
+  int rc = guarded([&] {
+    a->ast = sql::parse_app(siddhiql ? siddhiql : "");
+    build_app(a.get());
+    int dev = 0;
+    if (hipGetDeviceCount(&dev) != hipSuccess || dev == 0)
+      throw std::runtime_error("HIP error: no MI355X device visible (the engine has no CPU fallback)");
+    upload_app(a.get());
+    if (const char* e = getenv("SIDDHI_AMD_HEAP_WORDS")) a->heap_half = std::max(256, atoi(e));
+  });
+  if (rc == SM_OK) *out = a.release();
+  return rc;
+}
+
+void sm_app_destroy(sm_app* a) {
+  if (!a) return;
+  for (auto& q : a->queries) q->keys.release();
+  if (a->stream) (void)hipStreamDestroy(a->stream);
+  delete a;
+}
+
+int sm_app_start(sm_app* a) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    if (a->started) return;
+    a->started = true;
+    // absent start-state processors of non-partitioned queries schedule their first timer at start()
+    stage_record(a, NFA_START, -1, a->clock, 0);
+  });
+}
+
+int sm_app_flush(sm_app* a) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] { flush(a); });
+}
+
+int sm_app_shutdown(sm_app* a) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    if (a->shut) return;
+    flush(a);
+    a->shut = true;
+  });
+}
+
+int sm_app_input_handler(sm_app* a, const char* stream_id, sm_input** out) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    int s = stream_index(a->ast, stream_id ? stream_id : "");
+    if (s < 0) throw sql::ValidationError(std::string("stream '") + (stream_id ? stream_id : "") + "' is not defined");
+    auto in = std::make_unique<sm_input>();
+    in->app = a;
+    in->stream = s;
+    *out = in.get();
+    a->inputs.push_back(std::move(in));
+  });
+}
+
+int sm_input_send(sm_input* in, int64_t ts, const sm_value* row, size_t n) {
+  sm_app* a = in->app;
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    StreamStage& st = a->streams[in->stream];
+    if (n != st.def->attrs.size()) throw TypeError("row has " + std::to_string(n) + " values, stream '" + st.def->id +
+                                                   "' has " + std::to_string(st.def->attrs.size()) + " attributes");
+    for (size_t k = 0; k < n; ++k) put_value(st, (int)k, row[k], a);
+    st.row_pos.push_back((int64_t)a->ev_stream.size());
+    stage_record(a, in->stream, st.rows, ts, 0);
+    st.rows++;
+    maybe_autoflush(a);
+  });
+}
+
+int sm_input_send_columns(sm_input* in, size_t n, const int64_t* ts, const void* const* cols,
+                          const uint8_t* const* null_flags) {
+  sm_app* a = in->app;
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    StreamStage& st = a->streams[in->stream];
+    size_t na = st.def->attrs.size();
+    for (size_t i = 0; i < n; ++i) {
+      for (size_t k = 0; k < na; ++k) {
+        sm_value v{};
+        int t = (int)st.def->attrs[k].type;
+        v.type = t;
+        v.is_null = null_flags && null_flags[k] && null_flags[k][i];
+        switch (t) {
+          case T_INT: v.i = ((const int32_t*)cols[k])[i]; break;
+          case T_LONG: v.i = ((const int64_t*)cols[k])[i]; break;
+          case T_FLOAT: v.d = ((const float*)cols[k])[i]; break;
+          case T_DOUBLE: v.d = ((const double*)cols[k])[i]; break;
+          case T_STRING: v.s = ((const char* const*)cols[k])[i]; v.is_null |= v.s == nullptr; break;
+          default: v.i = ((const uint8_t*)cols[k])[i]; break;
+        }
+        put_value(st, (int)k, v, a);
+      }
+      st.row_pos.push_back((int64_t)a->ev_stream.size());
+      stage_record(a, in->stream, st.rows, ts[i], 0);
+      st.rows++;
+      maybe_autoflush(a);
+    }
+  });
+}
+
+int sm_app_stream_schema(sm_app* a, const char* stream_id, int32_t* types, size_t cap, size_t* n) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    int s = stream_index(a->ast, stream_id ? stream_id : "");
+    if (s < 0) throw sql::ValidationError(std::string("stream '") + (stream_id ? stream_id : "") + "' is not defined");
+    const auto& at = a->ast.streams[s].attrs;
+    *n = at.size();
+    for (size_t k = 0; k < at.size() && k < cap; ++k) types[k] = (int32_t)at[k].type;
+  });
+}
+
+int sm_app_advance_time(sm_app* a, int64_t ts) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    if (!a->ast.playback) return;
+    stage_record(a, NFA_TICK, -1, ts, 0);
+  });
+}
+
+int sm_app_advance_wallclock(sm_app* a, int64_t ts) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    if (!a->ast.playback) return;
+    stage_record(a, NFA_WALL, -1, ts, 1);
+  });
+}
+
+int sm_app_add_stream_callback(sm_app* a, const char* stream_id, sm_stream_callback cb, void* user) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    Callback c;
+    c.scb = cb;
+    c.user = user;
+    a->stream_cbs[stream_id].push_back(c);
+  });
+}
+
+int sm_app_add_query_callback(sm_app* a, const char* query_name, sm_query_callback cb, void* user) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    bool found = false;
+    for (auto& q : a->queries)
+      if (q->cq.name == query_name) found = true;
+    if (!found) throw sql::ValidationError(std::string("No query with name ") + query_name + " exists");
+    Callback c;
+    c.qcb = cb;
+    c.user = user;
+    a->query_cbs[query_name].push_back(c);
+  });
+}
+
+int sm_app_set_collect(sm_app* a, int collect) {
+  std::lock_guard<std::mutex> g(a->mu);
+  a->collect = collect != 0;
+  return SM_OK;
+}
+
+size_t sm_app_dump_outputs(sm_app* a, char* buf, size_t len) {
+  std::lock_guard<std::mutex> g(a->mu);
+  std::string s = dump_json(a);
+  if (buf && len > s.size()) {
+    memcpy(buf, s.data(), s.size());
+    buf[s.size()] = 0;
+  }
+  return s.size();
+}
+
+int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    std::string k = key ? key : "";
+    if (k == "heap_words") {
+      for (auto& q : a->queries)
+        if (q->state_slots) throw std::runtime_error("heap_words must be set before the first flush");
+      a->heap_half = (int32_t)std::max<int64_t>(256, value);
+    } else if (k == "batch_events") {
+      a->batch_events = std::max<int64_t>(1, value);
+    } else {
+      throw std::invalid_argument("unknown option " + k);
+    }
+  });
+}
+
+int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, const int64_t* d_ts,
+                                const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
+                                void* hip_stream) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    int s = stream_index(a->ast, stream_id ? stream_id : "");
+    if (s < 0) throw sql::ValidationError("unknown stream");
+    hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
+    StreamStage& st = a->streams[s];
+    NfaStream d;
+    memset(&d, 0, sizeof(d));
+    d.nattr = (int)st.def->attrs.size();
+    for (int k = 0; k < d.nattr; ++k) {
+      d.types[k] = (int)st.def->attrs[k].type;
+      d.cols[k] = d_cols[k];
+    }
+    a->d_streams.ensure(sizeof(NfaStream));
+    SM_HIP(hipMemcpyAsync(a->d_streams.p, &d, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
+    ensure_scratch(a, n * 64 + (64 << 20));
+    for (auto& qp : a->queries) {
+      QueryRt& q = *qp;
+      const CompiledQuery& cq = q.cq;
+      if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
+      a->sc.used = 0;
+      const char* blob = (const char*)q.blob.p;
+      if (cq.hdr.kind == 0) {
+        int64_t* rows = (int64_t*)a->sc.take(n * 8);
+        int64_t nm = filter_rows((const NfaStream*)a->d_streams.p, (int64_t)n,
+                                 (const Instr*)(blob + cq.hdr.off_code) + cq.hdr.filt_off, cq.hdr.filt_len,
+                                 (const DVal*)(blob + cq.hdr.off_const), rows, a->sc, hs);
+        q.dev_pairs.ensure(std::max<size_t>(nm * 8, 16));
+        q.dev_n = nm;
+        // rows stay as int64 row indices (ordinal = base + row)
+        SM_HIP(hipMemcpyAsync(q.dev_pairs.p, rows, nm * 8, hipMemcpyDeviceToDevice, hs));
+        continue;
+      }
+      if (!cq.fast_every_within)
+        throw sql::UnsupportedError("device batches support filter queries and `every e1 -> e2 within T` patterns; "
+                                    "query '" + cq.name + "' needs the host API");
+      FastArgs fa{};
+      fa.n = (int64_t)n;
+      fa.ts = d_ts;
+      fa.st = (const NfaStream*)a->d_streams.p;
+      fa.key = cq.partition >= 0 ? (const KeyProg*)q.keyprogs.p : nullptr;
+      if (fa.key) {
+        const CompiledPartition& cp = *q.part;
+        int idx = (int)(std::find(cp.streams.begin(), cp.streams.end(), s) - cp.streams.begin());
+        fa.key = (const KeyProg*)q.keyprogs.p + idx;
+      }
+      fa.code = (const Instr*)(blob + cq.hdr.off_code);
+      fa.consts = (const DVal*)(blob + cq.hdr.off_const);
+      fa.c1_off = cq.fast_c1_off;
+      fa.c1_len = cq.fast_c1_len;
+      fa.c2_off = cq.fast_c2_off;
+      fa.c2_len = cq.fast_c2_len;
+      fa.within = cq.fast_within;
+      fa.ordinals = d_ordinals;
+      fa.ordinal_base = ordinal_base;
+      q.dev_pairs.ensure(std::max<size_t>(n * 8, 16));
+      q.dev_n = fast_every_within(fa, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs);
+    }
+  });
+}
+
+int sm_app_device_matches(sm_app* a, const char* query_name, const uint32_t** d_pairs, size_t* n) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    for (auto& q : a->queries)
+      if (q->cq.name == query_name) {
+        *d_pairs = (const uint32_t*)q->dev_pairs.p;
+        *n = (size_t)q->dev_n;
+        return;
+      }
+    throw sql::ValidationError(std::string("No query with name ") + query_name);
+  });
+}
+
+}  // extern "C"

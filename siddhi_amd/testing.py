@@ -1,0 +1,113 @@
+"""Adapters used by the parity tests: drive the product through the C ABI with the same surface as the
+oracle's OracleApp (start / send / advance_time / advance_wallclock / flush / outputs)."""
+import ctypes
+import json
+
+from . import _lib
+from ._lib import check, lib
+
+
+class EngineError(Exception):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _call(rc):
+    if rc != _lib.SM_OK:
+        raise EngineError(rc, lib().sm_last_error().decode(errors="replace"))
+
+
+class ProductApp:
+    _mgr = None
+
+    def __init__(self, siddhiql, **options):
+        L = lib()
+        if ProductApp._mgr is None:
+            m = ctypes.c_void_p()
+            _call(L.sm_manager_create(ctypes.byref(m)))
+            ProductApp._mgr = m
+        h = ctypes.c_void_p()
+        _call(L.sm_app_create(ProductApp._mgr, siddhiql.encode(), ctypes.byref(h)))
+        self.h = h
+        for k, v in options.items():
+            _call(L.sm_app_set_option(self.h, k.encode(), int(v)))
+        _call(L.sm_app_set_collect(self.h, 1))
+        self._inputs = {}
+
+    def close(self):
+        if self.h:
+            lib().sm_app_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def start(self):
+        _call(lib().sm_app_start(self.h))
+
+    def _input(self, sid):
+        if sid not in self._inputs:
+            h = ctypes.c_void_p()
+            _call(lib().sm_app_input_handler(self.h, sid.encode(), ctypes.byref(h)))
+            self._inputs[sid] = h
+        return self._inputs[sid]
+
+    def send(self, sid, ts, row, types):
+        arr = (_lib.SmValue * max(len(row), 1))()
+        keep = []
+        for k, (v, t) in enumerate(zip(row, types)):
+            arr[k].type = _lib.TYPE_CODES[t]
+            if v is None:
+                arr[k].is_null = 1
+            elif t == "STRING":
+                b = str(v).encode()
+                keep.append(b)
+                arr[k].s = b
+            elif t in ("FLOAT", "DOUBLE"):
+                arr[k].d = float(v)
+            elif t == "BOOL":
+                arr[k].i = 1 if v else 0
+            else:
+                arr[k].i = int(v)
+        _call(lib().sm_input_send(self._input(sid), int(ts), arr, len(row)))
+
+    def send_columns(self, sid, ts, cols):
+        """ts: int64 numpy array; cols: list of numpy arrays (native widths)."""
+        n = len(ts)
+        ptrs = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        _call(lib().sm_input_send_columns(self._input(sid), n, ts.ctypes.data, ptrs, None))
+
+    def advance_time(self, ts):
+        _call(lib().sm_app_advance_time(self.h, int(ts)))
+
+    def advance_wallclock(self, ts):
+        _call(lib().sm_app_advance_wallclock(self.h, int(ts)))
+
+    def flush(self):
+        _call(lib().sm_app_flush(self.h))
+
+    def outputs(self):
+        L = lib()
+        n = L.sm_app_dump_outputs(self.h, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        L.sm_app_dump_outputs(self.h, buf, n + 1)
+        return json.loads(buf.value.decode())
+
+    def set_option(self, key, value):
+        _call(lib().sm_app_set_option(self.h, key.encode(), int(value)))
+
+    def process_device_batch(self, stream, ts_tensor, col_tensors, ordinals=None, ordinal_base=0, hip_stream=None):
+        ptrs = (ctypes.c_void_p * len(col_tensors))(*[t.data_ptr() for t in col_tensors])
+        _call(lib().sm_app_process_device_batch(self.h, stream.encode(), ts_tensor.numel(), ts_tensor.data_ptr(), ptrs,
+                                                ordinals.data_ptr() if ordinals is not None else None,
+                                                int(ordinal_base), hip_stream))
+
+    def device_matches(self, query):
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        _call(lib().sm_app_device_matches(self.h, query.encode(), ctypes.byref(p), ctypes.byref(n)))
+        return p.value, n.value

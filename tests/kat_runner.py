@@ -166,3 +166,49 @@ def _drive(app, kat, schemas, wallclock_absent):
                 if len(exp) != len(g) or not all(values_equal(a, b) for a, b in zip(exp, g)):
                     raise KatFailure(f"{cb['target']} event {i + 1}: expected {exp}, got {g}")
     return "pass"
+
+
+def drive_only(factory, kat):
+    """Drive a KAT's event sequence (no expectation checks); returns the outputs dict or an error code."""
+    app_text = kat["app"]
+    wallclock_absent = kat.get("absent_wallclock", False)
+    if wallclock_absent:
+        app_text = "@app:playback " + app_text
+    schemas = stream_schemas(app_text)
+    try:
+        app = factory(app_text)
+    except Exception as e:
+        return ("create-error", getattr(e, "code", None))
+    wall = BASE_TS
+    try:
+        for ev in kat["events"]:
+            tag = ev[0]
+            if tag == "__start__":
+                if wallclock_absent:
+                    app.advance_time(wall)
+                app.start()
+            elif tag == "__sleep__":
+                wall += ev[1]
+                if wallclock_absent:
+                    app.advance_wallclock(wall)
+            elif tag in ("__assert__", "__wait__"):
+                if tag == "__wait__":
+                    # waits end immediately in synchronous processing when the count is reached; emulate by
+                    # advancing `sleep` once (both engines see the same sequence)
+                    pass
+                continue
+            else:
+                sid, ts, vals = ev
+                types = schemas[sid]
+                row = [coerce(v, t) for v, t in zip(vals, types)]
+                if wallclock_absent and ts is None:
+                    app.advance_wallclock(wall)
+                app.send(sid, wall if ts is None else ts, row, types)
+        app.flush()
+        return app.outputs()
+    except Exception as e:
+        return ("runtime-error", getattr(e, "code", None))
+    finally:
+        close = getattr(app, "close", None)
+        if close:
+            close()
