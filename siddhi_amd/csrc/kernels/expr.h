@@ -6,7 +6,7 @@
 //   not:      NotConditionExpressionExecutor.java:43-50 (not null → true)
 //   math:     core/executor/math/** (result type by promotion; x/0 and x%0 → null; Java int wrap-around)
 #pragma once
-#include <hip/hip_runtime.h>
+#include "hd.h"
 
 #include "../plan.h"
 

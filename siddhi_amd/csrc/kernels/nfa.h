@@ -1,6 +1,6 @@
 // Device batch descriptors shared by the runtime (host) and the NFA / filter / fast-path kernels.
 #pragma once
-#include <hip/hip_runtime.h>
+#include "hd.h"
 
 #include "../plan.h"
 
@@ -26,7 +26,7 @@ struct NfaBatch {
   const int64_t* ev_row;     // row within the stream's columns
   const int64_t* ev_ts;
   const int64_t* ev_clock;   // playback clock after the record's sendData
-  int64_t ordinal_base;      // global ordinal of record 0
+  const int64_t* ev_ord;     // global arrival ordinal of each data event (-1 for markers)
   const NfaStream* streams;
   // advance points (playback listener firings / wall ticks), ascending position
   const int64_t* adv_pos;

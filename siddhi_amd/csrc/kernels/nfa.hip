@@ -1,1114 +1,14 @@
-// General pattern/sequence NFA interpreter for gfx950: one lane per partition key (one lane in total for a
-// non-partitioned query), stepping that key's events in arrival order against the key's persistent
-// partial-match state in HBM.
-//
-// The per-key state is a small copying-collected heap of
-//   run records  (StateEvent, core/event/state/StateEvent.java:53)      — shared by reference
-//   chain nodes  (StreamEvent copies, StreamEventCloner.java:46-63)       — shared by shallow copies
-//   list nodes   (pending / newAndEvery LinkedLists of each pre-state processor)
-// plus per-processor flags and FIFO timer queues (util/Scheduler.java:44). Every function below restates
-// the reference method named in its comment; the CPU oracle (oracle/cpu_ref.cpp) restates the same methods
-// independently over an object graph.
-#include "nfa.h"
-
-#include "expr.h"
+// HIP launch wrapper of the NFA interpreter (implementation in nfa_impl.h).
+#include "nfa_impl.h"
 
 namespace sm {
-
 namespace {
-
-constexpr int K_REC = 1, K_NODE = 2, K_LNODE = 3, K_FWD = 0xFF;
-
-struct Lane;
-
-struct StateLoader {  // OP_VAR loads for a run record
-  const Lane* L;
-  int rec;
-  __device__ StackVal var(const Instr& in) const;
-};
-
-struct Lane {
-  // plan
-  const DQuery* q;
-  const DPre* pre;
-  const DPost* post;
-  const DInner* inner;
-  const DReceiver* recv;
-  const DWithin* within;
-  const Instr* code;
-  const DVal* consts;
-  const int32_t* sel;
-  const int32_t* refs;
-  // state
-  int64_t* ks;
-  int64_t* heap;
-  int32_t half;  // words per semispace
-  // batch
-  const NfaBatch* b;
-  // output
-  int32_t key;
-  int64_t pos, time;
-  int32_t phase, sched;
-  int32_t seq;
-  int32_t err;
-  int64_t clock;  // EventTimeBasedMillisTimestampGenerator.currentTime() as seen by this lane
-
-  // ------------------------------------------------------------ heap
-  __device__ int64_t& misc(int k) const { return ks[q->ks_misc + k]; }
-  __device__ int32_t alloc(int words) {
-    int64_t space = misc(2);
-    int64_t end = (space + 1) * half;
-    int64_t bump = misc(1);
-    if (bump + words > end) {
-      err |= NFA_ERR_ARENA;
-      return 2 * half;  // dummy region (writes harmless; lane aborts at the next safe point)
-    }
-    misc(1) = bump + words;
-    return (int32_t)bump;
-  }
-  __device__ int kind_of(int32_t o) const { return (int)(heap[o] & 0xFF); }
-  __device__ int32_t hi(int32_t o) const { return (int32_t)(heap[o] >> 32); }
-  __device__ void set_hi(int32_t o, int32_t v) const {
-    heap[o] = (heap[o] & 0xFFFFFFFFll) | ((int64_t)(uint32_t)v << 32);
-  }
-  // run record
-  __device__ int64_t& rts(int32_t r) const { return heap[r + 1]; }
-  __device__ int32_t slot(int32_t r, int s) const {
-    int64_t w = heap[r + 2 + (s >> 1)];
-    return (s & 1) ? (int32_t)(w >> 32) : (int32_t)w;
-  }
-  __device__ void set_slot(int32_t r, int s, int32_t v) const {
-    int64_t& w = heap[r + 2 + (s >> 1)];
-    if (s & 1) w = (w & 0xFFFFFFFFll) | ((int64_t)(uint32_t)v << 32);
-    else w = (w & ~0xFFFFFFFFll) | (int64_t)(uint32_t)v;
-  }
-  __device__ int32_t new_rec() {
-    int32_t r = alloc(q->rec_words);
-    heap[r] = K_REC;
-    heap[r + 1] = -1;  // StateEvent.timestamp = -1
-    for (int k = 2; k < q->rec_words; ++k) heap[r + k] = -1;  // all slots null (two -1 halves)
-    return r;
-  }
-  // StateEventCloner.copyStateEvent :46-57 (shallow)
-  __device__ int32_t copy_rec(int32_t src) {
-    int32_t r = alloc(q->rec_words);
-    for (int k = 0; k < q->rec_words; ++k) heap[r + k] = heap[src + k];
-    return r;
-  }
-  // chain node
-  __device__ int32_t nnext(int32_t n) const { return hi(n); }
-  __device__ void set_nnext(int32_t n, int32_t v) const { set_hi(n, v); }
-  __device__ int64_t nts(int32_t n) const { return heap[n + 1]; }
-  __device__ int64_t nord(int32_t n) const { return heap[n + 2]; }
-  __device__ int32_t copy_node(int32_t src) {  // StreamEventCloner.copyStreamEvent: next = null
-    int32_t n = alloc(q->node_words);
-    for (int k = 1; k < q->node_words; ++k) heap[n + k] = heap[src + k];
-    heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
-    return n;
-  }
-  __device__ int32_t empty_node() {  // streamEventPool.borrowEvent(): ts -1, null data
-    int32_t n = alloc(q->node_words);
-    heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
-    heap[n + 1] = -1;
-    heap[n + 2] = -1;
-    heap[n + 3] = -1;  // every attribute null
-    for (int k = 4; k < q->node_words; ++k) heap[n + k] = 0;
-    return n;
-  }
-  // the incoming event, materialised as a chain node once per delivery
-  __device__ int32_t event_node(int64_t p) {
-    int s = b->ev_stream[p];
-    int64_t row = b->ev_row[p];
-    const NfaStream& st = b->streams[s];
-    int32_t n = alloc(q->node_words);
-    heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
-    heap[n + 1] = b->ev_ts[p];
-    heap[n + 2] = b->ordinal_base + p;
-    int64_t nulls = 0;
-    for (int a = 0; a < st.nattr; ++a) {
-      int64_t v = 0;
-      bool isnull = st.nulls[a] && st.nulls[a][row];
-      switch (st.types[a]) {
-        case T_INT: v = ((const int32_t*)st.cols[a])[row]; break;
-        case T_LONG: v = ((const int64_t*)st.cols[a])[row]; break;
-        case T_FLOAT: { double d = (double)((const float*)st.cols[a])[row]; v = __double_as_longlong(d); break; }
-        case T_DOUBLE: v = __double_as_longlong(((const double*)st.cols[a])[row]); break;
-        case T_STRING: v = ((const int32_t*)st.cols[a])[row]; isnull = isnull || v < 0; break;
-        default: v = ((const uint8_t*)st.cols[a])[row]; break;
-      }
-      if (isnull) nulls |= (1ll << a);
-      heap[n + 4 + a] = v;
-    }
-    heap[n + 3] = nulls;
-    return n;
-  }
-  // StateEvent.addEvent :212-222
-  __device__ void add_event(int32_t r, int s, int32_t n) {
-    int32_t a = slot(r, s);
-    if (a < 0) { set_slot(r, s, n); return; }
-    while (nnext(a) >= 0) a = nnext(a);
-    set_nnext(a, n);
-  }
-  // StateEvent.removeLastEvent :224-235
-  __device__ void remove_last_event(int32_t r, int s) {
-    int32_t a = slot(r, s);
-    if (a >= 0) {
-      while (nnext(a) >= 0) {
-        if (nnext(nnext(a)) < 0) { set_nnext(a, -1); return; }
-        a = nnext(a);
-      }
-      set_slot(r, s, -1);
-    }
-  }
-  // StateEvent.getStreamEvent(int[] position) :138-182
-  __device__ int32_t at(int32_t r, int chain, int idx) const {
-    int32_t e = slot(r, chain);
-    if (e < 0) return -1;
-    if (idx >= 0) {
-      for (int k = 1; k <= idx; ++k) {
-        e = nnext(e);
-        if (e < 0) return -1;
-      }
-    } else if (idx == -1) {
-      while (nnext(e) >= 0) e = nnext(e);
-    } else if (idx == -2) {
-      if (nnext(e) < 0) return -1;
-      while (nnext(nnext(e)) >= 0) e = nnext(e);
-    } else {
-      int len = 0;
-      for (int32_t x = e; x >= 0; x = nnext(x)) ++len;
-      int index = len + idx;
-      if (index < 0) return -1;
-      for (int k = 0; k < index; ++k) e = nnext(e);
-    }
-    return e;
-  }
-
-  // ------------------------------------------------------------ lists (LinkedList<StateEvent>)
-  __device__ int64_t& lw(int p, int which) const { return ks[q->ks_pre + p * kPreWords + which]; }
-  __device__ int32_t lhead(int p, int w) const { return (int32_t)lw(p, w); }
-  __device__ int32_t ltail(int p, int w) const { return (int32_t)(lw(p, w) >> 32); }
-  __device__ void lset(int p, int w, int32_t h, int32_t t) const {
-    lw(p, w) = (int64_t)(uint32_t)h | ((int64_t)(uint32_t)t << 32);
-  }
-  __device__ int32_t ln_rec(int32_t ln) const { return hi(ln); }
-  __device__ int32_t ln_next(int32_t ln) const { return (int32_t)heap[ln + 1]; }
-  __device__ void ln_set_next(int32_t ln, int32_t v) const { heap[ln + 1] = v; }
-  __device__ bool lempty(int p, int w) const { return lhead(p, w) < 0; }
-  __device__ void lappend(int p, int w, int32_t rec) {
-    int32_t ln = alloc(2);
-    heap[ln] = K_LNODE | ((int64_t)(uint32_t)rec << 32);
-    heap[ln + 1] = -1;
-    int32_t t = ltail(p, w);
-    if (t < 0) lset(p, w, ln, ln);
-    else {
-      ln_set_next(t, ln);
-      lset(p, w, lhead(p, w), ln);
-    }
-  }
-  __device__ void lclear(int p, int w) const { lset(p, w, -1, -1); }
-  __device__ int lsize(int p, int w) const {
-    int n = 0;
-    for (int32_t x = lhead(p, w); x >= 0; x = ln_next(x)) ++n;
-    return n;
-  }
-  __device__ void lsplice(int p, int dst, int src) {  // dst.addAll(src); src.clear()
-    int32_t sh = lhead(p, src);
-    if (sh < 0) return;
-    int32_t dt = ltail(p, dst);
-    if (dt < 0) lset(p, dst, sh, ltail(p, src));
-    else {
-      ln_set_next(dt, sh);
-      lset(p, dst, lhead(p, dst), ltail(p, src));
-    }
-    lclear(p, src);
-  }
-  // iterator.remove(): unlink `cur` whose predecessor is `prev` (-1 = head); returns the successor
-  __device__ int32_t lerase(int p, int w, int32_t prev, int32_t cur) {
-    int32_t nx = ln_next(cur);
-    int32_t h = lhead(p, w), t = ltail(p, w);
-    if (prev < 0) h = nx;
-    else ln_set_next(prev, nx);
-    if (t == cur) t = prev;
-    lset(p, w, h, t);
-    return nx;
-  }
-  __device__ void lremove_rec(int p, int w, int32_t rec) {  // LinkedList.remove(Object): first occurrence
-    int32_t prev = -1;
-    for (int32_t x = lhead(p, w); x >= 0; prev = x, x = ln_next(x))
-      if (ln_rec(x) == rec) {
-        lerase(p, w, prev, x);
-        return;
-      }
-  }
-
-  // ------------------------------------------------------------ flags
-  __device__ int64_t& flags(int p) const { return lw(p, 2); }
-  __device__ bool fl(int p, int64_t f) const { return (flags(p) & f) != 0; }
-  __device__ void setfl(int p, int64_t f, bool v) const {
-    if (v) flags(p) |= f;
-    else flags(p) &= ~f;
-  }
-  __device__ int64_t& lastArrival(int p) const { return lw(p, 3); }
-  __device__ int64_t& returned(int o) const { return ks[q->ks_post + o]; }
-
-  // ------------------------------------------------------------ timers (Scheduler FIFO)
-  __device__ int64_t* sq(int s) const { return ks + q->ks_sched + s * (2 + kSchedCap); }
-  __device__ void notifyAt(int s, int64_t t) {  // Scheduler.notifyAt :66-74
-    int64_t* S = sq(s);
-    if (S[1] >= kSchedCap) {
-      err |= NFA_ERR_TIMERS;
-      return;
-    }
-    S[2 + (S[0] + S[1]) % kSchedCap] = t;
-    S[1]++;
-  }
-  __device__ bool qempty(int s) const { return sq(s)[1] == 0; }
-  __device__ int64_t qhead(int s) const {
-    const int64_t* S = sq(s);
-    return S[2 + S[0]];
-  }
-  __device__ void qpop(int s) const {
-    int64_t* S = sq(s);
-    S[0] = (S[0] + 1) % kSchedCap;
-    S[1]--;
-  }
-
-  // ------------------------------------------------------------ evaluation
-  __device__ bool filter_pass(int p, int32_t rec) const {
-    const DPre& P = pre[p];
-    if (P.progLen == 0) return true;
-    StateLoader ld{this, rec};
-    return truthy(eval_prog(code + P.progOff, P.progLen, consts, ld));
-  }
-  __device__ bool is_absent(int p) const { return pre[p].kind == PK_ABSENT_STREAM || pre[p].kind == PK_ABSENT_LOGICAL; }
-
-  // StreamPreStateProcessor.isExpired :102-121
-  __device__ bool expired(int p, int32_t rec, int64_t now) {
-    const DPre& P = pre[p];
-    for (int w = 0; w < P.withinCnt; ++w) {
-      const DWithin& W = within[P.withinOff + w];
-      for (int k = 0; k < W.n; ++k) {
-        int id = W.ids[k];
-        int64_t ref;
-        if (id < 0) ref = rts(rec);
-        else {
-          int32_t se = slot(rec, id);
-          if (se < 0) {
-            err |= NFA_ERR_NPE;
-            return false;
-          }
-          ref = nts(se);
-        }
-        int64_t d = ref - now;
-        if (d < 0) d = -d;
-        if (d > W.t) return true;
-      }
-    }
-    return false;
-  }
-
-  // ------------------------------------------------------------ selector (QuerySelector.processNoGroupBy)
-  __device__ void emit(int32_t rec) {
-    uint32_t idx = atomicAdd(b->out_count, 1u);
-    if (idx >= b->out_cap) {
-      err |= NFA_ERR_OUTPUT;
-      return;
-    }
-    char* base = (char*)b->out + (size_t)idx * b->out_stride;
-    OutRec* o = (OutRec*)base;
-    o->pos = pos;
-    o->time = time;
-    o->create = q->partitioned ? misc(0) : -1;
-    o->ts = rts(rec);
-    o->phase = phase;
-    o->query = q->query_order;
-    o->sched = sched;
-    o->seq = seq++;
-    o->key = key;
-    DVal* vals = (DVal*)(base + sizeof(OutRec));
-    StateLoader ld{this, rec};
-    for (int k = 0; k < q->nsel; ++k) {
-      StackVal v = eval_prog(code + sel[3 * k], sel[3 * k + 1], consts, ld);
-      if (sel[3 * k + 2] == T_FLOAT || sel[3 * k + 2] == T_DOUBLE) vals[k].d = v.d;
-      else vals[k].i = v.i;
-      vals[k].null = v.null;
-      vals[k].pad = 0;
-    }
-    int64_t* rf = (int64_t*)(vals + q->nsel);
-    for (int k = 0; k < q->nrefs; ++k) {
-      int32_t n = at(rec, refs[2 * k], refs[2 * k + 1]);
-      rf[k] = n >= 0 ? nord(n) : -1;
-    }
-  }
-
-  // ------------------------------------------------------------ pre-state processors
-  // StreamPreStateProcessor.init :165-174
-  __device__ void pre_init(int p) {
-    const DPre& P = pre[p];
-    const DPost& TP = post[P.post];
-    if (P.isStart && (!fl(p, F_INITIALIZED) || TP.nextEveryPre >= 0 ||
-                      (P.sequence && TP.nextPre >= 0 && is_absent(TP.nextPre)))) {
-      int32_t r = new_rec();
-      misc(3)++;
-      addState(p, r);
-      setfl(p, F_INITIALIZED, true);
-    }
-  }
-
-  __device__ void addState(int p, int32_t r) {
-    const DPre& P = pre[p];
-    switch (P.kind) {
-      case PK_STREAM:  // StreamPreStateProcessor.addState :208-221
-        if (P.sequence) {
-          if (lempty(p, 1)) lappend(p, 1, r);
-        } else {
-          lappend(p, 1, r);
-        }
-        break;
-      case PK_COUNT:  // CountPreStateProcessor.addState :109-127
-        if (P.sequence) {
-          if (lempty(p, 1)) lappend(p, 1, r);
-        } else {
-          lappend(p, 1, r);
-        }
-        if (P.minCount == 0 && slot(r, P.stateId) < 0) count_minReached(P.post, r);
-        break;
-      case PK_LOGICAL:
-      case PK_ABSENT_LOGICAL: {  // LogicalPreStateProcessor.addState :62-77 (+ AbsentLogical override)
-        if (P.kind == PK_ABSENT_LOGICAL && !fl(p, F_ACTIVE)) return;
-        int pt = P.partner;
-        if (P.isStart || P.sequence) {
-          if (lempty(p, 1)) lappend(p, 1, r);
-          if (pt >= 0 && lempty(pt, 1)) lappend(pt, 1, r);
-        } else {
-          lappend(p, 1, r);
-          if (pt >= 0) lappend(pt, 1, r);
-        }
-        if (P.kind == PK_ABSENT_LOGICAL && !P.isStart && P.waitingTime != -1) {
-          notifyAt(P.sched, rts(r) + P.waitingTime);
-          if (pre[pt].kind == PK_ABSENT_LOGICAL) notifyAt(pre[pt].sched, rts(r) + pre[pt].waitingTime);
-        }
-        break;
-      }
-      default:  // PK_ABSENT_STREAM: AbsentStreamPreStateProcessor.addState :89-108
-        if (!fl(p, F_ACTIVE)) return;
-        if (P.sequence) {
-          lclear(p, 1);
-          lappend(p, 1, r);
-        } else {
-          lappend(p, 1, r);
-        }
-        if (!P.isStart) notifyAt(P.sched, rts(r) + P.waitingTime);
-        break;
-    }
-  }
-
-  __device__ void addEveryState(int p, int32_t r) {
-    const DPre& P = pre[p];
-    switch (P.kind) {
-      case PK_LOGICAL: {  // LogicalPreStateProcessor.addEveryState :80-88
-        int32_t c = copy_rec(r);
-        set_slot(c, P.stateId, -1);
-        lappend(p, 1, c);
-        if (P.partner >= 0) {
-          set_slot(c, pre[P.partner].stateId, -1);
-          lappend(P.partner, 1, c);
-        }
-        break;
-      }
-      case PK_ABSENT_LOGICAL: {  // AbsentLogicalPreStateProcessor.addEveryState
-        int32_t c = copy_rec(r);
-        int32_t own = slot(c, P.stateId);
-        if (own >= 0) rts(c) = nts(own);
-        set_slot(c, P.stateId, -1);
-        set_slot(c, pre[P.partner].stateId, -1);
-        lappend(p, 1, c);
-        lappend(P.partner, 1, c);
-        break;
-      }
-      default:  // StreamPreStateProcessor.addEveryState :224-226
-        lappend(p, 1, copy_rec(r));
-        break;
-    }
-  }
-
-  __device__ void updateState(int p) {
-    const DPre& P = pre[p];
-    if (P.kind == PK_COUNT && fl(p, F_START_RESET)) {  // CountPreStateProcessor.updateState :145-151
-      setfl(p, F_START_RESET, false);
-      pre_init(p);
-    }
-    lsplice(p, 0, 1);  // StreamPreStateProcessor.updateState :268-271
-    if (P.kind == PK_LOGICAL || P.kind == PK_ABSENT_LOGICAL) lsplice(P.partner, 0, 1);
-  }
-
-  __device__ bool seq_guard(int p) const {
-    const DPre& P = pre[p];
-    const DPost& TP = post[P.post];
-    return P.sequence && TP.nextEveryPre < 0 && TP.nextPre >= 0 && !lempty(TP.nextPre, 0);
-  }
-
-  __device__ void resetState(int p) {
-    const DPre& P = pre[p];
-    switch (P.kind) {
-      case PK_STREAM:
-      case PK_COUNT:  // StreamPreStateProcessor.resetState :253-265
-        lclear(p, 0);
-        if (P.isStart && lempty(p, 1)) {
-          if (P.sequence && post[P.post].nextEveryPre < 0 && post[P.post].nextPre < 0) {
-            err |= NFA_ERR_NPE;
-            return;
-          }
-          if (seq_guard(p)) return;
-          pre_init(p);
-        }
-        break;
-      case PK_LOGICAL:
-      case PK_ABSENT_LOGICAL:  // LogicalPreStateProcessor.resetState :98-113
-        if (P.ltype == LT_OR || lsize(p, 0) == lsize(P.partner, 0)) {
-          lclear(p, 0);
-          lclear(P.partner, 0);
-          if (P.isStart && lempty(p, 1)) {
-            if (seq_guard(p)) return;
-            pre_init(p);
-          }
-        }
-        break;
-      default:  // AbsentStreamPreStateProcessor.resetState :111-126
-        lclear(p, 0);
-        if (P.isStart) {
-          if (seq_guard(p)) return;
-          pre_init(p);
-        }
-        break;
-    }
-  }
-
-  // CountPreStateProcessor.startStateReset :137-142
-  // (the callback branch re-enters the same processor; callbackPreStateProcessor is only ever set from
-  //  CountPostStateProcessor.setNextStatePreProcessor before setStartState runs, so it is never taken)
-  __device__ void count_startStateReset(int p) { setfl(p, F_START_RESET, true); }
-
-  // StreamPreStateProcessor.process(StateEvent) :123-129 → FilterProcessor → post
-  __device__ void pre_process(int p, int32_t r) {
-    setfl(p, F_STATE_CHANGED, false);
-    if (!filter_pass(p, r)) return;
-    post_process(pre[p].post, r);
-  }
-
-  // processAndReturn of every pre kind; returned records are appended to the temporary list `ret`
-  // (list words kept in ks slots 4/5 of the pre: the selector runs after the loop, as in the receivers).
-  __device__ void processAndReturn(int p, int32_t evnode, int64_t now) {
-    const DPre& P = pre[p];
-    const int sid = P.stateId;
-    lclear(p, 4 - 0);  // ret list lives in word 4 (head|tail); word 5 spare
-    switch (P.kind) {
-      case PK_STREAM:
-      case PK_ABSENT_STREAM: {
-        if (P.kind == PK_ABSENT_STREAM && !fl(p, F_ACTIVE)) return;
-        int32_t prev = -1;
-        for (int32_t ln = lhead(p, 0); ln >= 0;) {
-          if (err) return;
-          int32_t s = ln_rec(ln);
-          if (P.withinCnt > 0 && expired(p, s, now)) {
-            ln = lerase(p, 0, prev, ln);
-            continue;
-          }
-          set_slot(s, sid, copy_node(evnode));
-          pre_process(p, s);
-          int tl = P.thisLast;
-          if (returned(tl)) {
-            returned(tl) = 0;
-            lappend(p, 4, s);
-          }
-          if (fl(p, F_STATE_CHANGED)) {
-            ln = lerase(p, 0, prev, ln);
-          } else if (!P.sequence) {
-            set_slot(s, sid, -1);
-            prev = ln;
-            ln = ln_next(ln);
-          } else {
-            set_slot(s, sid, -1);
-            ln = lerase(p, 0, prev, ln);
-            int cb = post[P.post].callbackPre;
-            if (cb >= 0) count_startStateReset(cb);
-          }
-        }
-        if (P.kind == PK_ABSENT_STREAM) lclear(p, 4);  // AbsentStreamPreStateProcessor.processAndReturn :218-231
-        return;
-      }
-      case PK_COUNT: {  // CountPreStateProcessor.processAndReturn :58-93
-        int32_t prev = -1;
-        for (int32_t ln = lhead(p, 0); ln >= 0;) {
-          if (err) return;
-          int32_t s = ln_rec(ln);
-          if ((q->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (q->nslots > sid + 2 && slot(s, sid + 2) >= 0)) {
-            ln = lerase(p, 0, prev, ln);
-            continue;
-          }
-          add_event(s, sid, copy_node(evnode));
-          setfl(p, F_SUCCESS, false);
-          pre_process(p, s);
-          int tl = P.thisLast;
-          if (returned(tl)) {
-            returned(tl) = 0;
-            lappend(p, 4, s);
-          }
-          bool removed = false;
-          if (fl(p, F_STATE_CHANGED)) {
-            ln = lerase(p, 0, prev, ln);
-            removed = true;
-          }
-          if (!fl(p, F_SUCCESS)) {
-            remove_last_event(s, sid);
-            if (P.sequence) {
-              if (removed) {
-                err |= NFA_ERR_NPE;
-                return;
-              }
-              ln = lerase(p, 0, prev, ln);
-              removed = true;
-            }
-          }
-          if (!removed) {
-            prev = ln;
-            ln = ln_next(ln);
-          }
-        }
-        return;
-      }
-      case PK_LOGICAL: {  // LogicalPreStateProcessor.processAndReturn :125-163
-        int32_t prev = -1;
-        const int psid = pre[P.partner].stateId;
-        for (int32_t ln = lhead(p, 0); ln >= 0;) {
-          if (err) return;
-          int32_t s = ln_rec(ln);
-          if (P.withinCnt > 0 && expired(p, s, now)) {
-            ln = lerase(p, 0, prev, ln);
-            continue;
-          }
-          if (P.ltype == LT_OR && slot(s, psid) >= 0) {
-            ln = lerase(p, 0, prev, ln);
-            continue;
-          }
-          set_slot(s, sid, copy_node(evnode));
-          pre_process(p, s);
-          int tl = P.thisLast;
-          if (returned(tl)) {
-            returned(tl) = 0;
-            lappend(p, 4, s);
-          }
-          if (fl(p, F_STATE_CHANGED)) {
-            ln = lerase(p, 0, prev, ln);
-          } else if (!P.sequence) {
-            set_slot(s, sid, -1);
-            prev = ln;
-            ln = ln_next(ln);
-          } else {
-            set_slot(s, sid, -1);
-            ln = lerase(p, 0, prev, ln);
-          }
-        }
-        return;
-      }
-      default: {  // PK_ABSENT_LOGICAL: AbsentLogicalPreStateProcessor.processAndReturn (always returns empty)
-        if (!fl(p, F_ACTIVE)) return;
-        int32_t prev = -1;
-        const int psid = pre[P.partner].stateId;
-        for (int32_t ln = lhead(p, 0); ln >= 0;) {
-          if (err) return;
-          int32_t s = ln_rec(ln);
-          if (P.withinCnt > 0 && expired(p, s, now)) {
-            ln = lerase(p, 0, prev, ln);
-            continue;
-          }
-          if (P.ltype == LT_OR && slot(s, psid) >= 0) {
-            ln = lerase(p, 0, prev, ln);
-            continue;
-          }
-          int32_t current = slot(s, sid);
-          set_slot(s, sid, copy_node(evnode));
-          pre_process(p, s);
-          if (P.waitingTime != -1 || (P.sequence && P.ltype == LT_AND && post[P.post].nextEveryPre >= 0))
-            set_slot(s, sid, current);
-          bool removed = false;
-          int tl = P.thisLast;
-          if (returned(tl)) {
-            returned(tl) = 0;
-            int32_t nx = lerase(p, 0, prev, ln);
-            removed = true;
-            if (P.sequence) lremove_rec(P.partner, 0, s);
-            ln = nx;
-          }
-          if (!fl(p, F_STATE_CHANGED)) {
-            set_slot(s, sid, current);
-            if (P.sequence) {
-              if (removed) {
-                err |= NFA_ERR_NPE;
-                return;
-              }
-              ln = lerase(p, 0, prev, ln);
-              removed = true;
-            }
-          }
-          if (!removed) {
-            prev = ln;
-            ln = ln_next(ln);
-          }
-        }
-        return;
-      }
-    }
-  }
-
-  // ------------------------------------------------------------ post-state processors
-  __device__ void stream_post(int o, int32_t r) {  // StreamPostStateProcessor.process :53-72
-    const DPost& O = post[o];
-    setfl(O.thisPre, F_STATE_CHANGED, true);
-    rts(r) = nts(slot(r, O.stateId));
-    if (O.hasNext) returned(o) = 1;
-    if (O.nextPre >= 0) addState(O.nextPre, r);
-    if (O.nextEveryPre >= 0) addEveryState(O.nextEveryPre, r);
-    if (O.callbackPre >= 0) count_startStateReset(O.callbackPre);
-  }
-  // CountPostStateProcessor.processMinCountReached :73-85
-  __device__ void count_minReached(int o, int32_t r) {
-    const DPost& O = post[o];
-    if (O.hasNext) {
-      setfl(O.thisPre, F_STATE_CHANGED, true);
-      returned(o) = 1;
-    }
-    if (O.nextPre >= 0) addState(O.nextPre, r);
-    if (O.nextEveryPre >= 0) addEveryState(O.nextEveryPre, r);
-  }
-  // AbsentLogicalPreStateProcessor.partnerCanProceed
-  __device__ bool partnerCanProceed(int p, int32_t r) {
-    const DPre& P = pre[p];
-    const DPost& TP = post[P.post];
-    if (P.sequence && TP.nextEveryPre < 0 && lastArrival(p) > 0) return false;
-    if (P.waitingTime == -1) {
-      if (TP.nextEveryPre < 0) return slot(r, P.stateId) < 0;
-      if (lastArrival(p) > 0) {
-        lastArrival(p) = 0;
-        pre_init(p);
-        return false;
-      }
-      return true;
-    }
-    return slot(r, P.stateId) >= 0;
-  }
-  __device__ void post_process(int o, int32_t r) {
-    const DPost& O = post[o];
-    switch (O.kind) {
-      case PK_STREAM: stream_post(o, r); break;
-      case PK_COUNT: {  // CountPostStateProcessor.process :45-71
-        int32_t e = slot(r, O.stateId);
-        int n = 1;
-        while (nnext(e) >= 0) {
-          ++n;
-          e = nnext(e);
-        }
-        setfl(O.thisPre, F_SUCCESS, true);
-        rts(r) = nts(e);
-        if (n >= O.minCount) {
-          if (pre[O.thisPre].sequence) {
-            if (O.nextPre >= 0) addState(O.nextPre, r);
-            if (n != O.maxCount) addState(O.thisPre, r);
-          } else if (n == O.minCount) {
-            count_minReached(o, r);
-          }
-          if (n == O.maxCount) setfl(O.thisPre, F_STATE_CHANGED, true);
-        }
-        break;
-      }
-      case PK_LOGICAL: {  // LogicalPostStateProcessor.process :59-87
-        if (O.ltype == LT_AND) {
-          bool proceed;
-          if (pre[O.partnerPre].kind == PK_ABSENT_LOGICAL) proceed = partnerCanProceed(O.partnerPre, r);
-          else proceed = slot(r, pre[O.partnerPre].stateId) >= 0;
-          if (proceed) stream_post(o, r);
-          else setfl(O.thisPre, F_STATE_CHANGED, true);
-        } else {
-          stream_post(o, r);
-          if (post[O.partnerPost].hasNext && pre[O.thisPre].thisLast == O.partnerPost) returned(O.partnerPost) = 1;
-        }
-        break;
-      }
-      case PK_ABSENT_STREAM: {  // AbsentStreamPostStateProcessor.process :36-55
-        setfl(O.thisPre, F_STATE_CHANGED, true);
-        int32_t se = slot(r, O.stateId);
-        rts(r) = nts(se);
-        returned(o) = 1;
-        if (pre[O.thisPre].isStart && O.nextEveryPre >= 0 && O.nextEveryPre == O.thisPre)
-          addEveryState(O.nextEveryPre, r);
-        lastArrival(O.thisPre) = nts(se);
-        break;
-      }
-      default: {  // AbsentLogicalPostStateProcessor.process :37-50
-        setfl(O.thisPre, F_STATE_CHANGED, true);
-        returned(o) = 1;
-        lastArrival(O.thisPre) = nts(slot(r, O.stateId));
-        break;
-      }
-    }
-  }
-
-  // ------------------------------------------------------------ absent timers
-  __device__ void absent_sendEvent(int p, int32_t r) {  // AbsentStreamPreStateProcessor.sendEvent :200-215
-    const DPre& P = pre[p];
-    const DPost& TP = post[P.post];
-    if (TP.hasNext) emit(r);
-    if (TP.nextPre >= 0) addState(TP.nextPre, r);
-    if (TP.nextEveryPre >= 0) {
-      addEveryState(TP.nextEveryPre, r);
-    } else if (P.isStart) {
-      setfl(p, F_ACTIVE, false);
-      if (P.kind == PK_ABSENT_LOGICAL && P.ltype == LT_OR && pre[P.partner].kind == PK_ABSENT_LOGICAL)
-        setfl(P.partner, F_ACTIVE, false);
-    }
-    if (TP.callbackPre >= 0) count_startStateReset(TP.callbackPre);
-  }
-
-  // AbsentStreamPreStateProcessor.process(ComplexEventChunk) :129-198 /
-  // AbsentLogicalPreStateProcessor.process(ComplexEventChunk)
-  __device__ void absent_timer(int p, int64_t now) {
-    const DPre& P = pre[p];
-    if (!fl(p, F_ACTIVE)) return;
-    bool notProcessed = true;
-    const int sid = P.stateId;
-    lclear(p, 4);
-    if (now >= lastArrival(p) + P.waitingTime) {
-      if (P.kind == PK_ABSENT_STREAM) {
-        bool initialize = P.isStart && lempty(p, 1) && lempty(p, 0);
-        if (initialize && P.sequence && post[P.post].nextEveryPre < 0 && lastArrival(p) > 0) initialize = false;
-        if (initialize) {
-          addState(p, new_rec());
-        } else if (P.sequence && !lempty(p, 1)) {
-          resetState(p);
-        }
-      } else {
-        if (P.isStart && P.sequence && lempty(p, 1) && lempty(p, 0)) addState(p, new_rec());
-        else if (P.sequence && !lempty(p, 1)) resetState(p);
-      }
-      updateState(p);
-      int32_t prev = -1;
-      for (int32_t ln = lhead(p, 0); ln >= 0;) {
-        if (err) return;
-        int32_t s = ln_rec(ln);
-        if (P.withinCnt > 0 && expired(p, s, now)) {
-          ln = lerase(p, 0, prev, ln);
-          continue;
-        }
-        if (P.kind == PK_ABSENT_STREAM) {
-          if (now >= rts(s) + P.waitingTime) {
-            ln = lerase(p, 0, prev, ln);
-            rts(s) = now;
-            lappend(p, 4, s);
-            continue;
-          }
-        } else {
-          int32_t own = slot(s, sid);
-          bool passed = own >= 0 ? now >= nts(own) + P.waitingTime : now >= rts(s) + P.waitingTime;
-          if (passed) {
-            ln = lerase(p, 0, prev, ln);
-            bool partner_has = slot(s, pre[P.partner].stateId) >= 0;
-            if (P.ltype == LT_OR && !partner_has) {
-              add_event(s, sid, empty_node());
-              lappend(p, 4, s);
-            } else if (P.ltype == LT_AND && partner_has) {
-              lappend(p, 4, s);
-            } else if (P.ltype == LT_AND && !partner_has) {
-              add_event(s, sid, empty_node());
-            }
-            continue;
-          }
-        }
-        prev = ln;
-        ln = ln_next(ln);
-      }
-      notProcessed = lempty(p, 4);
-      for (int32_t ln = lhead(p, 4); ln >= 0; ln = ln_next(ln)) absent_sendEvent(p, ln_rec(ln));
-      lclear(p, 4);
-      lastArrival(p) = 0;
-    }
-    const DPost& TP = post[P.post];
-    bool rearm = (P.kind == PK_ABSENT_STREAM) ? (TP.nextEveryPre == p || (notProcessed && P.isStart))
-                                              : (TP.nextEveryPre >= 0 || (notProcessed && P.isStart));
-    if (rearm) {
-      int64_t base = (P.kind == PK_ABSENT_STREAM) ? now : clock;
-      int64_t nb = (lastArrival(p) == 0) ? base + P.waitingTime : lastArrival(p) + P.waitingTime;
-      notifyAt(P.sched, nb);
-    }
-  }
-
-  // ------------------------------------------------------------ inner runtime reset/update (sequences)
-  __device__ void inner_reset(int in) {
-    // recursion depth bounded by the pattern size; explicit stack for the device
-    int st[32];
-    int sp = 0;
-    st[sp++] = in;
-    while (sp) {
-      const DInner& d = inner[st[--sp]];
-      switch (d.kind) {
-        case IK_STREAM:
-        case IK_COUNT:
-        case IK_EVERY: resetState(d.first); break;  // EveryInnerStateRuntime inherits Stream's reset
-        case IK_NEXT: st[sp++] = d.a; st[sp++] = d.b; break;  // next.reset() then current.reset()
-        default: st[sp++] = d.b; break;                         // Logical: inner2 only
-      }
-    }
-  }
-  __device__ void inner_update(int in) {
-    int st[32];
-    int sp = 0;
-    st[sp++] = in;
-    while (sp) {
-      const DInner& d = inner[st[--sp]];
-      switch (d.kind) {
-        case IK_STREAM:
-        case IK_COUNT:
-        case IK_EVERY: updateState(d.first); break;
-        case IK_NEXT: st[sp++] = d.b; st[sp++] = d.a; break;  // current.update() then next.update()
-        default: st[sp++] = d.b; break;
-      }
-    }
-  }
-
-  // ------------------------------------------------------------ garbage collection (Cheney, safe points only)
-  __device__ int32_t fwd(int32_t o, int64_t& top) {
-    if (o < 0) return o;
-    int k = kind_of(o);
-    if (k == K_FWD) return hi(o);
-    int words = (k == K_REC) ? q->rec_words : (k == K_NODE) ? q->node_words : 2;
-    int32_t n = (int32_t)top;
-    for (int w = 0; w < words; ++w) heap[n + w] = heap[o + w];
-    top += words;
-    heap[o] = K_FWD | ((int64_t)(uint32_t)n << 32);
-    return n;
-  }
-  __device__ void gc() {
-    int64_t space = misc(2);
-    int64_t to = (1 - space) * half;
-    int64_t top = to, scan = to;
-    for (int p = 0; p < q->npre; ++p)
-      for (int w = 0; w < 2; ++w) {
-        int32_t h = fwd(lhead(p, w), top);
-        int32_t t = ltail(p, w) >= 0 ? fwd(ltail(p, w), top) : -1;
-        lset(p, w, h, t);
-      }
-    while (scan < top) {
-      int32_t o = (int32_t)scan;
-      int k = kind_of(o);
-      if (k == K_LNODE) {
-        set_hi(o, fwd(hi(o), top));
-        int32_t nx = (int32_t)heap[o + 1];
-        heap[o + 1] = fwd(nx, top);
-        scan += 2;
-      } else if (k == K_REC) {
-        for (int s = 0; s < q->nslots; ++s) set_slot(o, s, fwd(slot(o, s), top));
-        scan += q->rec_words;
-      } else {
-        set_hi(o, fwd(hi(o), top));
-        scan += q->node_words;
-      }
-    }
-    misc(2) = 1 - space;
-    misc(1) = top;
-  }
-  __device__ void safe_point() {
-    int64_t used = misc(1) - misc(2) * half;
-    if (used * 2 > half) gc();
-  }
-
-  // ------------------------------------------------------------ event delivery
-  // MultiProcessStreamReceiver.receive / SingleProcessStreamReceiver.processAndClear + selector dispatch
-  __device__ void deliver(int64_t p) {
-    int s = b->ev_stream[p];
-    const DReceiver* R = nullptr;
-    for (int k = 0; k < q->nrecv; ++k)
-      if (recv[k].stream == s) R = &recv[k];
-    if (!R) return;
-    pos = p;
-    time = 0;
-    phase = 1;
-    sched = -1;
-    int32_t ev = event_node(p);
-    int64_t now = b->ev_ts[p];
-    // stabilizeStates
-    if (q->kind == 2) {
-      inner_reset(q->root_inner);
-      inner_update(q->root_inner);
-    } else if (R->multi) {
-      for (int k = 0; k < R->nstate; ++k) updateState(R->stateProcs[k]);
-    } else if (R->nstate > 0) {
-      updateState(R->stateProcs[0]);
-    }
-    for (int k = 0; k < R->nproc && !err; ++k) {
-      int pp = R->procs[k];
-      processAndReturn(pp, ev, now);
-      if (err) return;
-      if (!lempty(pp, 4)) {
-        if (!R->hasQuerySelector && !R->multi) {
-          err |= NFA_ERR_NPE;
-          return;
-        }
-        if (R->hasQuerySelector)
-          for (int32_t ln = lhead(pp, 4); ln >= 0; ln = ln_next(ln)) emit(ln_rec(ln));
-      }
-      lclear(pp, 4);
-    }
-  }
-
-  // Playback listeners: every scheduler of this key drains its FIFO while head <= now (Scheduler.sendTimerEvents)
-  __device__ void fire_all(int64_t now, int64_t at_pos, int64_t step_time) {
-    clock = now;
-    for (int p = 0; p < q->npre; ++p) {
-      if (!is_absent(p)) continue;
-      int s = pre[p].sched;
-      while (!qempty(s) && qhead(s) - now <= 0 && !err) {
-        int64_t t = qhead(s);
-        qpop(s);
-        pos = at_pos;
-        time = step_time;
-        phase = 0;
-        sched = s;
-        absent_timer(p, t);
-      }
-    }
-  }
-  __device__ bool min_head(int64_t& t) const {
-    bool any = false;
-    for (int p = 0; p < q->npre; ++p) {
-      if (!is_absent(p)) continue;
-      int s = pre[p].sched;
-      if (!qempty(s)) {
-        int64_t h = qhead(s);
-        if (!any || h < t) t = h;
-        any = true;
-      }
-    }
-    return any;
-  }
-};
-
-__device__ StackVal StateLoader::var(const Instr& in) const {
-  StackVal v;
-  v.i = 0;
-  v.d = 0;
-  v.null = 1;
-  int32_t n = L->at(rec, in.a, in.b);
-  if (n < 0) return v;
-  if ((L->heap[n + 3] >> in.c) & 1) return v;
-  int64_t w = L->heap[n + 4 + in.c];
-  v.null = 0;
-  if (in.t0 == T_FLOAT || in.t0 == T_DOUBLE) v.d = __longlong_as_double(w);
-  else v.i = w;
-  return v;
-}
 
 __global__ void nfa_kernel(NfaBatch b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
                            int32_t heap_half, int32_t nkeys, int32_t* err_out) {
   int key = blockIdx.x * blockDim.x + threadIdx.x;
   if (key >= nkeys) return;
-  const DQuery* q = (const DQuery*)blob;
-  Lane L;
-  L.q = q;
-  L.pre = (const DPre*)(blob + q->off_pre);
-  L.post = (const DPost*)(blob + q->off_post);
-  L.inner = (const DInner*)(blob + q->off_inner);
-  L.recv = (const DReceiver*)(blob + q->off_recv);
-  L.within = (const DWithin*)(blob + q->off_within);
-  L.code = (const Instr*)(blob + q->off_code);
-  L.consts = (const DVal*)(blob + q->off_const);
-  L.sel = (const int32_t*)(blob + q->off_sel);
-  L.refs = (const int32_t*)(blob + q->off_refs);
-  L.ks = ks_all + (int64_t)key * q->ks_words;
-  L.half = heap_half;
-  L.heap = heap_all + (int64_t)key * (2 * (int64_t)heap_half + 64);
-  L.b = &b;
-  L.key = key;
-  L.err = 0;
-  L.seq = 0;
-  L.clock = b.clock_in;
-
-  const int64_t ebeg = b.key_off[key], eend = b.key_off[key + 1];
-  const bool has_timers = q->nsched > 0;
-  // lane creation: QueryRuntime constructor → init() seeds the start state (PartitionRuntime.clonePartition)
-  if (L.misc(4) == 0) {
-    if (ebeg == eend && !(b.create_all)) return;
-    const int32_t* init = (const int32_t*)(blob + q->filt_off);
-    for (int p = 0; p < q->npre; ++p) {
-      L.lset(p, 0, -1, -1);
-      L.lset(p, 1, -1, -1);
-      L.flags(p) = F_ACTIVE;
-      L.lastArrival(p) = 0;
-      L.lset(p, 4, -1, -1);
-    }
-    for (int o = 0; o < q->npost; ++o) L.returned(o) = 0;
-    for (int s = 0; s < q->nsched; ++s) {
-      L.sq(s)[0] = 0;
-      L.sq(s)[1] = 0;
-    }
-    L.misc(0) = (ebeg < eend) ? b.ordinal_base + b.key_pos[ebeg] : -1;  // creation ordinal
-    L.misc(1) = 0;
-    L.misc(2) = 0;
-    L.misc(3) = 0;
-    L.misc(4) = 1;
-    for (int k = 0; k < init[0]; ++k) L.pre_init(init[1 + k]);
-  }
-  if (ebeg == eend && !has_timers) {
-    return;
-  }
-  // Walk this key's events; before each, fire timers due at clock-advance points (playback) in order.
-  int64_t k = ebeg;
-  int64_t search_from = 0;  // advance-point index
-  for (;;) {
-    int64_t next_pos = (k < eend) ? b.key_pos[k] : INT64_MAX;
-    if (has_timers) {
-      for (;;) {
-        if (L.err) break;
-        int64_t t;
-        if (!L.min_head(t)) break;
-        // first advance point at or after search_from whose position <= next_pos and (clock >= t or wall tick)
-        int64_t a = search_from;
-        while (a < b.nadv && b.adv_pos[a] <= next_pos && b.adv_clock[a] < t) ++a;
-        if (a >= b.nadv || b.adv_pos[a] > next_pos) {
-          search_from = a;
-          break;
-        }
-        if (b.adv_wall[a] >= 0) {
-          // wall-clock emulation: step through due timer times up to the tick target
-          int64_t target = b.adv_wall[a];
-          int64_t h;
-          while (L.min_head(h) && h <= target && h >= L.clock && !L.err) L.fire_all(h, b.adv_pos[a], h);
-          L.fire_all(target, b.adv_pos[a], target);
-        } else {
-          L.fire_all(b.adv_clock[a], b.adv_pos[a], b.adv_clock[a]);
-        }
-        search_from = a + 1;
-        L.safe_point();
-      }
-    }
-    if (L.err || k >= eend) break;
-    int64_t p = b.key_pos[k];
-    // clock as of this event (sendData advanced it before delivery)
-    L.clock = b.ev_clock[p];
-    if (b.ev_stream[p] == NFA_START) {
-      // SiddhiAppRuntime.start → AbsentStreamPreStateProcessor.start :261-269 (non-partitioned queries)
-      for (int pp = 0; pp < q->npre; ++pp)
-        if (L.is_absent(pp) && L.pre[pp].isStart && L.pre[pp].waitingTime != -1 && L.fl(pp, F_ACTIVE))
-          L.notifyAt(L.pre[pp].sched, L.clock + L.pre[pp].waitingTime);
-    } else {
-      L.deliver(p);
-    }
-    // timers scheduled by this event may only fire at later advance points
-    while (search_from < b.nadv && b.adv_pos[search_from] <= p) ++search_from;
-    ++k;
-    if (L.err) break;
-    L.safe_point();
-  }
-  if (L.err) atomicOr(err_out, L.err);
+  nfa_lane(b, blob, ks_all, heap_all, heap_half, key, err_out);
 }
 
 }  // namespace

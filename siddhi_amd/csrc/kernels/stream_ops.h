@@ -28,7 +28,7 @@ struct KeyTable {
 int64_t filter_rows(const NfaStream* st_dev, int64_t n, const Instr* code, int len, const DVal* consts,
                     int64_t* out_rows, Scratch& sc, hipStream_t s);
 void project_rows(const NfaStream* st_dev, const int64_t* rows, int64_t nm, const int64_t* row_pos,
-                  const int64_t* ev_ts, int64_t ordinal_base, const char* blob_dev, int32_t query_order, char* out,
+                  const int64_t* ev_ts, const int64_t* ev_ord, const char* blob_dev, int32_t query_order, char* out,
                   uint32_t stride, hipStream_t s);
 int64_t select_records(const int32_t* ev_stream, int64_t n, uint64_t stream_mask, bool with_start, int64_t* out_pos,
                        Scratch& sc, hipStream_t s);

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kFThreads) void filter_write_kernel(const uint64_t*
 
 __global__ void project_kernel(const NfaStream* __restrict__ st, const int64_t* __restrict__ rows, int64_t nm,
                                const int64_t* __restrict__ row_pos, const int64_t* __restrict__ ev_ts,
-                               int64_t ordinal_base, const char* __restrict__ blob, int32_t query_order, char* out,
+                               const int64_t* __restrict__ ev_ord, const char* __restrict__ blob, int32_t query_order, char* out,
                                uint32_t stride) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nm) return;
@@ -139,7 +139,7 @@ __global__ void project_kernel(const NfaStream* __restrict__ st, const int64_t* 
     vals[k].pad = 0;
   }
   int64_t* rf = (int64_t*)(vals + q->nsel);
-  for (int k = 0; k < q->nrefs; ++k) rf[k] = ordinal_base + p;
+  for (int k = 0; k < q->nrefs; ++k) rf[k] = ev_ord[p];
 }
 
 // records of the query's streams (+ START markers when `with_start`), as positions
@@ -420,10 +420,10 @@ int64_t filter_rows(const NfaStream* st_dev, int64_t n, const Instr* code, int l
 }
 
 void project_rows(const NfaStream* st_dev, const int64_t* rows, int64_t nm, const int64_t* row_pos,
-                  const int64_t* ev_ts, int64_t ordinal_base, const char* blob_dev, int32_t query_order, char* out,
+                  const int64_t* ev_ts, const int64_t* ev_ord, const char* blob_dev, int32_t query_order, char* out,
                   uint32_t stride, hipStream_t s) {
   if (nm == 0) return;
-  hipLaunchKernelGGL(project_kernel, grid_for(nm), dim3(256), 0, s, st_dev, rows, nm, row_pos, ev_ts, ordinal_base,
+  hipLaunchKernelGGL(project_kernel, grid_for(nm), dim3(256), 0, s, st_dev, rows, nm, row_pos, ev_ts, ev_ord,
                      blob_dev, query_order, out, stride);
 }
 

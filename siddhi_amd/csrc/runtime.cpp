@@ -146,7 +146,8 @@ struct sm_app {
   std::map<std::string, std::vector<sm::Callback>> stream_cbs, query_cbs;
   // batch staging
   std::vector<int32_t> ev_stream;
-  std::vector<int64_t> ev_row, ev_ts, ev_clock;
+  std::vector<int64_t> ev_row, ev_ts, ev_clock, ev_ord;
+  int64_t next_ordinal = 0;
   std::vector<int64_t> adv_pos, adv_clock, adv_wall;
   int64_t ordinal_base = 0;
   int64_t clock = 0;          // playback clock (EventTimeBasedMillisTimestampGenerator.lastEventTimestamp)
@@ -159,7 +160,7 @@ struct sm_app {
   std::map<std::string, std::vector<std::string>> collected_streams;  // JSON fragments
   std::map<std::string, std::vector<std::string>> collected_queries;
   hipStream_t stream = nullptr;
-  sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_adv_pos, d_adv_clock, d_adv_wall, d_streams, d_err, d_count,
+  sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_ev_ord, d_adv_pos, d_adv_clock, d_adv_wall, d_streams, d_err, d_count,
       d_keyoff, scratch;
   sm::Scratch sc;
 };
@@ -464,6 +465,7 @@ void flush(sm_app* a) {
   upload(a, a->d_ev_row, a->ev_row);
   upload(a, a->d_ev_ts, a->ev_ts);
   upload(a, a->d_ev_clock, a->ev_clock);
+  upload(a, a->d_ev_ord, a->ev_ord);
   upload(a, a->d_adv_pos, a->adv_pos);
   upload(a, a->d_adv_clock, a->adv_clock);
   upload(a, a->d_adv_wall, a->adv_wall);
@@ -486,7 +488,7 @@ void flush(sm_app* a) {
       int64_t nm = filter_rows(sd, st.rows, (const Instr*)(blob + hd->off_code) + h.filt_off, h.filt_len,
                                (const DVal*)(blob + hd->off_const), rows, a->sc, a->stream);
       q.out.ensure(std::max<size_t>((size_t)nm * stride, 16));
-      project_rows(sd, rows, nm, (const int64_t*)st.drow_pos.p, (const int64_t*)a->d_ev_ts.p, a->ordinal_base, blob,
+      project_rows(sd, rows, nm, (const int64_t*)st.drow_pos.p, (const int64_t*)a->d_ev_ts.p, (const int64_t*)a->d_ev_ord.p, blob,
                    h.query_order, (char*)q.out.p, (uint32_t)stride, a->stream);
       read_outputs(a, (int)qi, q.out.p, nm, outs);
       continue;
@@ -520,7 +522,7 @@ void flush(sm_app* a) {
     b.ev_row = (const int64_t*)a->d_ev_row.p;
     b.ev_ts = (const int64_t*)a->d_ev_ts.p;
     b.ev_clock = (const int64_t*)a->d_ev_clock.p;
-    b.ordinal_base = a->ordinal_base;
+    b.ev_ord = (const int64_t*)a->d_ev_ord.p;
     b.streams = (const NfaStream*)a->d_streams.p;
     b.adv_pos = (const int64_t*)a->d_adv_pos.p;
     b.adv_clock = (const int64_t*)a->d_adv_clock.p;
@@ -561,6 +563,7 @@ void flush(sm_app* a) {
   a->ev_row.clear();
   a->ev_ts.clear();
   a->ev_clock.clear();
+  a->ev_ord.clear();
   a->adv_pos.clear();
   a->adv_clock.clear();
   a->adv_wall.clear();
@@ -574,6 +577,7 @@ void stage_record(sm_app* a, int32_t stream, int64_t row, int64_t ts, int wall) 
   a->ev_stream.push_back(stream);
   a->ev_row.push_back(row);
   a->ev_ts.push_back(ts);
+  a->ev_ord.push_back(stream >= 0 ? a->next_ordinal++ : -1);
   if (a->ast.playback && stream != NFA_START) {
     if (ts >= a->clock) {
       a->clock = ts;
