@@ -99,7 +99,8 @@ int sm_app_set_collect(sm_app* app, int collect);
 size_t sm_app_dump_outputs(sm_app* app, char* buf, size_t len);
 
 /* Options (before the first flush): "heap_words" (per-key partial-match arena, words per semispace),
- * "batch_events" (auto-flush threshold). */
+ * "batch_events" (auto-flush threshold), "fast_general" (1 = device batches always take the general
+ * closed-form kernels), "fast_timing" (1 = record HIP events around the device-batch phases). */
 int sm_app_set_option(sm_app* app, const char* key, int64_t value);
 
 /* Device-resident batch of ONE stream (columns already in HBM, hipStream given as void*): every record is
@@ -112,6 +113,9 @@ int sm_app_process_device_batch(sm_app* app, const char* stream_id, size_t n, co
 /* Match tuples of the last device batch for a query: n pairs (e1, e2) of ordinals relative to the batch's
  * ordinal_base, uint32[2*n] in device memory, in reference output order (e2 ordinal, then e1 ordinal). */
 int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** d_pairs, size_t* n);
+/* Diagnostics of the last device batch: "fast_path:<query>" (2 = onesweep kernels, 1 = general kernels),
+ * "fast_ms:group" / "fast_ms:walk" / "fast_ms:order" (phase times in ms; needs the "fast_timing" option). */
+int sm_app_get_stat(sm_app* app, const char* key, double* out);
 
 #ifdef __cplusplus
 }

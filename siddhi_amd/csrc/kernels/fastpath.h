@@ -1,4 +1,5 @@
-// Host entry of the closed-form `every e1 -> e2 within T` kernel (fastpath.hip).
+// Host entry of the closed-form `every e1 -> e2 within T` kernels (fastpath.hip: general form;
+// fastpath2.hip: onesweep/bandwidth form for single-column keys and a single compared attribute).
 #pragma once
 #include "nfa.h"
 #include "primitives.h"
@@ -19,11 +20,35 @@ struct FastArgs {
   int64_t ordinal_base;
 };
 
-struct FastTimings {          // optional HIP events bracketing the phases (group / scan / order)
+// Host-side facts about the plan and the batch used to pick the v2 kernels.
+struct FastHostInfo {
+  const void* const* cols;    // host array of device column pointers
+  const int32_t* types;       // column types
+  int key_col = -1;           // partition key is this column (-1: expression or none)
+  int key_type = 0;
+  int vattr = -1;             // the only attribute c2 reads (-1: not eligible)
+  int vtype = 0;
+};
+
+// Persistent device state of the v2 kernels (look-back status words are epoch-tagged, never re-zeroed).
+struct FastState {
+  void* status = nullptr;
+  size_t status_bytes = 0;
+  uint32_t epoch = 0;
+  ~FastState() {
+    if (status) (void)hipFree(status);
+  }
+};
+
+struct FastTimings {          // optional HIP events: [0] start, [1] keyed sort done, [2] walk done, [3] end
   hipEvent_t ev[4];
 };
 
 int64_t fast_every_within(const FastArgs& a, uint32_t* pairs_out, int64_t pairs_cap, Scratch& sc, hipStream_t s,
                           FastTimings* tm = nullptr);
+
+// -1: outside the v2 envelope (caller falls back to fast_every_within)
+int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastState& fs, uint32_t* pairs_out,
+                             int64_t pairs_cap, Scratch& sc, hipStream_t s, FastTimings* tm = nullptr);
 
 }  // namespace sm

@@ -121,7 +121,33 @@ struct QueryRt {
   // device batch results
   DBuf dev_pairs;
   int64_t dev_n = 0;
+  FastState fast;            // v2 kernels' persistent look-back state
+  int fast_path_used = 0;    // 2 = onesweep form, 1 = general form (last device batch)
 };
+
+// v2 eligibility: c2 may read one attribute only (of e1 / e2 slots), c1 only e1, no timestamp reads.
+int fast_vattr(const CompiledQuery& cq, const std::vector<int32_t>& types) {
+  const DQuery& h = cq.hdr;
+  const Instr* code = (const Instr*)(cq.blob.data() + h.off_code);
+  int vattr = -1;
+  for (int k = 0; k < cq.fast_c2_len; ++k) {
+    const Instr& in = code[cq.fast_c2_off + k];
+    if (in.op == OP_TS || in.op == OP_COL) return -1;
+    if (in.op == OP_VAR) {
+      if (in.a < 0 || in.a > 1 || !(in.b == 0 || in.b == -1)) return -1;
+      if (vattr >= 0 && in.c != vattr) return -1;
+      vattr = in.c;
+    }
+  }
+  for (int k = 0; k < cq.fast_c1_len; ++k) {
+    const Instr& in = code[cq.fast_c1_off + k];
+    if (in.op == OP_TS) return -1;
+    if (in.op == OP_VAR && (in.a != 0 || !(in.b == 0 || in.b == -1))) return -1;
+  }
+  if (vattr < 0) vattr = 0;
+  if (vattr >= (int)types.size() || types[vattr] == T_STRING) return -1;
+  return vattr;
+}
 
 }  // namespace
 }  // namespace sm
@@ -137,6 +163,11 @@ struct sm_input {
 
 struct sm_app {
   std::mutex mu;
+  // device-batch fast path knobs (sm_app_set_option "fast_general" / "fast_timing") and the last timings
+  bool force_general_fast = false;
+  bool fast_timing = false;
+  bool fast_tm_ready = false;
+  sm::FastTimings fast_tm{};
   sql::App ast;
   sm::Dict dict;
   std::vector<sm::StreamStage> streams;
@@ -841,6 +872,14 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       for (auto& q : a->queries)
         if (q->state_slots) throw std::runtime_error("heap_words must be set before the first flush");
       a->heap_half = (int32_t)std::max<int64_t>(256, value);
+    } else if (k == "fast_general") {
+      a->force_general_fast = value != 0;
+    } else if (k == "fast_timing") {
+      if (value && !a->fast_tm_ready) {
+        for (auto& e : a->fast_tm.ev) SM_HIP(hipEventCreate(&e));
+        a->fast_tm_ready = true;
+      }
+      a->fast_timing = value != 0;
     } else if (k == "batch_events") {
       a->batch_events = std::max<int64_t>(1, value);
     } else {
@@ -908,8 +947,55 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
       fa.ordinals = d_ordinals;
       fa.ordinal_base = ordinal_base;
       q.dev_pairs.ensure(std::max<size_t>(n * 8, 16));
-      q.dev_n = fast_every_within(fa, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs);
+      std::vector<int32_t> types(d.types, d.types + d.nattr);
+      FastHostInfo hi;
+      hi.cols = d_cols;
+      hi.types = types.data();
+      hi.vattr = fast_vattr(cq, types);
+      if (hi.vattr >= 0) hi.vtype = types[hi.vattr];
+      if (fa.key) {
+        const CompiledPartition& cp = *q.part;
+        int idx = (int)(std::find(cp.streams.begin(), cp.streams.end(), s) - cp.streams.begin());
+        const auto& kc = cp.key_code[idx];
+        if (kc.size() == 1 && kc[0].op == OP_COL) {
+          hi.key_col = kc[0].a;
+          hi.key_type = types[hi.key_col];
+        }
+      }
+      int64_t m = -1;
+      if (!a->force_general_fast) m = fast_every_within_v2(fa, hi, q.fast, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs,
+                                                           a->fast_timing ? &a->fast_tm : nullptr);
+      q.fast_path_used = 2;
+      if (m < 0) {
+        m = fast_every_within(fa, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs, a->fast_timing ? &a->fast_tm : nullptr);
+        q.fast_path_used = 1;
+      }
+      q.dev_n = m;
     }
+  });
+}
+
+int sm_app_get_stat(sm_app* a, const char* key, double* out) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    std::string k = key ? key : "";
+    if (k.rfind("fast_path:", 0) == 0) {
+      for (auto& q : a->queries)
+        if (q->cq.name == k.substr(10)) {
+          *out = q->fast_path_used;
+          return;
+        }
+      throw sql::ValidationError("No query with name " + k.substr(10));
+    }
+    if (k == "fast_ms:group" || k == "fast_ms:walk" || k == "fast_ms:order") {
+      if (!a->fast_tm_ready) throw std::invalid_argument("fast_timing option is off");
+      int i = k == "fast_ms:group" ? 0 : k == "fast_ms:walk" ? 1 : 2;
+      float ms = 0;
+      SM_HIP(hipEventElapsedTime(&ms, a->fast_tm.ev[i], a->fast_tm.ev[i + 1]));
+      *out = ms;
+      return;
+    }
+    throw std::invalid_argument("unknown stat " + k);
   });
 }
 

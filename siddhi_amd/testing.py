@@ -111,3 +111,32 @@ class ProductApp:
         n = ctypes.c_size_t()
         _call(lib().sm_app_device_matches(self.h, query.encode(), ctypes.byref(p), ctypes.byref(n)))
         return p.value, n.value
+
+    def get_stat(self, key):
+        v = ctypes.c_double()
+        _call(lib().sm_app_get_stat(self.h, key.encode(), ctypes.byref(v)))
+        return v.value
+
+    def device_matches_host(self, query):
+        """Copy the last device batch's match tuples to the host: numpy uint32 array of shape (n, 2) = (e1, e2)."""
+        import numpy as np
+        p, n = self.device_matches(query)
+        out = np.empty((n, 2), dtype=np.uint32)
+        if n:
+            _hip_memcpy_d2h(out.ctypes.data, p, n * 8)
+        return out
+
+
+_hip = None
+
+
+def _hip_memcpy_d2h(dst, src, nbytes):
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _hip.hipDeviceSynchronize.argtypes = []
+    _hip.hipDeviceSynchronize()
+    rc = _hip.hipMemcpy(dst, src, nbytes, 2)  # hipMemcpyDeviceToHost
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed ({rc})")
