@@ -102,6 +102,10 @@ def cpu_baseline(sample, K, ts_div):
     return sample / dt, dt, m
 
 
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -158,8 +162,10 @@ def main():
                                  ordinal_base=0, hip_stream=ctypes.c_void_p(stream.cuda_stream))
         return app.device_matches("q")[1]
 
+    log(f"rank {rank}: {hi - lo} events resident; warmup {args.warmup}")
     for _ in range(args.warmup):
         step()
+    log(f"rank {rank}: timing {args.steps} steps")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -1,0 +1,53 @@
+"""Key sharding of a partitioned stream across GPUs (one process per GPU, torch.distributed over RCCL/xGMI).
+
+The reference runs every partition key in one JVM (PartitionStreamReceiver.receive
+core/partition/PartitionStreamReceiver.java:156 → PartitionRuntime.cloneIfNotExist core/partition/PartitionRuntime.java:256):
+keys are independent, and for one input event only the runtime of that event's key runs. So a partitioned app
+shards by key with ONE exchange step: every rank ingests a contiguous slice of the arrival order, computes
+`owner = key mod world`, and the ranks swap events with one all-to-all-v. Each rank then holds the complete
+event sequence of the keys it owns, in global arrival order (stable local order + contiguous rank slices), with
+the events' global ordinals, so the per-rank device pipeline returns exactly the reference's match tuples of
+those keys. Every event belongs to one key, hence the matches triggered by one event come from one rank and a
+merge by trigger ordinal (`merge_matches`) reproduces the reference's global output order.
+"""
+import torch
+import torch.distributed as dist
+
+
+def owner_of(keys: torch.Tensor, world: int) -> torch.Tensor:
+    """Owning rank of each key (non-negative modulo, also for negative keys)."""
+    return torch.remainder(keys.to(torch.int64), world)
+
+
+def exchange_by_key(keys: torch.Tensor, columns, world: int, group=None):
+    """All-to-all-v of `columns` (list of 1-D tensors aligned with `keys`) so that each rank receives the rows
+    whose key it owns. Returns (received columns, received counts per source rank). Row order in the result:
+    by source rank, then original order — i.e. global arrival order when rank r holds the r-th contiguous slice."""
+    if world == 1:
+        return list(columns), [keys.numel()]
+    owner = owner_of(keys, world)
+    order = torch.argsort(owner, stable=True)
+    send_counts = torch.bincount(owner, minlength=world)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    nrecv = sum(rc)
+    out = []
+    for col in columns:
+        buf = torch.empty(nrecv, dtype=col.dtype, device=col.device)
+        dist.all_to_all_single(buf, col[order].contiguous(), rc, sc, group=group)
+        out.append(buf)
+    return out, rc
+
+
+def merge_matches(parts):
+    """Merge per-rank match tuples (each an (n, 2) int array of global (e1, e2) ordinals in reference order for
+    that rank's keys) into the reference's global order: by e2 ordinal; ties (same e2) come from one rank and
+    keep that rank's order. Host-side (numpy) helper."""
+    import numpy as np
+    parts = [np.asarray(p, dtype=np.int64).reshape(-1, 2) for p in parts]
+    if not parts:
+        return np.zeros((0, 2), dtype=np.int64)
+    allp = np.concatenate(parts)
+    order = np.argsort(allp[:, 1], kind="stable")
+    return allp[order]
