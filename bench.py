@@ -121,6 +121,7 @@ def main():
     import torch
     import torch.distributed as dist
     from siddhi_amd.testing import ProductApp
+    from siddhi_amd.shard import exchange_by_key
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -139,32 +140,26 @@ def main():
 
     app = ProductApp(APP)
     stream = torch.cuda.current_stream(dev)
+    hip_stream = ctypes.c_void_p(stream.cuda_stream)
+    n_local = [hi - lo]
 
     def step():
         if world > 1:
-            owner = symbol % world
-            order = torch.argsort(owner, stable=True)
-            send_counts = torch.bincount(owner, minlength=world)
-            recv_counts = torch.empty_like(send_counts)
-            dist.all_to_all_single(recv_counts, send_counts)
-            sc, rc = send_counts.tolist(), recv_counts.tolist()
-            nrecv = sum(rc)
-            out = []
-            for t in (symbol, price, ts, ordinals):
-                buf = torch.empty(nrecv, dtype=t.dtype, device=dev)
-                dist.all_to_all_single(buf, t[order], rc, sc)
-                out.append(buf)
-            s_sym, s_price, s_ts, s_ord = out
+            (s_sym, s_price, s_ts, s_ord), _ = exchange_by_key(symbol, [symbol, price, ts, ordinals], world)
         else:
             s_sym, s_price, s_ts, s_ord = symbol, price, ts, None
+        n_local[0] = s_ts.numel()
         # columns: symbol, price, volume, timestamp (volume/timestamp are not read by the plan)
         app.process_device_batch("StockStream", s_ts, [s_sym, s_price, s_price, s_price], ordinals=s_ord,
-                                 ordinal_base=0, hip_stream=ctypes.c_void_p(stream.cuda_stream))
+                                 ordinal_base=0, hip_stream=hip_stream)
         return app.device_matches("q")[1]
 
     log(f"rank {rank}: {hi - lo} events resident; warmup {args.warmup}")
     for _ in range(args.warmup):
         step()
+    # per-launch HIP events inside the library, on the launch stream (a few event records per step)
+    app.set_option("fast_timing", 1)
+    ktot = {}
     log(f"rank {rank}: timing {args.steps} steps")
     torch.cuda.synchronize()
     if world > 1:
@@ -174,6 +169,12 @@ def main():
     nm = 0
     for _ in range(args.steps):
         nm = step()
+        for lab in KERNELS:  # the library synchronised its stream before returning: the marks are complete
+            c = app.get_stat("kernel_calls:" + lab)
+            if c:
+                e = ktot.setdefault(lab, [0.0, 0])
+                e[0] += app.get_stat("kernel_ms:" + lab)
+                e[1] += int(c)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -188,13 +189,10 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = N / (dt / args.steps)
 
-    # roofline of the dominant kernel phase, timed with HIP events on the launch stream
-    roof = None
-    prof = profile_phases(app, symbol, price, ts, stream) if world == 1 else None
-    if prof:
-        roof = prof
+    roof = roofline(ktot, n_local[0], nm, args.steps)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
+        log(f"cpu baseline on {args.cpu_sample} events")
         v, sec, mm = cpu_baseline(args.cpu_sample, K, args.ts_div)
         cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port",
                "sample": f"first {args.cpu_sample} events of the same stream through oracle/cpu_ref "
@@ -217,25 +215,38 @@ def main():
         dist.destroy_process_group()
 
 
-def profile_phases(app, symbol, price, ts, stream):
-    """Re-run one step with HIP events bracketing the phases inside the library (key grouping sort, forward
-    scan, output ordering) and report the dominant phase against HBM peak."""
-    import torch
-    from siddhi_amd import _lib
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    # whole-step time on the launch stream
-    evs[0].record(stream)
-    app.process_device_batch("StockStream", ts, [symbol, price, price, price], ordinals=None, ordinal_base=0,
-                             hip_stream=ctypes.c_void_p(stream.cuda_stream))
-    evs[1].record(stream)
-    torch.cuda.synchronize()
-    ms = evs[0].elapsed_time(evs[1])
-    n = ts.numel()
-    m = app.device_matches("q")[1]
-    alg = 20 * n + 8 * m  # SURVEY §8(d) config 4: key i32 + price f64 + ts i64 in, (i, j) u32 pairs out
-    ach = alg / (ms * 1e-3)
+# Kernels of the device pipeline (labels recorded by kernels/fastpath2.hip) and their ALGORITHMIC bytes per
+# launch for a batch of n events with m matches: what each launch must read and write at minimum.
+KERNELS = ["prep", "key_hist", "hist_scan", "key_pass0", "key_pass", "walk", "j_hist", "j_pass", "j_pass_last"]
+
+
+def alg_bytes(label, n, m):
+    return {"prep": 12 * n,                 # key i32 + ts i64
+            "key_hist": 4 * n,              # key i32
+            "hist_scan": 0,
+            "key_pass0": 20 * n + 20 * n,   # key + price + ts in, 20-B keyed record out
+            "key_pass": 20 * n + 20 * n,    # 20-B record in and out
+            "walk": 20 * n + 8 * m,         # records in, (j, i) u32 pairs out
+            "j_hist": 4 * m,
+            "j_pass": 16 * m,               # (j, i) in and out
+            "j_pass_last": 16 * m}[label]
+
+
+def roofline(ktot, n, m, steps):
+    """Dominant kernel (largest total time over the timed steps): algorithmic bytes per launch / average launch
+    duration, against HBM peak. Also the per-kernel breakdown."""
+    if not ktot:
+        return None
+    dom = max(ktot, key=lambda k: ktot[k][0])
+    tot_ms, calls = ktot[dom]
+    avg_ms = tot_ms / calls
+    per_launch = alg_bytes(dom, n, m)
+    ach = per_launch / (avg_ms * 1e-3)
+    brk = {k: {"avg_ms": v[0] / v[1], "calls_per_step": v[1] / steps,
+               "gbps": alg_bytes(k, n, m) / (v[0] / v[1] * 1e-3) / 1e9} for k, v in ktot.items()}
     return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
-            "traffic": None, "kernel": "fast_every_within pipeline (whole step)", "ms": ms}
+            "traffic": None, "kernel": dom, "avg_launch_ms": avg_ms, "alg_bytes_per_launch": per_launch,
+            "breakdown": brk}
 
 
 if __name__ == "__main__":

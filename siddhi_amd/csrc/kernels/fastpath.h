@@ -28,6 +28,8 @@ struct FastHostInfo {
   int key_type = 0;
   int vattr = -1;             // the only attribute c2 reads (-1: not eligible)
   int vtype = 0;
+  const Instr* c2_host = nullptr;  // host copy of the c2 program (specialisation of the walk's compare)
+  int c2_len = 0;
 };
 
 // Persistent device state of the v2 kernels (look-back status words are epoch-tagged, never re-zeroed).
@@ -42,6 +44,17 @@ struct FastState {
 
 struct FastTimings {          // optional HIP events: [0] start, [1] keyed sort done, [2] walk done, [3] end
   hipEvent_t ev[4];
+  // per-launch marks of the v2 pipeline: mk[0] before the first kernel, mk[k] after the k-th, label[k] its kernel
+  static constexpr int kMaxMarks = 32;
+  hipEvent_t mk[kMaxMarks];
+  const char* label[kMaxMarks];
+  int nmk = 0;
+  void mark(const char* l, hipStream_t s) {
+    if (nmk < kMaxMarks) {
+      label[nmk] = l;
+      (void)hipEventRecord(mk[nmk++], s);
+    }
+  }
 };
 
 int64_t fast_every_within(const FastArgs& a, uint32_t* pairs_out, int64_t pairs_cap, Scratch& sc, hipStream_t s,

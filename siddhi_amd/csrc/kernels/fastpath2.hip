@@ -18,6 +18,7 @@
 // contiguous stores.
 #include "expr.h"
 #include "fastpath.h"
+#include "lookback.h"
 
 namespace sm {
 
@@ -34,7 +35,9 @@ constexpr uint32_t kKeyMask = 0x7fffffffu;
 constexpr int kWalkBlock = 256;
 constexpr int kWalkItems = 8;
 constexpr int kWalkTile = kWalkBlock * kWalkItems;
-constexpr unsigned long long kSpinLimit = 1ull << 26;
+constexpr int kWalkHalo = 256;  // records staged past the tile for scans that leave it
+constexpr int kWalkLds = kWalkTile + kWalkHalo;
+constexpr int kLookW = 8;  // look-back window (independent status loads per step)
 
 static_assert(kBins % kBlock == 0, "bins per thread");
 
@@ -108,6 +111,65 @@ __device__ __forceinline__ bool eval_cond(const Instr* code, int len, const DVal
     return do_compare(code[2], l, r);
   }
   return truthy(eval_prog(code, len, consts, ld));
+}
+
+// A condition program decoded once per thread: its kernel-uniform instructions and constants stay in scalar
+// registers across the scan loops instead of being re-read every iteration.
+struct Cond {
+  const Instr* code;
+  int len;
+  const DVal* consts;
+  bool simple;  // `x CMP y` with x, y variables or constants
+  Instr a, b, op;
+  StackVal ka, kb;
+};
+
+__device__ __forceinline__ StackVal const_val(const DVal* consts, int k) {
+  const DVal c = consts[k];
+  StackVal v;
+  v.i = c.i;
+  v.d = c.d;
+  v.null = c.null;
+  return v;
+}
+
+__device__ __forceinline__ Cond make_cond(const Instr* code, int len, const DVal* consts) {
+  Cond c;
+  c.code = code;
+  c.len = len;
+  c.consts = consts;
+  c.simple = len == 3 && code[2].op == OP_CMP && code[0].op != OP_CMP && code[1].op != OP_CMP &&
+             code[0].op != OP_MATH && code[1].op != OP_MATH && code[0].op != OP_NOT && code[1].op != OP_NOT;
+  if (c.simple) {
+    c.a = code[0];
+    c.b = code[1];
+    c.op = code[2];
+    if (c.a.op == OP_CONST) c.ka = const_val(consts, c.a.a);
+    if (c.b.op == OP_CONST) c.kb = const_val(consts, c.b.a);
+  }
+  return c;
+}
+
+template <typename Ld>
+__device__ __forceinline__ bool eval(const Cond& c, const Ld& ld) {
+  if (c.len == 0) return true;
+  if (c.simple) {
+    const StackVal l = c.a.op == OP_CONST ? c.ka : ld.var(c.a);
+    const StackVal r = c.b.op == OP_CONST ? c.kb : ld.var(c.b);
+    if (l.null || r.null) return c.op.sub == CMP_NE;
+    return do_compare(c.op, l, r);
+  }
+  return truthy(eval_prog(c.code, c.len, c.consts, ld));
+}
+
+template <int OP, typename T>
+__device__ __forceinline__ bool cmp_fixed(T x, T y) {
+  if constexpr (OP == CMP_EQ) return x == y;
+  else if constexpr (OP == CMP_NE) return x != y;
+  else if constexpr (OP == CMP_LT) return x < y;
+  else if constexpr (OP == CMP_LE) return x <= y;
+  else if constexpr (OP == CMP_GT) return x > y;
+  else return x >= y;
 }
 
 // e1-only program on an original row (c1)
@@ -230,27 +292,37 @@ __global__ void __launch_bounds__(kBlock) hist_scan_kernel(uint32_t* __restrict_
 // ---------------------------------------------------------------- onesweep pass
 
 // record sources / sinks
-struct OrigSrc {  // pass 0 of the keyed sort: builds the record from the original columns
+// canonical 64-bit image of a typed column value (as canon(), with the column type fixed at compile time)
+template <typename VT>
+__device__ __forceinline__ uint64_t canon_t(VT v) {
+  if constexpr (std::is_floating_point<VT>::value) return (uint64_t)__double_as_longlong((double)v);
+  else return (uint64_t)(int64_t)v;
+}
+
+// Pass 0 of the keyed sort: builds the record from the original columns. Key and compared-attribute column
+// types are template parameters (no per-element type switch in the unrolled item loops); c1 is evaluated by
+// c1(), once per event, outside the unrolled loops.
+template <typename KT, typename VT>
+struct OrigSrc {
+  static constexpr bool kC1 = true;
   const NfaStream* st;
-  const void* kcol;
-  int ktype;
+  const KT* kcol;
+  const VT* vcol;
   int64_t kmin;
-  const Instr* c1;
+  const Instr* c1p;
   int c1_len;
   const DVal* consts;
-  int vattr, vtype;
   const int64_t* ts;
   int64_t ts0;
   const int64_t* ord;
   int64_t obase;
-  __device__ uint32_t key(int64_t p) const {
-    int64_t k = ktype == T_INT ? (int64_t)((const int32_t*)kcol)[p] : ((const int64_t*)kcol)[p];
+  __device__ uint32_t key(int64_t p) const { return (uint32_t)((int64_t)kcol[p] - kmin); }
+  __device__ bool c1(int64_t p) const {
     RowLoader ld{st, p};
-    const bool c = eval_cond(c1, c1_len, consts, ld);
-    return (uint32_t)(k - kmin) | (c ? 0x80000000u : 0u);
+    return eval_cond(c1p, c1_len, consts, ld);
   }
   __device__ uint32_t f0(int64_t p) const { return ord ? (uint32_t)(ord[p] - obase) : (uint32_t)p; }
-  __device__ uint64_t f1(int64_t p) const { return canon(col_value(st, vattr, p), vtype); }
+  __device__ uint64_t f1(int64_t p) const { return canon_t(vcol[p]); }
   __device__ uint32_t f2(int64_t p) const { return (uint32_t)(ts[p] - ts0); }
 };
 
@@ -262,6 +334,7 @@ struct RecSoA {  // keyed record, structure of arrays
 };
 
 struct RecSrc {
+  static constexpr bool kC1 = false;
   const uint32_t* k;
   const uint32_t* f0;
   const uint64_t* f1;
@@ -269,42 +342,6 @@ struct RecSrc {
   __device__ uint32_t key(int64_t p) const { return k[p]; }
   __device__ uint32_t g0(int64_t p) const { return f0[p]; }
 };
-
-// status word: epoch(30) | flag(2) | value(32); flag 1 = tile aggregate, 2 = inclusive prefix
-__device__ __forceinline__ void st_put(unsigned long long* p, uint32_t epoch, uint32_t flag, uint32_t v) {
-  __hip_atomic_store(p, ((unsigned long long)epoch << 34) | ((unsigned long long)flag << 32) | v, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// exclusive prefix of `cnt` over all earlier tiles for one lane-owned counter
-__device__ __forceinline__ uint32_t lookback(unsigned long long* status, int64_t stride, int64_t tile, uint32_t epoch,
-                                             uint32_t cnt, unsigned int* err) {
-  if (tile == 0) {
-    st_put(status, epoch, 2, cnt);
-    return 0;
-  }
-  st_put(status + tile * stride, epoch, 1, cnt);
-  uint32_t excl = 0;
-  int64_t p = tile - 1;
-  unsigned long long spins = 0;
-  while (true) {
-    unsigned long long s = __hip_atomic_load(status + p * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t flag = (uint32_t)(s >> 32) & 3u;
-    if ((uint32_t)(s >> 34) != epoch || flag == 0) {
-      if (++spins > kSpinLimit) {
-        atomicOr(err, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    excl += (uint32_t)s;
-    if (flag == 2) break;
-    --p;
-  }
-  st_put(status + tile * stride, epoch, 2, excl + cnt);
-  return excl;
-}
 
 // Shared onesweep core: ranks the tile's keys, runs the per-digit look-back and leaves, in LDS, for every
 // record its local sorted position and every digit's global base. MODE selects the record layout moved.
@@ -320,13 +357,13 @@ __global__ void __launch_bounds__(kBlock) onesweep_kernel(Src src, RecSoA dst, u
                                                           unsigned long long* __restrict__ status, uint32_t epoch,
                                                           unsigned int* __restrict__ tile_ctr,
                                                           unsigned int* __restrict__ err) {
-  __shared__ uint64_t xbuf[kTile];
+  __shared__ uint32_t xb32[kTile];  // exchange buffer, one 32-bit field at a time (u64 fields in two halves)
   __shared__ uint16_t wcnt[kWaves][kBins];
   __shared__ uint32_t tstart[kBins];
   __shared__ uint32_t gbase[kBins];
+  __shared__ uint32_t tcnt[kBins];
   __shared__ uint32_t lw[kWaves];
   __shared__ uint32_t sh_tile;
-  uint32_t* xb32 = (uint32_t*)xbuf;
 
   const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
   if (threadIdx.x == 0) sh_tile = atomicAdd(tile_ctr, 1u);
@@ -339,6 +376,14 @@ __global__ void __launch_bounds__(kBlock) onesweep_kernel(Src src, RecSoA dst, u
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = lanemask_lt();
 
+  uint32_t c1m = 0;  // c1 flag of each item (bit k), evaluated in a rolled loop to keep the code compact
+  if constexpr (Src::kC1) {
+#pragma unroll 1
+    for (int k = 0; k < kItems; ++k) {
+      const int e = w * 64 * kItems + k * 64 + lane;
+      if (e < tile_n && src.c1(base + e)) c1m |= 1u << k;
+    }
+  }
   uint32_t keys[kItems];
   uint32_t lp[kItems];  // rank within (wave, digit), then local sorted position
 #pragma unroll
@@ -346,7 +391,7 @@ __global__ void __launch_bounds__(kBlock) onesweep_kernel(Src src, RecSoA dst, u
     const int e = w * 64 * kItems + k * 64 + lane;
     const bool valid = e < tile_n;
     uint32_t key = 0;
-    if (valid) key = src.key(base + e);
+    if (valid) key = src.key(base + e) | (((c1m >> k) & 1u) << 31);
     keys[k] = key;
     const uint32_t d = ((key & kKeyMask) >> shift) & (kBins - 1);
     uint64_t peers = __ballot(valid);
@@ -397,11 +442,14 @@ __global__ void __launch_bounds__(kBlock) onesweep_kernel(Src src, RecSoA dst, u
       run += cnt[b];
     }
   }
-  // decoupled look-back per digit
+  // decoupled look-back per digit; lanes take consecutive digits so each status read is coalesced
+#pragma unroll
+  for (int b = 0; b < kBinsPerThread; ++b) tcnt[threadIdx.x * kBinsPerThread + b] = cnt[b];
+  __syncthreads();
 #pragma unroll
   for (int b = 0; b < kBinsPerThread; ++b) {
-    const int d = threadIdx.x * kBinsPerThread + b;
-    const uint32_t excl = lookback(status + d, kBins, tile, epoch, cnt[b], err);
+    const int d = b * kBlock + threadIdx.x;
+    const uint32_t excl = lookback_win<kLookW>(status + d, kBins, tile, epoch, tcnt[d], err);
     gbase[d] = gstart[d] + excl;
   }
   __syncthreads();
@@ -430,18 +478,24 @@ __global__ void __launch_bounds__(kBlock) onesweep_kernel(Src src, RecSoA dst, u
     }
   }
 
-  if constexpr (MODE == 3) {  // (j, i) → interleaved (i, j): one 8-byte exchange
+  if constexpr (MODE == 3) {  // (j, i) → interleaved (i, j): j is already in xb32 at the sorted slots
+    uint32_t jj[kItems];
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+      const int s = r * kBlock + threadIdx.x;
+      jj[r] = s < tile_n ? xb32[s] : 0u;
+    }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int e = w * 64 * kItems + k * 64 + lane;
-      if (e < tile_n) xbuf[lp[k]] = ((uint64_t)keys[k] << 32) | src.g0(base + e);
+      if (e < tile_n) xb32[lp[k]] = src.g0(base + e);
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
       const int s = r * kBlock + threadIdx.x;
-      if (s < tile_n) dpairs[dest[r]] = xbuf[s];
+      if (s < tile_n) dpairs[dest[r]] = ((uint64_t)jj[r] << 32) | xb32[s];
     }
     return;
   } else {
@@ -465,21 +519,38 @@ __global__ void __launch_bounds__(kBlock) onesweep_kernel(Src src, RecSoA dst, u
       }
     }
     if constexpr (MODE == 0 || MODE == 1) {
-      // payload field 1 (u64)
+      // payload field 1 (u64), low then high half
+      uint32_t hi[kItems];
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < kItems; ++k) {
         const int e = w * 64 * kItems + k * 64 + lane;
         if (e < tile_n) {
-          if constexpr (MODE == 0) xbuf[lp[k]] = src.f1(base + e);
-          else xbuf[lp[k]] = src.f1[base + e];
+          uint64_t x;
+          if constexpr (MODE == 0) x = src.f1(base + e);
+          else x = src.f1[base + e];
+          xb32[lp[k]] = (uint32_t)x;
+          hi[k] = (uint32_t)(x >> 32);
         }
+      }
+      __syncthreads();
+      uint32_t lo[kItems];
+#pragma unroll
+      for (int r = 0; r < kItems; ++r) {
+        const int s = r * kBlock + threadIdx.x;
+        lo[r] = s < tile_n ? xb32[s] : 0u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) {
+        const int e = w * 64 * kItems + k * 64 + lane;
+        if (e < tile_n) xb32[lp[k]] = hi[k];
       }
       __syncthreads();
 #pragma unroll
       for (int r = 0; r < kItems; ++r) {
         const int s = r * kBlock + threadIdx.x;
-        if (s < tile_n) dst.f1[dest[r]] = xbuf[s];
+        if (s < tile_n) dst.f1[dest[r]] = ((uint64_t)xb32[s] << 32) | lo[r];
       }
       // payload field 2 (u32)
       __syncthreads();
@@ -502,6 +573,7 @@ __global__ void __launch_bounds__(kBlock) onesweep_kernel(Src src, RecSoA dst, u
 }
 
 struct PairSrc {
+  static constexpr bool kC1 = false;
   const uint32_t* j;
   const uint32_t* i;
   __device__ uint32_t key(int64_t p) const { return j[p]; }
@@ -509,6 +581,12 @@ struct PairSrc {
 };
 
 // ---------------------------------------------------------------- walk
+//
+// One lane per record (tile order = record order, so the look-back compaction keeps matches in record order).
+// The tile's records plus a halo of the next kWalkHalo records are staged into LDS with coalesced loads; every
+// forward scan reads LDS and leaves it only when a key run (keyed) or a window (unkeyed) runs past the halo,
+// where it continues from global memory. A scan stops at the first event satisfying c2 (match), at the end of
+// the key run, or when the window closes.
 
 struct WalkArgs {
   // keyed (sorted records) or original columns
@@ -531,12 +609,80 @@ struct WalkArgs {
 };
 
 template <bool KEYED>
+struct WalkLds;
+template <>
+struct WalkLds<true> {
+  uint64_t v[kWalkLds];
+  uint32_t k[kWalkLds];
+  uint32_t t[kWalkLds];
+};
+template <>
+struct WalkLds<false> {
+  uint64_t v[kWalkLds];
+  int64_t t[kWalkLds];
+};
+
+// Forward scan of one partial (record lu of the tile, keyed: c1 already known to hold). Returns the position
+// of the first event satisfying c2 inside the key run (keyed) and the window, or -1.
+// c2 as a fixed compare `e2.x OP e1.x` over the carried attribute (OP >= 0; FP: compared as double, else as
+// int64 — exact for every column type the spec admits), or the generic condition program (OP < 0).
+template <int OP, bool FP>
+struct C2 {
+  Cond c;
+  int vtype;
+  __device__ __forceinline__ bool operator()(uint64_t v1, uint64_t v2) const {
+    if constexpr (OP < 0) {
+      return eval(c, PairLoader{v1, v2, vtype});
+    } else {
+      if constexpr (FP) return cmp_fixed<OP>(__longlong_as_double((long long)v2), __longlong_as_double((long long)v1));
+      else return cmp_fixed<OP>((int64_t)v2, (int64_t)v1);
+    }
+  }
+};
+
+template <bool KEYED, typename CF>
+__device__ __forceinline__ int64_t scan_partial(const WalkArgs& a, const WalkLds<KEYED>& L, const CF& c2,
+                                                int64_t base, int64_t lend, int lu) {
+  const int64_t n = a.n;
+  const uint64_t vu = L.v[lu];
+  int64_t v = base + lu + 1;
+  if constexpr (KEYED) {
+    const uint32_t key = L.k[lu] & kKeyMask, tu = L.t[lu];
+    for (; v < lend; ++v) {  // staged records
+      const int lv = (int)(v - base);
+      if ((L.k[lv] & kKeyMask) != key || (a.within >= 0 && (int64_t)(L.t[lv] - tu) > a.within)) return -1;
+      if (c2(vu, L.v[lv])) return v;
+    }
+    for (; v < n; ++v) {  // the key run continues past the halo
+      if ((a.k[v] & kKeyMask) != key || (a.within >= 0 && (int64_t)(a.f2[v] - tu) > a.within)) return -1;
+      if (c2(vu, a.f1[v])) return v;
+    }
+  } else {
+    const int64_t tu = L.t[lu];
+    for (; v < lend; ++v) {
+      const int64_t d = L.t[v - base] - tu;
+      if (a.within >= 0 && (d < 0 ? -d : d) > a.within) return -1;
+      if (c2(vu, L.v[v - base])) return v;
+    }
+    for (; v < n; ++v) {
+      const int64_t d = a.ts[v] - tu;
+      if (a.within >= 0 && (d < 0 ? -d : d) > a.within) return -1;
+      if (c2(vu, canon(col_value(a.st, a.vattr, v), a.vtype))) return v;
+    }
+  }
+  return -1;
+}
+
+template <bool KEYED, int OP, bool FP>
 __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, uint32_t* __restrict__ mj,
                                                           uint32_t* __restrict__ mi,
                                                           unsigned long long* __restrict__ status, uint32_t epoch,
                                                           unsigned int* __restrict__ tile_ctr,
                                                           unsigned int* __restrict__ nmatch,
                                                           unsigned int* __restrict__ err) {
+  __shared__ WalkLds<KEYED> L;
+  __shared__ uint32_t sj[kWalkItems][kWalkBlock];      // matched position of each item (valid where bal bit set)
+  __shared__ uint64_t sbal[kWalkBlock / 64][kWalkItems];
   __shared__ uint32_t wtot[kWalkBlock / 64];
   __shared__ uint32_t sh_tile, sh_base;
   if (threadIdx.x == 0) sh_tile = atomicAdd(tile_ctr, 1u);
@@ -545,83 +691,79 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, uint32_t* 
   const int64_t base = tile * kWalkTile;
   const int64_t n = a.n;
   if (base >= n) return;
+  const int nload = (int)((n - base) < kWalkLds ? (n - base) : kWalkLds);
+  for (int e = threadIdx.x; e < nload; e += kWalkBlock) {
+    const int64_t p = base + e;
+    if constexpr (KEYED) {
+      L.k[e] = a.k[p];
+      L.t[e] = a.f2[p];
+      L.v[e] = a.f1[p];
+    } else {
+      L.t[e] = a.ts[p];
+      L.v[e] = canon(col_value(a.st, a.vattr, p), a.vtype);
+    }
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = lanemask_lt();
-  uint32_t jv[kWalkItems], iv[kWalkItems];
-  uint64_t hm[kWalkItems];
-  uint32_t mine = 0;  // matches of this wave before item k (running, wave-uniform)
-  uint32_t woff[kWalkItems];
-#pragma unroll
+  const int64_t lend = base + nload;
+  C2<OP, FP> c2;
+  if constexpr (OP < 0) c2.c = make_cond(a.c2, a.c2_len, a.consts);
+  c2.vtype = a.vtype;
+  Cond c1;
+  if constexpr (!KEYED) c1 = make_cond(a.c1, a.c1_len, a.consts);
+  uint32_t mine = 0;  // matches of this wave (wave-uniform)
+  // items in a rolled loop (one copy of the scan code); per-item results go through LDS
+#pragma unroll 1
   for (int k = 0; k < kWalkItems; ++k) {
-    const int64_t u = base + w * 64 * kWalkItems + k * 64 + lane;
-    bool has = false;
-    uint32_t j = 0, i = 0;
+    const int lu = w * 64 * kWalkItems + k * 64 + lane;
+    const int64_t u = base + lu;
+    int64_t hit = -1;
     if (u < n) {
-      if constexpr (KEYED) {
-        const uint32_t ku = a.k[u];
-        if (ku >> 31) {
-          const uint32_t key = ku & kKeyMask, tu = a.f2[u];
-          const uint64_t vu = a.f1[u];
-          for (int64_t v = u + 1; v < n; ++v) {
-            const uint32_t kv = a.k[v];
-            if ((kv & kKeyMask) != key) break;
-            if (a.within >= 0 && (int64_t)(a.f2[v] - tu) > a.within) break;
-            PairLoader ld{vu, a.f1[v], a.vtype};
-            if (eval_cond(a.c2, a.c2_len, a.consts, ld)) {
-              has = true;
-              j = a.f0[v];
-              i = a.f0[u];
-              break;
-            }
-          }
-        }
-      } else {
-        RowLoader rl{a.st, u};
-        if (eval_cond(a.c1, a.c1_len, a.consts, rl)) {
-          const int64_t tu = a.ts[u];
-          const uint64_t vu = canon(col_value(a.st, a.vattr, u), a.vtype);
-          for (int64_t v = u + 1; v < n; ++v) {
-            const int64_t d = a.ts[v] - tu;
-            if (a.within >= 0 && (d < 0 ? -d : d) > a.within) break;
-            PairLoader ld{vu, canon(col_value(a.st, a.vattr, v), a.vtype), a.vtype};
-            if (eval_cond(a.c2, a.c2_len, a.consts, ld)) {
-              has = true;
-              j = a.ord ? (uint32_t)(a.ord[v] - a.obase) : (uint32_t)v;
-              i = a.ord ? (uint32_t)(a.ord[u] - a.obase) : (uint32_t)u;
-              break;
-            }
-          }
-        }
-      }
+      bool c1u;
+      if constexpr (KEYED) c1u = (L.k[lu] >> 31) != 0;
+      else c1u = eval(c1, RowLoader{a.st, u});
+      if (c1u) hit = scan_partial<KEYED>(a, L, c2, base, lend, lu);
     }
-    const uint64_t bal = __ballot(has);
-    hm[k] = bal;
-    woff[k] = mine + (uint32_t)__popcll(bal & lt);
+    const uint64_t bal = __ballot(hit >= 0);
+    if (hit >= 0) sj[k][threadIdx.x] = (uint32_t)(hit - base);  // < 2^31: offset inside or past the tile
+    if (lane == 0) sbal[w][k] = bal;
     mine += (uint32_t)__popcll(bal);
-    jv[k] = j;
-    iv[k] = i;
   }
   if (lane == 0) wtot[w] = mine;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
+  if (threadIdx.x < 64) {
+    uint32_t t = 0, mywt = 0;
     for (int q = 0; q < kWalkBlock / 64; ++q) {
       const uint32_t c = wtot[q];
-      wtot[q] = t;
+      if (q == lane) mywt = t;
       t += c;
     }
-    const uint32_t excl = lookback(status, 1, tile, epoch, t, err);
-    sh_base = excl;
-    if (base + kWalkTile >= n) *nmatch = excl + t;  // last tile publishes the total
+    const uint32_t excl = lookback_wave(status, tile, epoch, t, err);
+    if (lane < kWalkBlock / 64) wtot[lane] = mywt;
+    if (lane == 0) {
+      sh_base = excl;
+      if (base + kWalkTile >= n) *nmatch = excl + t;  // last tile publishes the total
+    }
   }
   __syncthreads();
-  const uint32_t ob = sh_base + wtot[w];
-#pragma unroll
+  uint32_t ob = sh_base + wtot[w];
+#pragma unroll 1
   for (int k = 0; k < kWalkItems; ++k) {
-    if ((hm[k] >> lane) & 1ull) {
-      mj[ob + woff[k]] = jv[k];
-      mi[ob + woff[k]] = iv[k];
+    const uint64_t bal = sbal[w][k];
+    if ((bal >> lane) & 1ull) {
+      const uint32_t pos = ob + (uint32_t)__popcll(bal & lt);
+      const int64_t u = base + w * 64 * kWalkItems + k * 64 + lane;
+      const int64_t v = base + sj[k][threadIdx.x];
+      if constexpr (KEYED) {
+        mj[pos] = a.f0[v];
+        mi[pos] = a.f0[u];
+      } else {
+        mj[pos] = a.ord ? (uint32_t)(a.ord[v] - a.obase) : (uint32_t)v;
+        mi[pos] = a.ord ? (uint32_t)(a.ord[u] - a.obase) : (uint32_t)u;
+      }
     }
+    ob += (uint32_t)__popcll(bal);
   }
 }
 
@@ -632,6 +774,87 @@ inline int bits_for(uint64_t v) {
 }
 
 }  // namespace
+
+template <typename KT, typename VT>
+void launch_pass0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int64_t ts0,
+                    unsigned grid, hipStream_t s, RecSoA dst, const uint32_t* hist, unsigned long long* status,
+                    uint32_t epoch, unsigned int* ctr, unsigned int* err) {
+  OrigSrc<KT, VT> os{a.st, (const KT*)kcol, (const VT*)hi.cols[hi.vattr], kmin, a.code + a.c1_off, a.c1_len,
+                     a.consts, a.ts, ts0, a.ordinals, a.ordinal_base};
+  hipLaunchKernelGGL((onesweep_kernel<0, OrigSrc<KT, VT>>), dim3(grid), dim3(kBlock), 0, s, os, dst, nullptr,
+                     nullptr, nullptr, a.n, nullptr, 0, hist, status, epoch, ctr, err);
+}
+
+template <typename KT>
+void launch_pass0_k(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int64_t ts0,
+                    unsigned grid, hipStream_t s, RecSoA dst, const uint32_t* hist, unsigned long long* status,
+                    uint32_t epoch, unsigned int* ctr, unsigned int* err) {
+  switch (hi.vtype) {
+    case T_INT: launch_pass0_t<KT, int32_t>(hi, a, kcol, kmin, ts0, grid, s, dst, hist, status, epoch, ctr, err); break;
+    case T_LONG: launch_pass0_t<KT, int64_t>(hi, a, kcol, kmin, ts0, grid, s, dst, hist, status, epoch, ctr, err); break;
+    case T_FLOAT: launch_pass0_t<KT, float>(hi, a, kcol, kmin, ts0, grid, s, dst, hist, status, epoch, ctr, err); break;
+    case T_DOUBLE: launch_pass0_t<KT, double>(hi, a, kcol, kmin, ts0, grid, s, dst, hist, status, epoch, ctr, err); break;
+    default: throw std::runtime_error("fast path: unsupported compared-attribute type");
+  }
+}
+
+void launch_pass0(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int64_t ts0,
+                  unsigned grid, hipStream_t s, RecSoA dst, const uint32_t* hist, unsigned long long* status,
+                  uint32_t epoch, unsigned int* ctr, unsigned int* err) {
+  if (hi.key_type == T_INT) launch_pass0_k<int32_t>(hi, a, kcol, kmin, ts0, grid, s, dst, hist, status, epoch, ctr, err);
+  else launch_pass0_k<int64_t>(hi, a, kcol, kmin, ts0, grid, s, dst, hist, status, epoch, ctr, err);
+}
+
+// Compare spec of c2 for the walk: op * 2 + fp, normalised to `e2.x OP e1.x`, or -1 (generic program).
+// Admitted: `eK.x CMP eL.x` over the carried attribute, one operand per slot, compared in its own type.
+int c2_spec(const FastHostInfo& hi) {
+  if (!hi.c2_host || hi.c2_len != 3) return -1;
+  const Instr* c = hi.c2_host;
+  if (c[0].op != OP_VAR || c[1].op != OP_VAR || c[2].op != OP_CMP) return -1;
+  if (c[0].c != hi.vattr || c[1].c != hi.vattr || c[0].a == c[1].a) return -1;
+  const int ct = c[2].t0;
+  const bool ok = (hi.vtype == T_DOUBLE && ct == CT_DOUBLE) || (hi.vtype == T_FLOAT && ct == CT_FLOAT) ||
+                  (hi.vtype == T_INT && ct == CT_INT) || (hi.vtype == T_LONG && ct == CT_LONG);
+  if (!ok) return -1;
+  int op = c[2].sub;
+  if (c[0].a == 0) {  // e1 OP e2  →  e2 OP' e1
+    static const int flip[6] = {CMP_EQ, CMP_NE, CMP_GT, CMP_GE, CMP_LT, CMP_LE};
+    op = flip[op];
+  }
+  const bool fp = hi.vtype == T_DOUBLE || hi.vtype == T_FLOAT;
+  return op * 2 + (fp ? 1 : 0);
+}
+
+template <bool KEYED, int OP, bool FP>
+void launch_walk_t(int64_t tiles, hipStream_t s, const WalkArgs& wa, uint32_t* mj, uint32_t* mi,
+                   unsigned long long* status, uint32_t epoch, unsigned int* ctr, unsigned int* nmatch,
+                   unsigned int* err) {
+  hipLaunchKernelGGL((walk_kernel<KEYED, OP, FP>), dim3((unsigned)tiles), dim3(kWalkBlock), 0, s, wa, mj, mi, status,
+                     epoch, ctr, nmatch, err);
+}
+
+template <bool KEYED>
+void launch_walk(int spec, int64_t tiles, hipStream_t s, const WalkArgs& wa, uint32_t* mj, uint32_t* mi,
+                 unsigned long long* status, uint32_t epoch, unsigned int* ctr, unsigned int* nmatch,
+                 unsigned int* err) {
+#define SM_WALK(OP, FP) launch_walk_t<KEYED, OP, FP>(tiles, s, wa, mj, mi, status, epoch, ctr, nmatch, err)
+  switch (spec) {
+    case CMP_EQ * 2: SM_WALK(CMP_EQ, false); break;
+    case CMP_EQ * 2 + 1: SM_WALK(CMP_EQ, true); break;
+    case CMP_NE * 2: SM_WALK(CMP_NE, false); break;
+    case CMP_NE * 2 + 1: SM_WALK(CMP_NE, true); break;
+    case CMP_LT * 2: SM_WALK(CMP_LT, false); break;
+    case CMP_LT * 2 + 1: SM_WALK(CMP_LT, true); break;
+    case CMP_LE * 2: SM_WALK(CMP_LE, false); break;
+    case CMP_LE * 2 + 1: SM_WALK(CMP_LE, true); break;
+    case CMP_GT * 2: SM_WALK(CMP_GT, false); break;
+    case CMP_GT * 2 + 1: SM_WALK(CMP_GT, true); break;
+    case CMP_GE * 2: SM_WALK(CMP_GE, false); break;
+    case CMP_GE * 2 + 1: SM_WALK(CMP_GE, true); break;
+    default: SM_WALK(-1, false); break;
+  }
+#undef SM_WALK
+}
 
 // Returns -1 when the batch is outside the v2 envelope (caller takes the general path).
 int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastState& fs, uint32_t* pairs_out,
@@ -650,9 +873,17 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   }
   const void* kcol = keyed ? hi.cols[hi.key_col] : nullptr;
   const unsigned grid_rd = (unsigned)std::min<int64_t>(2048, (n + 511) / 512);
-  if (tm) SM_HIP(hipEventRecord(tm->ev[0], s));
+  if (tm) {
+    SM_HIP(hipEventRecord(tm->ev[0], s));
+    tm->nmk = 0;
+    tm->mark("start", s);
+  }
+  auto tmark = [&](const char* l) {
+    if (tm) tm->mark(l, s);
+  };
   hipLaunchKernelGGL(prep_kernel, dim3(grid_rd), dim3(512), 0, s, kcol, hi.key_type, a.ts, a.ordinals,
                      a.ordinal_base, n, c);
+  tmark("prep");
   Ctrl hc;
   SM_HIP(hipMemcpyAsync(&hc, c, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));
@@ -710,11 +941,11 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     B.f1 = (uint64_t*)sc.take(n * 8);
     B.f2 = (uint32_t*)sc.take(n * 4);
     hipLaunchKernelGGL(key_hist_kernel, dim3(grid_rd), dim3(kBlock), 0, s, kcol, hi.key_type, kmin, n, fpass, hist);
+    tmark("key_hist");
     hipLaunchKernelGGL(hist_scan_kernel, dim3(fpass), dim3(kBlock), 0, s, hist);
-    OrigSrc os{a.st, kcol, hi.key_type, kmin, a.code + a.c1_off, a.c1_len, a.consts, hi.vattr, hi.vtype, a.ts,
-               hc.ts0, a.ordinals, a.ordinal_base};
-    hipLaunchKernelGGL((onesweep_kernel<0, OrigSrc>), dim3(sort_grid), dim3(kBlock), 0, s, os, A, nullptr, nullptr,
-                       nullptr, n, nullptr, 0, hist, status, ++fs.epoch, ctr + ctr_used++, &c->err);
+    tmark("hist_scan");
+    launch_pass0(hi, a, kcol, kmin, hc.ts0, sort_grid, s, A, hist, status, ++fs.epoch, ctr + ctr_used++, &c->err);
+    tmark("key_pass0");
     RecSoA* cur = &A;
     RecSoA* nxt = &B;
     for (int p = 1; p < fpass; ++p) {
@@ -722,6 +953,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
       hipLaunchKernelGGL((onesweep_kernel<1, RecSrc>), dim3(sort_grid), dim3(kBlock), 0, s, rs, *nxt, nullptr,
                          nullptr, nullptr, n, nullptr, p * kRB, hist + p * kBins, status, ++fs.epoch,
                          ctr + ctr_used++, &c->err);
+      tmark("key_pass");
       std::swap(cur, nxt);
     }
     if (tm) SM_HIP(hipEventRecord(tm->ev[1], s));
@@ -733,8 +965,8 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     mi = nxt->f0;
     pj = (uint32_t*)nxt->f1;
     pi = (uint32_t*)nxt->f1 + n;
-    hipLaunchKernelGGL((walk_kernel<true>), dim3((unsigned)wtiles), dim3(kWalkBlock), 0, s, wa, mj, mi, status,
-                       ++fs.epoch, ctr + ctr_used++, &c->nmatch, &c->err);
+    launch_walk<true>(c2_spec(hi), wtiles, s, wa, mj, mi, status, ++fs.epoch, ctr + ctr_used++, &c->nmatch, &c->err);
+    tmark("walk");
   } else {
     if (tm) SM_HIP(hipEventRecord(tm->ev[1], s));
     mj = (uint32_t*)sc.take(n * 4);
@@ -744,15 +976,17 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     WalkArgs wa{nullptr, nullptr, nullptr, nullptr, a.st, a.ts, a.ordinals, a.ordinal_base,
                 a.code + a.c1_off, a.c1_len, a.code + a.c2_off, a.c2_len, a.consts, hi.vattr, hi.vtype,
                 a.within, n};
-    hipLaunchKernelGGL((walk_kernel<false>), dim3((unsigned)wtiles), dim3(kWalkBlock), 0, s, wa, mj, mi, status,
-                       ++fs.epoch, ctr + ctr_used++, &c->nmatch, &c->err);
+    launch_walk<false>(c2_spec(hi), wtiles, s, wa, mj, mi, status, ++fs.epoch, ctr + ctr_used++, &c->nmatch, &c->err);
+    tmark("walk");
   }
   if (tm) SM_HIP(hipEventRecord(tm->ev[2], s));
 
   // order by j: LSD passes over (j, i); the last one writes the interleaved output
   uint32_t* jh = hist + 4 * kBins;
   hipLaunchKernelGGL(u32_hist_kernel, dim3(grid_rd), dim3(kBlock), 0, s, mj, &c->nmatch, jpass, jh);
+  tmark("j_hist");
   hipLaunchKernelGGL(hist_scan_kernel, dim3(jpass), dim3(kBlock), 0, s, jh);
+  tmark("hist_scan");
   uint32_t *cj = mj, *ci = mi, *nj = pj, *ni = pi;
   for (int p = 0; p < jpass; ++p) {
     PairSrc ps{cj, ci};
@@ -760,10 +994,12 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
       hipLaunchKernelGGL((onesweep_kernel<3, PairSrc>), dim3(sort_grid), dim3(kBlock), 0, s, ps, RecSoA{}, nullptr,
                          nullptr, (uint64_t*)pairs_out, n, &c->nmatch, p * kRB, jh + p * kBins, status, ++fs.epoch,
                          ctr + ctr_used++, &c->err);
+      tmark("j_pass_last");
     } else {
       hipLaunchKernelGGL((onesweep_kernel<2, PairSrc>), dim3(sort_grid), dim3(kBlock), 0, s, ps, RecSoA{}, nj, ni,
                          nullptr, n, &c->nmatch, p * kRB, jh + p * kBins, status, ++fs.epoch, ctr + ctr_used++,
                          &c->err);
+      tmark("j_pass");
       std::swap(cj, nj);
       std::swap(ci, ni);
     }

@@ -145,7 +145,7 @@ int fast_vattr(const CompiledQuery& cq, const std::vector<int32_t>& types) {
     if (in.op == OP_VAR && (in.a != 0 || !(in.b == 0 || in.b == -1))) return -1;
   }
   if (vattr < 0) vattr = 0;
-  if (vattr >= (int)types.size() || types[vattr] == T_STRING) return -1;
+  if (vattr >= (int)types.size() || types[vattr] == T_STRING || types[vattr] == T_BOOL) return -1;
   return vattr;
 }
 
@@ -877,6 +877,7 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
     } else if (k == "fast_timing") {
       if (value && !a->fast_tm_ready) {
         for (auto& e : a->fast_tm.ev) SM_HIP(hipEventCreate(&e));
+        for (auto& e : a->fast_tm.mk) SM_HIP(hipEventCreate(&e));
         a->fast_tm_ready = true;
       }
       a->fast_timing = value != 0;
@@ -952,6 +953,8 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
       hi.cols = d_cols;
       hi.types = types.data();
       hi.vattr = fast_vattr(cq, types);
+      hi.c2_host = (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.fast_c2_off;
+      hi.c2_len = cq.fast_c2_len;
       if (hi.vattr >= 0) hi.vtype = types[hi.vattr];
       if (fa.key) {
         const CompiledPartition& cp = *q.part;
@@ -993,6 +996,23 @@ int sm_app_get_stat(sm_app* a, const char* key, double* out) {
       float ms = 0;
       SM_HIP(hipEventElapsedTime(&ms, a->fast_tm.ev[i], a->fast_tm.ev[i + 1]));
       *out = ms;
+      return;
+    }
+    // per-kernel totals of the last device batch: "kernel_ms:<label>" / "kernel_calls:<label>" (fast_timing)
+    if (k.rfind("kernel_ms:", 0) == 0 || k.rfind("kernel_calls:", 0) == 0) {
+      if (!a->fast_tm_ready) throw std::invalid_argument("fast_timing option is off");
+      const bool calls = k[7] == 'c';
+      const std::string label = k.substr(calls ? 13 : 10);
+      double tot = 0;
+      int cnt = 0;
+      for (int i = 1; i < a->fast_tm.nmk; ++i)
+        if (label == a->fast_tm.label[i]) {
+          float ms = 0;
+          SM_HIP(hipEventElapsedTime(&ms, a->fast_tm.mk[i - 1], a->fast_tm.mk[i]));
+          tot += ms;
+          ++cnt;
+        }
+      *out = calls ? cnt : tot;
       return;
     }
     throw std::invalid_argument("unknown stat " + k);

@@ -4,6 +4,7 @@ RCCL) → per-rank matching with global ordinals → merge_matches must equal th
 The per-rank matcher here is the CPU oracle (this test checks the sharding logic, not the kernels; the GPU
 kernels on a rank's key subset are checked in tests/test_device_batch.py::test_sharded_ordinals_match_oracle_subset)."""
 import ctypes
+import json
 import os
 import socket
 
@@ -37,7 +38,7 @@ def oracle_refs(cols, ts):
     return np.array([r[2] for r in out], dtype=np.int64).reshape(-1, 2)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, outfile):
     from siddhi_amd.shard import exchange_by_key
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -57,7 +58,8 @@ def _worker(rank, world, port, q):
         parts = [None] * world
         dist.all_gather_object(parts, glob.tolist())
         if rank == 0:
-            q.put(parts)
+            with open(outfile, "w") as f:
+                json.dump(parts, f)
     finally:
         dist.destroy_process_group()
 
@@ -70,13 +72,14 @@ def _free_port():
     return p
 
 
+@pytest.mark.timeout(240)
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_exchange_and_merge_equal_single_process(world):
+def test_sharded_exchange_and_merge_equal_single_process(world, tmp_path):
     from siddhi_amd.shard import merge_matches
-    ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    mp.start_processes(_worker, args=(world, _free_port(), q), nprocs=world, join=True, start_method="spawn")
-    parts = q.get()
+    out = str(tmp_path / "parts.json")
+    mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    with open(out) as f:
+        parts = json.load(f)
     got = merge_matches(parts)
     sym, price, vol, tsa, ts = synth.gen_stock(0, N, K, DIV, synth.seed_for(4))
     exp = oracle_refs([sym, price, vol, tsa], ts)
