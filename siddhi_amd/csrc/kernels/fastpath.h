@@ -32,14 +32,11 @@ struct FastHostInfo {
   int c2_len = 0;
 };
 
-// Persistent device state of the v2 kernels (look-back status words are epoch-tagged, never re-zeroed).
+// Device facts cached across batches by the v2 kernels.
 struct FastState {
-  void* status = nullptr;
-  size_t status_bytes = 0;
-  uint32_t epoch = 0;
-  ~FastState() {
-    if (status) (void)hipFree(status);
-  }
+  int cus = 0;              // compute units of the device
+  int sort_wgs_per_cu = 0;  // resident down-sweep workgroups per CU (persistent-chunk grid)
+  int walk_wgs_per_cu = 0;  // resident walk workgroups per CU
 };
 
 struct FastTimings {          // optional HIP events: [0] start, [1] keyed sort done, [2] walk done, [3] end
