@@ -217,16 +217,17 @@ def main():
 
 # Kernels of the device pipeline (labels recorded by kernels/fastpath2.hip) and their ALGORITHMIC bytes per
 # launch for a batch of n events with m matches: what each launch must read and write at minimum.
-KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last"]
+KERNELS = ["prep", "c1_mask", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last"]
 
 
 def alg_bytes(label, n, m):
     return {"prep": 12 * n,                 # key i32 + ts i64
+            "c1_mask": 8 * n + n // 8,      # price f64 in (c1 = price > 20), one bit out
             "key_up": 4 * n,                # key digits (i32)
             "scan": 0,                      # per-chunk digit counts (O(chunks x 1024), not per event)
-            "key_pass0": 20 * n + 20 * n,   # key + price + ts in, 20-B keyed record out
-            "key_pass": 20 * n + 20 * n,    # 20-B record in and out
-            "walk": 20 * n + 8 * m,         # records in, (j, i) u32 pairs out
+            "key_pass0": 20 * n + 16 * n,   # key i32 + price f64 + ts i64 in, 16-B keyed record out
+            "key_pass": 16 * n + 16 * n,    # 16-B record in and out
+            "walk": 16 * n + 8 * m,         # records in, (j, i) u32 pairs out
             "j_up": 4 * m,
             "j_pass": 16 * m,               # (j, i) in and out
             "j_pass_last": 16 * m}[label]

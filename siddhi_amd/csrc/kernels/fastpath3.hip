@@ -5,19 +5,28 @@
 // Every pass is a reduce-then-scan pass over G persistent workgroups, each owning one contiguous chunk of the
 // input (no inter-workgroup waiting inside a launch: a decoupled look-back walks the status words of the
 // tiles still in flight one cross-XCD load at a time, which on MI355X cost more than the data movement):
-//   prep      key min/max, ts monotonicity + span, max relative ordinal               (reads key + ts)
+//   prep      key min/max, ts monotonicity + span, max relative ordinal, compared-attribute range
 //   up_key    per-chunk digit counts of the rebased key (pass 0 from the key column, later passes from the
-//             record keys)                                                              (reads 4 B/event)
-//   scan      per digit, exclusive over chunks; digit bases                             (G x 1024 counts)
+//             records)
+//   scan      per digit, exclusive over chunks; digit bases                             (G x kBins counts)
 //   down_*    per chunk, tile by tile: stable in-tile ranking by wave64 ballot peer masks, LDS exchange so
 //             that each digit run leaves the tile as contiguous stores, running per-digit chunk offsets in LDS.
-//             Key pass 0 builds the 20-byte record {key|c1<<31 : u32, ordinal : u32, c2 attribute : u64,
-//             ts - ts0 : u32} from the original columns (c1 evaluated here, once per event).
-//   walk      per chunk, tile by tile: records + halo staged in LDS, one lane per record with a lane-private
-//             queue of its records; forward scan inside the key run until c2 holds or the window closes;
-//             matches compacted chunk-locally (staging) with the digit-0 counts of j as a side product
+//             Key pass 0 builds the 16-byte keyed record (below) from the original columns (c1 evaluated
+//             there, once per event).
+//   walk      keyed: per chunk, tile by tile: records + halo staged in LDS, one lane per record with a
+//             lane-private queue of its records; forward scan inside the key run until c2 holds or the window
+//             closes; matches compacted chunk-locally (staging) with the digit-0 counts of j as a side product.
+//             Unkeyed (no partition): the same over the original columns.
 //   down_j    LSD passes over the (j, i) pairs by j; the first reads the chunk-local staging, the last writes
-//             the interleaved (i, j) output
+//             the output.
+//
+// Keyed record: ONE 16-byte element {key | c1 << 31, ordinal, value code, ts - ts0}. The scatter of every pass
+// is the cost that matters (each tile sends its elements to kBins digit runs); one aligned 16-byte stream per
+// element writes runs 4x longer than four 32-bit field arrays would. The value code is a monotone 32-bit image
+// of the compared attribute: exact for INT, FLOAT and for LONG batches whose range spans < 2^32; for DOUBLE
+// (and wide LONG) it is the high half of the order-preserving 64-bit image, so `code2 != code1` decides any
+// comparison and equal codes (or NaN) fall back to the exact column values (rare; the record's ordinal gives
+// the row).
 #include <type_traits>
 #include <vector>
 
@@ -32,27 +41,75 @@ constexpr int kBlock = 512;
 constexpr int kWaves = kBlock / 64;
 constexpr int kItems = 8;
 constexpr int kTile = kBlock * kItems;  // 4096 elements per down-sweep tile
-constexpr int kRB = 10;                 // radix bits per pass
+#ifndef SM_RB
+#define SM_RB 10
+#endif
+constexpr int kRB = SM_RB;  // radix bits per pass
 constexpr int kBins = 1 << kRB;
-constexpr int kBinsPerThread = kBins / kBlock;
+constexpr int kBinsPerThread = kBins >= kBlock ? kBins / kBlock : 1;  // digits owned per thread
 constexpr uint32_t kKeyMask = 0x7fffffffu;
-constexpr int kUpUnroll = 8;            // independent loads in flight per thread in the up-sweeps
+constexpr int kUpUnroll = 8;  // independent loads in flight per thread in the up-sweeps
 constexpr int kWalkBlock = 256;
 constexpr int kWalkItems = 4;
 constexpr int kWalkTile = kWalkBlock * kWalkItems;  // 1024 records per walk tile
 constexpr int kWalkHalo = 256;                      // records staged past the tile for scans that leave it
 constexpr int kWalkLds = kWalkTile + kWalkHalo;
 constexpr int kWalkWaves = kWalkBlock / 64;
+constexpr uint32_t kNanCode = 0xffffffffu;  // value code of a NaN (FLOAT / DOUBLE): always compared exactly
 
-static_assert(kBins % kBlock == 0, "bins per thread");
+// value-code modes
+enum : int { VC_I32 = 0, VC_F32 = 1, VC_F64 = 2, VC_I64R = 3, VC_I64H = 4 };
+
+static_assert(kBins % kBlock == 0 || kBlock % kBins == 0, "bins per thread");
 static_assert(kTile % kWalkTile == 0, "walk tiles nest in sort tiles");
+
+// Diagnostic build only (tests/native/micro_sort.hip defines SM_STAMPS): per-wave s_memtime stamps at phase
+// boundaries of the down-sweep tile loop, summed into sm_stamps[] (shares, not absolute times).
+#ifdef SM_STAMPS
+__device__ unsigned long long sm_stamps[16];
+#define SM_STAMP(i)                                                            \
+  do {                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    unsigned long long t_;                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    if ((i) > 0) st_acc[(i) - 1] += t_ - st_last;                              \
+    st_last = t_;                                                              \
+  } while (0)
+#define SM_STAMP_DECL                \
+  unsigned long long st_acc[8] = {}; \
+  unsigned long long st_last = 0
+#define SM_STAMP_FLUSH                                                    \
+  do {                                                                    \
+    if ((threadIdx.x & 63) == 0)                                          \
+      for (int q_ = 0; q_ < 8; ++q_) atomicAdd(&sm_stamps[q_], st_acc[q_]); \
+  } while (0)
+#else
+#define SM_STAMP(i) \
+  do {              \
+  } while (0)
+#define SM_STAMP_DECL
+#define SM_STAMP_FLUSH \
+  do {                 \
+  } while (0)
+#endif
 
 struct Ctrl {
   unsigned long long kmin, kmax;  // sign-biased key range
   unsigned long long omax;        // max relative ordinal
-  unsigned int bad_ts, pad;
+  unsigned long long vmin, vmax;  // sign-biased range of a LONG compared attribute
+  unsigned int bad_ts, bad_ord;   // ts decreasing / ordinals not increasing
   long long ts0, ts_last;
 };
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global stores
+// (__syncthreads() may also drain vmcnt, which exposes every round of scattered stores). No kernel here exchanges
+// global data between the waves of a workgroup.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const int lane = threadIdx.x & 63;
@@ -91,10 +148,25 @@ __device__ __forceinline__ StackVal uncanon(uint64_t bits, int type) {
   }
   return v;
 }
+
+// monotone 32-bit value code (see the header)
 template <typename VT>
-__device__ __forceinline__ uint64_t canon_t(VT v) {
-  if constexpr (std::is_floating_point<VT>::value) return (uint64_t)__double_as_longlong((double)v);
-  else return (uint64_t)(int64_t)v;
+__device__ __forceinline__ uint32_t vcode(VT v, int mode, int64_t vmin) {
+  if constexpr (std::is_same<VT, int32_t>::value) {
+    return (uint32_t)v ^ 0x80000000u;
+  } else if constexpr (std::is_same<VT, float>::value) {
+    if (v != v) return kNanCode;
+    const uint32_t b = v == 0.0f ? 0u : __float_as_uint(v);  // -0.0 == 0.0
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  } else if constexpr (std::is_same<VT, double>::value) {
+    if (v != v) return kNanCode;
+    const uint64_t b = v == 0.0 ? 0ull : (uint64_t)__double_as_longlong(v);
+    const uint64_t m = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+    return (uint32_t)(m >> 32);
+  } else {  // int64
+    if (mode == VC_I64R) return (uint32_t)(v - vmin);
+    return (uint32_t)(((uint64_t)v ^ 0x8000000000000000ull) >> 32);
+  }
 }
 
 // A condition program decoded once per thread: its kernel-uniform instructions and constants stay in scalar
@@ -173,8 +245,8 @@ struct PairLoader {
   __device__ StackVal var(const Instr& in) const { return uncanon(in.a == 0 ? v1 : v2, type); }
 };
 
-// c2 as a fixed compare `e2.x OP e1.x` over the carried attribute (OP >= 0; FP: compared as double, else as
-// int64 — exact for every column type the spec admits), or the generic condition program (OP < 0).
+// Unkeyed walk: c2 on canonical 64-bit values, as a fixed compare `e2.x OP e1.x` (OP >= 0; FP: compared as
+// double, else as int64) or the generic condition program (OP < 0).
 template <int OP, bool FP>
 struct C2 {
   Cond c;
@@ -186,6 +258,56 @@ struct C2 {
       if constexpr (FP) return cmp_fixed<OP>(__longlong_as_double((long long)v2), __longlong_as_double((long long)v1));
       else return cmp_fixed<OP>((int64_t)v2, (int64_t)v1);
     }
+  }
+};
+
+// Keyed walk: c2 = `e2.x OP e1.x` on value codes; equal inexact codes and NaN go to the exact column values.
+template <int OP, bool FP>
+struct C2Code {
+  bool exact_codes;  // the code mode is exact (INT, FLOAT, rebased LONG)
+  int vtype;
+  const void* vcol;
+  const int64_t* ord;  // ordinals of the batch rows (nullptr: row = relative ordinal)
+  int64_t obase, n;
+  __device__ int64_t row_of(uint32_t o) const {  // rows are in ordinal order
+    if (!ord) return o;
+    const int64_t want = (int64_t)o + obase;
+    int64_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ord[mid] < want) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  }
+  __device__ bool exact(uint32_t o1, uint32_t o2) const {
+    const int64_t r1 = row_of(o1), r2 = row_of(o2);
+    if constexpr (FP) {
+      double x1, x2;
+      if (vtype == T_FLOAT) {
+        x1 = ((const float*)vcol)[r1];
+        x2 = ((const float*)vcol)[r2];
+      } else {
+        x1 = ((const double*)vcol)[r1];
+        x2 = ((const double*)vcol)[r2];
+      }
+      return cmp_fixed<OP>(x2, x1);
+    } else {
+      int64_t x1, x2;
+      if (vtype == T_INT) {
+        x1 = ((const int32_t*)vcol)[r1];
+        x2 = ((const int32_t*)vcol)[r2];
+      } else {
+        x1 = ((const int64_t*)vcol)[r1];
+        x2 = ((const int64_t*)vcol)[r2];
+      }
+      return cmp_fixed<OP>(x2, x1);
+    }
+  }
+  __device__ __forceinline__ bool operator()(uint32_t c1, uint32_t o1, uint32_t c2, uint32_t o2) const {
+    const bool nan = FP && (c1 == kNanCode || c2 == kNanCode);
+    if (!nan && (exact_codes || c1 != c2)) return cmp_fixed<OP>(c2, c1);
+    return exact(o1, o2);
   }
 };
 
@@ -204,10 +326,11 @@ __device__ __forceinline__ void chunk_range(int g, int64_t n, int64_t per, const
 
 // ---------------------------------------------------------------- prep
 
-__global__ void prep_kernel(const void* __restrict__ kcol, int ktype, const int64_t* __restrict__ ts,
-                            const int64_t* __restrict__ ord, int64_t obase, int64_t n, Ctrl* __restrict__ c) {
-  unsigned long long lo = ~0ull, hi = 0, om = 0;
-  unsigned int bad = 0;
+__global__ void prep_kernel(const void* __restrict__ kcol, int ktype, const int64_t* __restrict__ vlong,
+                            const int64_t* __restrict__ ts, const int64_t* __restrict__ ord, int64_t obase, int64_t n,
+                            Ctrl* __restrict__ c) {
+  unsigned long long lo = ~0ull, hi = 0, om = 0, vlo = ~0ull, vhi = 0;
+  unsigned int bad = 0, bado = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (kcol) {
       int64_t k = ktype == T_INT ? (int64_t)((const int32_t*)kcol)[i] : ((const int64_t*)kcol)[i];
@@ -215,31 +338,60 @@ __global__ void prep_kernel(const void* __restrict__ kcol, int ktype, const int6
       lo = u < lo ? u : lo;
       hi = u > hi ? u : hi;
     }
+    if (vlong) {
+      unsigned long long u = (unsigned long long)vlong[i] ^ 0x8000000000000000ull;
+      vlo = u < vlo ? u : vlo;
+      vhi = u > vhi ? u : vhi;
+    }
     if (i > 0 && ts[i] < ts[i - 1]) bad = 1;
     if (ord) {
       unsigned long long o = (unsigned long long)(ord[i] - obase);
       om = o > om ? o : om;
+      if (i > 0 && ord[i] <= ord[i - 1]) bado = 1;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long a = __shfl_down(lo, o, 64), b = __shfl_down(hi, o, 64), d = __shfl_down(om, o, 64);
+    unsigned long long e = __shfl_down(vlo, o, 64), f = __shfl_down(vhi, o, 64);
     lo = a < lo ? a : lo;
     hi = b > hi ? b : hi;
     om = d > om ? d : om;
+    vlo = e < vlo ? e : vlo;
+    vhi = f > vhi ? f : vhi;
   }
   bad = __any(bad) ? 1u : 0u;
+  bado = __any(bado) ? 1u : 0u;
   if ((threadIdx.x & 63) == 0) {
     if (kcol) {
       atomicMin(&c->kmin, lo);
       atomicMax(&c->kmax, hi);
     }
+    if (vlong) {
+      atomicMin(&c->vmin, vlo);
+      atomicMax(&c->vmax, vhi);
+    }
     if (ord) atomicMax(&c->omax, om);
     if (bad) atomicOr(&c->bad_ts, 1u);
+    if (bado) atomicOr(&c->bad_ord, 1u);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     c->ts0 = ts[0];
     c->ts_last = ts[n - 1];
     if (!ord) c->omax = (unsigned long long)(n - 1);
+  }
+}
+
+// c1 of every event as a bit mask (bit p & 63 of word p >> 6): one lane per event, ballot per wave. Evaluated
+// once here, at full occupancy, instead of inside the sort tiles (where its loads would be serialised).
+__global__ void __launch_bounds__(256) c1_mask_kernel(const NfaStream* __restrict__ st, int64_t n,
+                                                      const Instr* __restrict__ code, int len,
+                                                      const DVal* __restrict__ consts, uint64_t* __restrict__ mask) {
+  const Cond c1 = make_cond(code, len, consts);
+  const int lane = threadIdx.x & 63;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p - lane < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const bool c = p < n && eval(c1, RowLoader{st, p});
+    const uint64_t bal = __ballot(c);
+    if (lane == 0) mask[p >> 6] = bal;
   }
 }
 
@@ -251,9 +403,13 @@ struct KeyColDigits {  // rebased key from the original key column
   int64_t kmin;
   __device__ uint32_t key(int64_t p) const { return (uint32_t)((int64_t)kcol[p] - kmin); }
 };
-struct U32Digits {  // record keys / j values
-  const uint32_t* v;
-  __device__ uint32_t key(int64_t p) const { return v[p]; }
+struct RecDigits {  // keys of keyed records (word 0 of each 16-byte record)
+  const uint4* r;
+  __device__ uint32_t key(int64_t p) const { return ((const uint32_t*)r)[4 * p]; }
+};
+struct PairDigits {  // j of (j << 32) | i pairs
+  const uint64_t* q;
+  __device__ uint32_t key(int64_t p) const { return (uint32_t)(q[p] >> 32); }
 };
 
 // per-chunk digit counts → cnt[d * G + g]
@@ -271,7 +427,7 @@ __global__ void __launch_bounds__(kBlock) upsweep_kernel(DS src, int64_t n, int6
 #pragma unroll
     for (int u = 0; u < kUpUnroll; ++u) {
       const int64_t p = b + u * kBlock + threadIdx.x;
-      k[u] = p < hi ? src.key(p) : 0xffffffffu;
+      k[u] = p < hi ? src.key(p) : 0u;
     }
 #pragma unroll
     for (int u = 0; u < kUpUnroll; ++u)
@@ -315,7 +471,8 @@ __global__ void __launch_bounds__(kBlock) digit_base_kernel(uint32_t* __restrict
   __shared__ uint32_t lw[kWaves];
   uint32_t v[kBinsPerThread], s = 0;
   for (int k = 0; k < kBinsPerThread; ++k) {
-    v[k] = tot[threadIdx.x * kBinsPerThread + k];
+    const int d = threadIdx.x * kBinsPerThread + k;
+    v[k] = d < kBins ? tot[d] : 0u;
     s += v[k];
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -329,7 +486,7 @@ __global__ void __launch_bounds__(kBlock) digit_base_kernel(uint32_t* __restrict
   uint32_t run = inc - s;
   for (int k = 0; k < w; ++k) run += lw[k];
   for (int k = 0; k < kBinsPerThread; ++k) {
-    tot[threadIdx.x * kBinsPerThread + k] = run;
+    if (threadIdx.x * kBinsPerThread + k < kBins) tot[threadIdx.x * kBinsPerThread + k] = run;
     run += v[k];
   }
 }
@@ -337,7 +494,7 @@ __global__ void __launch_bounds__(kBlock) digit_base_kernel(uint32_t* __restrict
 // ---------------------------------------------------------------- down-sweep
 
 // Pass 0 of the keyed sort: builds the record from the original columns. Key and compared-attribute column
-// types are template parameters; c1 is evaluated by c1(), once per event, outside the unrolled loops.
+// types are template parameters; c1 is evaluated once per event in a rolled loop.
 template <typename KT, typename VT>
 struct OrigSrc {
   static constexpr bool kC1 = true;
@@ -345,61 +502,47 @@ struct OrigSrc {
   const KT* kcol;
   const VT* vcol;
   int64_t kmin;
-  const Instr* c1p;
-  int c1_len;
-  const DVal* consts;
+  int vmode;
+  int64_t vmin;
+  const uint64_t* c1mask;
   const int64_t* ts;
   int64_t ts0;
   const int64_t* ord;
   int64_t obase;
-  __device__ uint32_t key(int64_t p) const { return (uint32_t)((int64_t)kcol[p] - kmin); }
-  __device__ uint32_t f0(int64_t p) const { return ord ? (uint32_t)(ord[p] - obase) : (uint32_t)p; }
-  __device__ uint64_t f1(int64_t p) const { return canon_t(vcol[p]); }
-  __device__ uint32_t f2(int64_t p) const { return (uint32_t)(ts[p] - ts0); }
-};
-
-struct RecSoA {  // keyed record, structure of arrays
-  uint32_t* k;
-  uint32_t* f0;
-  uint64_t* f1;
-  uint32_t* f2;
+  __device__ uint4 rec(int64_t p) const {
+    uint4 r;
+    r.x = (uint32_t)((int64_t)kcol[p] - kmin);
+    r.y = ord ? (uint32_t)(ord[p] - obase) : (uint32_t)p;
+    r.z = vcode<VT>(vcol[p], vmode, vmin);
+    r.w = (uint32_t)(ts[p] - ts0);
+    return r;
+  }
 };
 
 struct RecSrc {
   static constexpr bool kC1 = false;
-  const uint32_t* k;
-  const uint32_t* f0;
-  const uint64_t* f1;
-  const uint32_t* f2;
-  __device__ uint32_t key(int64_t p) const { return k[p]; }
-  __device__ uint32_t g0(int64_t p) const { return f0[p]; }
+  const uint4* r;
+  __device__ uint4 rec(int64_t p) const { return r[p]; }
 };
 
-struct PairSrc {
+struct PairSrc {  // (j << 32) | i
   static constexpr bool kC1 = false;
-  const uint32_t* j;
-  const uint32_t* i;
-  __device__ uint32_t key(int64_t p) const { return j[p]; }
-  __device__ uint32_t g0(int64_t p) const { return i[p]; }
+  const uint64_t* q;
 };
 
 // Down-sweep of one LSD pass over chunk blockIdx.x (persistent: tile by tile, running per-digit offsets).
-//   MODE 0: keyed record from the original columns (OrigSrc) → RecSoA
-//   MODE 1: keyed record (RecSrc) → RecSoA
-//   MODE 2: (j, i) pairs → two u32 arrays
-//   MODE 3: (j, i) pairs → interleaved (i, j) u32 pairs (last pass)
+//   MODE 0: keyed record from the original columns (OrigSrc) → records
+//   MODE 1: keyed records (RecSrc) → records
+//   MODE 2: (j << 32) | i pairs → pairs (the last pass writes the output: in memory the (i, j) u32 pairs)
 template <int MODE, typename Src>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) downsweep_kernel(Src src, RecSoA dst, uint32_t* __restrict__ dj,
-                                                           uint32_t* __restrict__ di, uint64_t* __restrict__ dpairs,
-                                                           int64_t n, int64_t per, const uint32_t* seg_len, int G,
-                                                           int shift, const uint32_t* __restrict__ cnt,
-                                                           const uint32_t* __restrict__ dbase) {
-  __shared__ uint32_t xb32[kTile];  // exchange buffer, one 32-bit field at a time (u64 fields in two halves)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+downsweep_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dpairs, int64_t n, int64_t per,
+                 const uint32_t* seg_len, int G, int shift, const uint32_t* __restrict__ cnt,
+                 const uint32_t* __restrict__ dbase) {
+  __shared__ uint64_t xb64[kTile];  // exchange buffer: records in two 64-bit halves, pairs whole
   __shared__ uint16_t wcnt[kWaves][kBins];
   __shared__ uint32_t tstart[kBins];
   __shared__ uint32_t run[kBins];  // next output position of each digit for this chunk
-  __shared__ uint16_t sdig[kTile];  // digit of the element at each sorted slot (destinations are recomputed
-                                    // per exchange from LDS instead of living in registers)
   __shared__ uint32_t lw[kWaves];
 
   int64_t lo, len;
@@ -407,54 +550,52 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
   for (int d = threadIdx.x; d < kBins; d += kBlock) run[d] = dbase[d] + cnt[(int64_t)d * G + blockIdx.x];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = lanemask_lt();
-  Cond c1;
-  if constexpr (Src::kC1) c1 = make_cond(src.c1p, src.c1_len, src.consts);
+  SM_STAMP_DECL;
 
   for (int64_t base = lo; base < lo + len; base += kTile) {
+    SM_STAMP(0);
     const int tile_n = (int)((lo + len - base) < kTile ? (lo + len - base) : kTile);
-    // every load of the tile is issued up front (one exposed memory latency per tile, not one per field)
-    uint32_t keys[kItems], p0[kItems], p2[kItems];
-    uint64_t p1[kItems];
+    // every load of the tile is issued up front (one exposed memory latency per tile)
+    uint64_t a[kItems], b[kItems];  // records: a = key | ordinal << 32, b = code | ts << 32; pairs: a only
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int e = w * 64 * kItems + k * 64 + lane;
       if (e < tile_n) {
         const int64_t p = base + e;
-        keys[k] = src.key(p);
-        if constexpr (MODE == 0) {
-          p0[k] = src.f0(p);
-          p1[k] = src.f1(p);
-          p2[k] = src.f2(p);
-        } else if constexpr (MODE == 1) {
-          p0[k] = src.f0[p];
-          p1[k] = src.f1[p];
-          p2[k] = src.f2[p];
+        if constexpr (MODE <= 1) {
+          const uint4 r = src.rec(p);
+          a[k] = (uint64_t)r.x | ((uint64_t)r.y << 32);
+          b[k] = (uint64_t)r.z | ((uint64_t)r.w << 32);
         } else {
-          p0[k] = src.g0(p);
+          a[k] = src.q[p];
         }
       }
     }
-    __syncthreads();  // previous tile's readers of wcnt / xb32 / sdig / run are done
+    lds_barrier();  // previous tile's readers of wcnt / xb64 / run are done
     for (int k = threadIdx.x; k < kWaves * kBins; k += kBlock) (&wcnt[0][0])[k] = 0;
-    if constexpr (Src::kC1) {  // c1 flag of each item → key bit 31, evaluated in a rolled loop
-#pragma unroll 1
+    if constexpr (Src::kC1) {  // c1 flag of each item → key bit 31 (one mask word per wave-item)
+#pragma unroll
       for (int k = 0; k < kItems; ++k) {
         const int e = w * 64 * kItems + k * 64 + lane;
-        if (e < tile_n && eval(c1, RowLoader{src.st, base + e})) keys[k] |= 0x80000000u;
+        if (e < tile_n && ((src.c1mask[(base + e) >> 6] >> ((base + e) & 63)) & 1ull)) a[k] |= 0x80000000ull;
       }
     }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every load of the tile retired (known to the compiler, so no
+                                         // later vmcnt wait for them lands behind this tile's stores)
+    lds_barrier();
+    SM_STAMP(1);
 
     uint32_t lp[kItems];  // rank within (wave, digit), then local sorted position
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int e = w * 64 * kItems + k * 64 + lane;
       const bool valid = e < tile_n;
-      const uint32_t d = valid ? ((keys[k] & kKeyMask) >> shift) & (kBins - 1) : 0u;
+      const uint32_t key = MODE <= 1 ? (uint32_t)a[k] : (uint32_t)(a[k] >> 32);
+      const uint32_t d = valid ? ((key & kKeyMask) >> shift) & (kBins - 1) : 0u;
       uint64_t peers = __ballot(valid);
 #pragma unroll
-      for (int b = 0; b < kRB; ++b) {
-        const bool bit = (d >> b) & 1u;
+      for (int bb = 0; bb < kRB; ++bb) {
+        const bool bit = (d >> bb) & 1u;
         const uint64_t bal = __ballot(bit);
         peers &= bit ? bal : ~bal;
       }
@@ -464,21 +605,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
       if (valid && below == 0) wcnt[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
       lp[k] = old + below;
     }
-    __syncthreads();
+    lds_barrier();
+    SM_STAMP(2);
 
     // per digit: wave offsets (exclusive, in place) and the tile count
     uint32_t cnt_t[kBinsPerThread];
     uint32_t csum = 0;
 #pragma unroll
-    for (int b = 0; b < kBinsPerThread; ++b) {
-      const int d = threadIdx.x * kBinsPerThread + b;
+    for (int bb = 0; bb < kBinsPerThread; ++bb) {
+      const int d = threadIdx.x * kBinsPerThread + bb;
       uint32_t r = 0;
-      for (int q = 0; q < kWaves; ++q) {
-        const uint32_t c = wcnt[q][d];
-        wcnt[q][d] = (uint16_t)r;
-        r += c;
-      }
-      cnt_t[b] = r;
+      if (d < kBins)
+        for (int q = 0; q < kWaves; ++q) {
+          const uint32_t c = wcnt[q][d];
+          wcnt[q][d] = (uint16_t)r;
+          r += c;
+        }
+      cnt_t[bb] = r;
       csum += r;
     }
     {  // block exclusive scan of the tile counts over digits → tstart
@@ -488,91 +631,77 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         if (lane >= o) inc += u;
       }
       if (lane == 63) lw[w] = inc;
-      __syncthreads();
+      lds_barrier();
       uint32_t r = inc - csum;
       for (int q = 0; q < w; ++q) r += lw[q];
 #pragma unroll
-      for (int b = 0; b < kBinsPerThread; ++b) {
-        tstart[threadIdx.x * kBinsPerThread + b] = r;
-        r += cnt_t[b];
+      for (int bb = 0; bb < kBinsPerThread; ++bb) {
+        if (threadIdx.x * kBinsPerThread + bb < kBins) tstart[threadIdx.x * kBinsPerThread + bb] = r;
+        r += cnt_t[bb];
       }
     }
-    __syncthreads();
+    lds_barrier();
+    SM_STAMP(3);
 
-    // local sorted positions; key exchange; slot digits
+    // local sorted positions; the first exchange carries the key, so each sorted slot learns its digit and
+    // destination from it
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int e = w * 64 * kItems + k * 64 + lane;
       if (e < tile_n) {
-        const uint32_t d = ((keys[k] & kKeyMask) >> shift) & (kBins - 1);
+        const uint32_t key = MODE <= 1 ? (uint32_t)a[k] : (uint32_t)(a[k] >> 32);
+        const uint32_t d = ((key & kKeyMask) >> shift) & (kBins - 1);
         lp[k] += tstart[d] + wcnt[w][d];
-        xb32[lp[k]] = keys[k];
+        xb64[lp[k]] = a[k];
       }
     }
-    __syncthreads();
-    auto dest_of = [&](int s) -> uint32_t {
-      const uint32_t d = sdig[s];
-      return run[d] + (uint32_t)s - tstart[d];
-    };
-    uint32_t jj[kItems];  // MODE 3: j of the sorted slots
+    lds_barrier();
+    uint32_t dest[kItems];
+    uint64_t sa[kItems];  // records: first half of the slot's record
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
       const int s = r * kBlock + threadIdx.x;
       if (s < tile_n) {
-        const uint32_t key = xb32[s];
+        const uint64_t x = xb64[s];
+        const uint32_t key = MODE <= 1 ? (uint32_t)x : (uint32_t)(x >> 32);
         const uint32_t d = ((key & kKeyMask) >> shift) & (kBins - 1);
-        sdig[s] = (uint16_t)d;
-        const uint32_t dst_pos = run[d] + (uint32_t)s - tstart[d];
-        if constexpr (MODE == 0 || MODE == 1) dst.k[dst_pos] = key;
-        if constexpr (MODE == 2) dj[dst_pos] = key;
-        if constexpr (MODE == 3) jj[r] = key;
+        dest[r] = run[d] + (uint32_t)s - tstart[d];
+        if constexpr (MODE <= 1) sa[r] = x;
+        else dpairs[dest[r]] = x;
       }
     }
-    // payload exchanges: scatter the field into sorted slots, then coalesced stores by slot
-    auto exchange = [&](const uint32_t (&v)[kItems], auto&& store) {
-      __syncthreads();
+    SM_STAMP(4);
+    if constexpr (MODE <= 1) {  // second half, then one 16-byte store per record
+      lds_barrier();
 #pragma unroll
       for (int k = 0; k < kItems; ++k) {
         const int e = w * 64 * kItems + k * 64 + lane;
-        if (e < tile_n) xb32[lp[k]] = v[k];
+        if (e < tile_n) xb64[lp[k]] = b[k];
       }
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int r = 0; r < kItems; ++r) {
         const int s = r * kBlock + threadIdx.x;
-        if (s < tile_n) store(r, s, xb32[s]);
+        if (s < tile_n) {
+          const uint64_t y = xb64[s];
+          drec[dest[r]] = make_uint4((uint32_t)sa[r], (uint32_t)(sa[r] >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+        }
       }
-    };
-    if constexpr (MODE == 3) {  // (j, i) → interleaved (i, j)
-      exchange(p0, [&](int r, int s, uint32_t x) { dpairs[dest_of(s)] = ((uint64_t)jj[r] << 32) | x; });
-    } else if constexpr (MODE == 2) {
-      exchange(p0, [&](int, int s, uint32_t x) { di[dest_of(s)] = x; });
-    } else {
-      exchange(p0, [&](int, int s, uint32_t x) { dst.f0[dest_of(s)] = x; });
-      uint32_t* f1w = (uint32_t*)dst.f1;  // u64 field as two 32-bit halves
-      uint32_t half[kItems];
-#pragma unroll
-      for (int k = 0; k < kItems; ++k) half[k] = (uint32_t)p1[k];
-      exchange(half, [&](int, int s, uint32_t x) { f1w[2 * (size_t)dest_of(s)] = x; });
-#pragma unroll
-      for (int k = 0; k < kItems; ++k) half[k] = (uint32_t)(p1[k] >> 32);
-      exchange(half, [&](int, int s, uint32_t x) { f1w[2 * (size_t)dest_of(s) + 1] = x; });
-      exchange(p2, [&](int, int s, uint32_t x) { dst.f2[dest_of(s)] = x; });
     }
-    __syncthreads();  // every destination computed from run[] before it advances
+    SM_STAMP(5);
+    lds_barrier();  // every destination computed from run[] before it advances
 #pragma unroll
-    for (int b = 0; b < kBinsPerThread; ++b) run[threadIdx.x * kBinsPerThread + b] += cnt_t[b];
+    for (int bb = 0; bb < kBinsPerThread; ++bb)
+      if (threadIdx.x * kBinsPerThread + bb < kBins) run[threadIdx.x * kBinsPerThread + bb] += cnt_t[bb];
+    SM_STAMP(6);
   }
+  SM_STAMP_FLUSH;
 }
 
 // ---------------------------------------------------------------- walk
 
 struct WalkArgs {
-  // keyed (sorted records) or original columns
-  const uint32_t* k;
-  const uint32_t* f0;
-  const uint64_t* f1;
-  const uint32_t* f2;
+  const uint4* rec;  // keyed: sorted records
   const NfaStream* st;
   const int64_t* ts;
   const int64_t* ord;
@@ -585,16 +714,18 @@ struct WalkArgs {
   int vattr, vtype;
   int64_t within;
   int64_t n;
+  bool exact_codes;
+  const uint64_t* c1mask;  // unkeyed: c1 bits of the events
 };
 
 template <bool KEYED>
 struct WalkLds;
 template <>
 struct WalkLds<true> {
-  uint64_t v[kWalkLds];
   uint32_t k[kWalkLds];
-  uint32_t t[kWalkLds];
   uint32_t o[kWalkLds];
+  uint32_t c[kWalkLds];
+  uint32_t t[kWalkLds];
 };
 template <>
 struct WalkLds<false> {
@@ -610,8 +741,7 @@ struct WalkLds<false> {
 // count goes to mcount[g] and the digit-0 counts of j to jcnt[d * G + g] (the first j pass needs no up-sweep).
 template <bool KEYED, int OP, bool FP>
 __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t per, int G,
-                                                          uint32_t* __restrict__ stj, uint32_t* __restrict__ sti,
-                                                          uint32_t* __restrict__ mcount,
+                                                          uint64_t* __restrict__ stq, uint32_t* __restrict__ mcount,
                                                           uint32_t* __restrict__ jcnt) {
   __shared__ WalkLds<KEYED> L;
   __shared__ uint32_t sj[kWalkItems][kWalkBlock];  // per item: matched position - tile base (or resume point)
@@ -628,28 +758,46 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
   if (threadIdx.x == 0) sh_run = 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = lanemask_lt();
-  C2<OP, FP> c2;
-  if constexpr (OP < 0) c2.c = make_cond(a.c2, a.c2_len, a.consts);
+  C2<OP, FP> c2;  // unkeyed
+  if constexpr (!KEYED && OP < 0) c2.c = make_cond(a.c2, a.c2_len, a.consts);
   c2.vtype = a.vtype;
-  Cond c1;
-  if constexpr (!KEYED) c1 = make_cond(a.c1, a.c1_len, a.consts);
+  C2Code<OP, FP> cc{a.exact_codes, a.vtype, a.st->cols[a.vattr], a.ord, a.obase, n};  // keyed
+
+  // keyed: the next tile's records are loaded into registers while the current tile is scanned
+  constexpr int kPre = (kWalkLds + kWalkBlock - 1) / kWalkBlock;
+  uint4 pre[kPre];
+  auto prefetch = [&](int64_t b) {
+#pragma unroll
+    for (int q = 0; q < kPre; ++q) {
+      const int64_t p = b + q * kWalkBlock + threadIdx.x;
+      if (q * kWalkBlock + threadIdx.x < kWalkLds && p < n) pre[q] = a.rec[p];
+    }
+  };
+  if constexpr (KEYED) prefetch(lo);
 
   for (int64_t base = lo; base < hi; base += kWalkTile) {
-    __syncthreads();  // previous tile's LDS readers are done
+    lds_barrier();  // previous tile's LDS readers are done
     const int nload = (int)((n - base) < kWalkLds ? (n - base) : kWalkLds);
-    for (int e = threadIdx.x; e < nload; e += kWalkBlock) {
-      const int64_t p = base + e;
-      if constexpr (KEYED) {
-        L.k[e] = a.k[p];
-        L.t[e] = a.f2[p];
-        L.v[e] = a.f1[p];
-        L.o[e] = a.f0[p];
-      } else {
+    if constexpr (KEYED) {
+#pragma unroll
+      for (int q = 0; q < kPre; ++q) {
+        const int e = q * kWalkBlock + threadIdx.x;
+        if (e < nload) {
+          L.k[e] = pre[q].x;
+          L.o[e] = pre[q].y;
+          L.c[e] = pre[q].z;
+          L.t[e] = pre[q].w;
+        }
+      }
+      if (base + kWalkTile < hi) prefetch(base + kWalkTile);
+    } else {
+      for (int e = threadIdx.x; e < nload; e += kWalkBlock) {
+        const int64_t p = base + e;
         L.t[e] = a.ts[p];
         L.v[e] = canon(col_value(a.st, a.vattr, p), a.vtype);
       }
     }
-    __syncthreads();
+    lds_barrier();
     const int lend = nload;  // staged positions are [0, lend) relative to base
     uint32_t c1m = 0;        // c1 of each item (bit k)
 #pragma unroll 1
@@ -658,7 +806,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       if (base + lu < hi) {
         bool c;
         if constexpr (KEYED) c = (L.k[lu] >> 31) != 0;
-        else c = eval(c1, RowLoader{a.st, base + lu});
+        else c = (a.c1mask[(base + lu) >> 6] >> ((base + lu) & 63)) & 1ull;
         if (c) c1m |= 1u << k;
       }
     }
@@ -668,15 +816,20 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
     int k = -1, v = 0;
     uint64_t vu = 0;
     int64_t tu = 0;
-    uint32_t key = 0;
+    uint32_t key = 0, cu = 0, ou = 0;
     auto take = [&]() -> bool {
       if (!todo) return false;
       k = __ffs(todo) - 1;
       todo &= todo - 1;
       const int lu = w * 64 * kWalkItems + k * 64 + lane;
-      vu = L.v[lu];
       tu = L.t[lu];
-      if constexpr (KEYED) key = L.k[lu] & kKeyMask;
+      if constexpr (KEYED) {
+        key = L.k[lu] & kKeyMask;
+        cu = L.c[lu];
+        ou = L.o[lu];
+      } else {
+        vu = L.v[lu];
+      }
       v = lu + 1;
       return true;
     };
@@ -690,16 +843,18 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
           }
           live = take();
         } else {
-          bool stop;
+          bool stop, hit;
           if constexpr (KEYED) {
             stop = (L.k[v] & kKeyMask) != key || (a.within >= 0 && (int64_t)(L.t[v] - (uint32_t)tu) > a.within);
+            hit = !stop && cc(cu, ou, L.c[v], L.o[v]);
           } else {
             const int64_t d = L.t[v] - tu;
             stop = a.within >= 0 && (d < 0 ? -d : d) > a.within;
+            hit = !stop && c2(vu, L.v[v]);
           }
           if (stop) {
             live = take();
-          } else if (c2(vu, L.v[v])) {
+          } else if (hit) {
             hasm |= 1u << k;
             sj[k][threadIdx.x] = (uint32_t)v;
             live = take();
@@ -715,25 +870,22 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       const int kk = __ffs(openm) - 1;
       openm &= openm - 1;
       const int luu = w * 64 * kWalkItems + kk * 64 + lane;
-      const uint64_t vuu = L.v[luu];
       for (int64_t p = base + sj[kk][threadIdx.x]; p < n; ++p) {
+        bool hit;
         if constexpr (KEYED) {
-          if ((a.k[p] & kKeyMask) != (L.k[luu] & kKeyMask) ||
-              (a.within >= 0 && (int64_t)(a.f2[p] - L.t[luu]) > a.within))
+          const uint4 r = a.rec[p];
+          if ((r.x & kKeyMask) != (L.k[luu] & kKeyMask) || (a.within >= 0 && (int64_t)(r.w - L.t[luu]) > a.within))
             break;
-          if (c2(vuu, a.f1[p])) {
-            hasm |= 1u << kk;
-            sj[kk][threadIdx.x] = (uint32_t)(p - base);
-            break;
-          }
+          hit = cc(L.c[luu], L.o[luu], r.z, r.y);
         } else {
           const int64_t d = a.ts[p] - L.t[luu];
           if (a.within >= 0 && (d < 0 ? -d : d) > a.within) break;
-          if (c2(vuu, canon(col_value(a.st, a.vattr, p), a.vtype))) {
-            hasm |= 1u << kk;
-            sj[kk][threadIdx.x] = (uint32_t)(p - base);
-            break;
-          }
+          hit = c2(L.v[luu], canon(col_value(a.st, a.vattr, p), a.vtype));
+        }
+        if (hit) {
+          hasm |= 1u << kk;
+          sj[kk][threadIdx.x] = (uint32_t)(p - base);
+          break;
         }
       }
     }
@@ -745,7 +897,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       mine += (uint32_t)__popcll(bal);
     }
     if (lane == 0) wtot[w] = mine;
-    __syncthreads();
+    lds_barrier();
     uint32_t ob = sh_run, tot = 0;
     for (int q = 0; q < kWalkWaves; ++q) {
       if (q < w) ob += wtot[q];
@@ -760,20 +912,19 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
         const uint32_t jv = sj[q][threadIdx.x];
         uint32_t jo, io;
         if constexpr (KEYED) {
-          jo = jv < (uint32_t)lend ? L.o[jv] : a.f0[base + jv];
+          jo = jv < (uint32_t)lend ? L.o[jv] : ((const uint32_t*)(a.rec + base + jv))[1];
           io = L.o[luq];
         } else {
           const int64_t vj = base + jv, ui = base + luq;
           jo = a.ord ? (uint32_t)(a.ord[vj] - a.obase) : (uint32_t)vj;
           io = a.ord ? (uint32_t)(a.ord[ui] - a.obase) : (uint32_t)ui;
         }
-        stj[pos] = jo;
-        sti[pos] = io;
+        stq[pos] = ((uint64_t)jo << 32) | io;
         atomicAdd(&jh[jo & (kBins - 1)], 1u);
       }
       ob += (uint32_t)__popcll(bal);
     }
-    __syncthreads();  // every wave read sh_run / wtot
+    lds_barrier();  // every wave read sh_run / wtot
     if (threadIdx.x == 0) sh_run += tot;
   }
   __syncthreads();
@@ -809,16 +960,15 @@ int c2_spec(const FastHostInfo& hi) {
 }
 
 template <bool KEYED, int OP, bool FP>
-void launch_walk_t(int G, hipStream_t s, const WalkArgs& wa, int64_t per, uint32_t* stj, uint32_t* sti,
-                   uint32_t* mcount, uint32_t* jcnt) {
-  hipLaunchKernelGGL((walk_kernel<KEYED, OP, FP>), dim3(G), dim3(kWalkBlock), 0, s, wa, per, G, stj, sti, mcount,
-                     jcnt);
+void launch_walk_t(int G, hipStream_t s, const WalkArgs& wa, int64_t per, uint64_t* stq, uint32_t* mcount,
+                   uint32_t* jcnt) {
+  hipLaunchKernelGGL((walk_kernel<KEYED, OP, FP>), dim3(G), dim3(kWalkBlock), 0, s, wa, per, G, stq, mcount, jcnt);
 }
 
 template <bool KEYED>
-void launch_walk(int spec, int G, hipStream_t s, const WalkArgs& wa, int64_t per, uint32_t* stj, uint32_t* sti,
-                 uint32_t* mcount, uint32_t* jcnt) {
-#define SM_WALK(OP, FP) launch_walk_t<KEYED, OP, FP>(G, s, wa, per, stj, sti, mcount, jcnt)
+void launch_walk(int spec, int G, hipStream_t s, const WalkArgs& wa, int64_t per, uint64_t* stq, uint32_t* mcount,
+                 uint32_t* jcnt) {
+#define SM_WALK(OP, FP) launch_walk_t<KEYED, OP, FP>(G, s, wa, per, stq, mcount, jcnt)
   switch (spec) {
     case CMP_EQ * 2: SM_WALK(CMP_EQ, false); break;
     case CMP_EQ * 2 + 1: SM_WALK(CMP_EQ, true); break;
@@ -832,28 +982,33 @@ void launch_walk(int spec, int G, hipStream_t s, const WalkArgs& wa, int64_t per
     case CMP_GT * 2 + 1: SM_WALK(CMP_GT, true); break;
     case CMP_GE * 2: SM_WALK(CMP_GE, false); break;
     case CMP_GE * 2 + 1: SM_WALK(CMP_GE, true); break;
-    default: SM_WALK(-1, false); break;
+    default:
+      if constexpr (KEYED) throw std::logic_error("keyed walk needs a compare spec");
+      else SM_WALK(-1, false);
+      break;
   }
 #undef SM_WALK
 }
 
 template <typename KT, typename VT>
-void launch_down0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int64_t ts0, int G,
-                    int64_t per, hipStream_t s, RecSoA dst, const uint32_t* cnt, const uint32_t* dbase) {
-  OrigSrc<KT, VT> os{a.st, (const KT*)kcol, (const VT*)hi.cols[hi.vattr], kmin, a.code + a.c1_off, a.c1_len,
-                     a.consts, a.ts, ts0, a.ordinals, a.ordinal_base};
-  hipLaunchKernelGGL((downsweep_kernel<0, OrigSrc<KT, VT>>), dim3(G), dim3(kBlock), 0, s, os, dst, nullptr, nullptr,
-                     nullptr, a.n, per, nullptr, G, 0, cnt, dbase);
+void launch_down0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int vmode, int64_t vmin,
+                    const uint64_t* c1mask, int64_t ts0, int G, int64_t per, hipStream_t s, uint4* dst,
+                    const uint32_t* cnt, const uint32_t* dbase) {
+  OrigSrc<KT, VT> os{a.st, (const KT*)kcol, (const VT*)hi.cols[hi.vattr], kmin, vmode, vmin, c1mask, a.ts, ts0,
+                     a.ordinals, a.ordinal_base};
+  hipLaunchKernelGGL((downsweep_kernel<0, OrigSrc<KT, VT>>), dim3(G), dim3(kBlock), 0, s, os, dst, nullptr, a.n, per,
+                     nullptr, G, 0, cnt, dbase);
 }
 
 template <typename KT>
-void launch_down0_k(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int64_t ts0, int G,
-                    int64_t per, hipStream_t s, RecSoA dst, const uint32_t* cnt, const uint32_t* dbase) {
+void launch_down0_k(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int vmode, int64_t vmin,
+                    const uint64_t* m, int64_t ts0, int G, int64_t per, hipStream_t s, uint4* dst,
+                    const uint32_t* cnt, const uint32_t* dbase) {
   switch (hi.vtype) {
-    case T_INT: launch_down0_t<KT, int32_t>(hi, a, kcol, kmin, ts0, G, per, s, dst, cnt, dbase); break;
-    case T_LONG: launch_down0_t<KT, int64_t>(hi, a, kcol, kmin, ts0, G, per, s, dst, cnt, dbase); break;
-    case T_FLOAT: launch_down0_t<KT, float>(hi, a, kcol, kmin, ts0, G, per, s, dst, cnt, dbase); break;
-    case T_DOUBLE: launch_down0_t<KT, double>(hi, a, kcol, kmin, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_INT: launch_down0_t<KT, int32_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_LONG: launch_down0_t<KT, int64_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_FLOAT: launch_down0_t<KT, float>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_DOUBLE: launch_down0_t<KT, double>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
     default: throw std::runtime_error("fast path: unsupported compared-attribute type");
   }
 }
@@ -870,6 +1025,8 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   if (n >= 0x7fffffffll || hi.vattr < 0) return -1;
   const bool keyed = a.key != nullptr;
   if (keyed && (hi.key_col < 0 || !(hi.key_type == T_INT || hi.key_type == T_LONG))) return -1;
+  const int spec = c2_spec(hi);
+  if (keyed && spec < 0) return -1;  // keyed records carry value codes: fixed compares only
   size_t mark = sc.used;
   auto bail = [&]() -> int64_t {
     sc.used = mark;
@@ -879,9 +1036,11 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   {
     Ctrl init{};
     init.kmin = ~0ull;
+    init.vmin = ~0ull;
     SM_HIP(hipMemcpyAsync(c, &init, sizeof(Ctrl), hipMemcpyHostToDevice, s));
   }
   const void* kcol = keyed ? hi.cols[hi.key_col] : nullptr;
+  const int64_t* vlong = (keyed && hi.vtype == T_LONG) ? (const int64_t*)hi.cols[hi.vattr] : nullptr;
   const unsigned grid_rd = (unsigned)std::min<int64_t>(2048, (n + 511) / 512);
   if (tm) {
     SM_HIP(hipEventRecord(tm->ev[0], s));
@@ -891,7 +1050,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   auto tmark = [&](const char* l) {
     if (tm) tm->mark(l, s);
   };
-  hipLaunchKernelGGL(prep_kernel, dim3(grid_rd), dim3(512), 0, s, kcol, hi.key_type, a.ts, a.ordinals,
+  hipLaunchKernelGGL(prep_kernel, dim3(grid_rd), dim3(512), 0, s, kcol, hi.key_type, vlong, a.ts, a.ordinals,
                      a.ordinal_base, n, c);
   tmark("prep");
   Ctrl hc;
@@ -904,7 +1063,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     }
     if ((unsigned long long)(hc.ts_last - hc.ts0) >= 0xffffffffull) return bail();
   }
-  if (hc.omax >= 0x7fffffffull) return bail();
+  if (hc.omax >= 0x7fffffffull || hc.bad_ord) return bail();
   int kbits = 0;
   int64_t kmin = 0;
   if (keyed) {
@@ -912,6 +1071,23 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     kbits = std::max(1, bits_for(span));
     if (kbits > 30) return bail();
     kmin = (int64_t)(hc.kmin ^ 0x8000000000000000ull);
+  }
+  // value code of the compared attribute
+  int vmode = VC_I32;
+  int64_t vmin = 0;
+  bool exact_codes = true;
+  switch (hi.vtype) {
+    case T_INT: vmode = VC_I32; break;
+    case T_FLOAT: vmode = VC_F32; break;
+    case T_DOUBLE: vmode = VC_F64; exact_codes = false; break;
+    default:
+      if (keyed && hc.vmax - hc.vmin <= 0xffffffffull) {
+        vmode = VC_I64R;
+        vmin = (int64_t)(hc.vmin ^ 0x8000000000000000ull);
+      } else {
+        vmode = VC_I64H;
+        exact_codes = false;
+      }
   }
   const int fpass = keyed ? (kbits + kRB - 1) / kRB : 0;
   const int jbits = std::max(1, bits_for(hc.omax));
@@ -949,9 +1125,13 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     tmark("scan");
   };
 
-  RecSoA A{}, B{};
-  uint32_t *stj = nullptr, *sti = nullptr;  // walk staging (chunk-local compaction)
-  uint32_t *pj = nullptr, *pi = nullptr, *qj = nullptr, *qi = nullptr;  // j-sort ping-pong
+  // c1 of every event, once
+  uint64_t* c1mask = (uint64_t*)sc.take(((n + 63) / 64) * 8);
+  hipLaunchKernelGGL(c1_mask_kernel, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, s, a.st,
+                     n, a.code + a.c1_off, a.c1_len, a.consts, c1mask);
+  tmark("c1_mask");
+  uint64_t* stq = nullptr;                // walk staging (chunk-local compaction), (j << 32) | i
+  uint64_t *pq = nullptr, *qq = nullptr;  // j-sort ping-pong
   WalkArgs wa{};
   wa.st = a.st;
   wa.ts = a.ts;
@@ -966,16 +1146,11 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   wa.vtype = hi.vtype;
   wa.within = a.within;
   wa.n = n;
-  const int spec = c2_spec(hi);
+  wa.exact_codes = exact_codes;
+  wa.c1mask = c1mask;
   if (keyed) {
-    A.k = (uint32_t*)sc.take(n * 4);
-    A.f0 = (uint32_t*)sc.take(n * 4);
-    A.f1 = (uint64_t*)sc.take(n * 8);
-    A.f2 = (uint32_t*)sc.take(n * 4);
-    B.k = (uint32_t*)sc.take(n * 4);
-    B.f0 = (uint32_t*)sc.take(n * 4);
-    B.f1 = (uint64_t*)sc.take(n * 8);
-    B.f2 = (uint32_t*)sc.take(n * 4);
+    uint4* A = (uint4*)sc.take(n * 16);
+    uint4* B = (uint4*)sc.take(n * 16);
     // key pass 0 from the original columns
     if (hi.key_type == T_INT)
       hipLaunchKernelGGL((upsweep_kernel<KeyColDigits<int32_t>>), dim3(G), dim3(kBlock), 0, s,
@@ -985,50 +1160,42 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
                          KeyColDigits<int64_t>{(const int64_t*)kcol, kmin}, n, per, G, 0, cnt);
     tmark("key_up");
     scan_counts(G);
-    if (hi.key_type == T_INT) launch_down0_k<int32_t>(hi, a, kcol, kmin, hc.ts0, G, per, s, A, cnt, dbase);
-    else launch_down0_k<int64_t>(hi, a, kcol, kmin, hc.ts0, G, per, s, A, cnt, dbase);
+    if (hi.key_type == T_INT)
+      launch_down0_k<int32_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
+    else launch_down0_k<int64_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
     tmark("key_pass0");
-    RecSoA* cur = &A;
-    RecSoA* nxt = &B;
+    uint4* cur = A;
+    uint4* nxt = B;
     for (int p = 1; p < fpass; ++p) {
-      hipLaunchKernelGGL((upsweep_kernel<U32Digits>), dim3(G), dim3(kBlock), 0, s, U32Digits{cur->k}, n, per, G,
+      hipLaunchKernelGGL((upsweep_kernel<RecDigits>), dim3(G), dim3(kBlock), 0, s, RecDigits{cur}, n, per, G,
                          p * kRB, cnt);
       tmark("key_up");
       scan_counts(G);
-      RecSrc rs{cur->k, cur->f0, cur->f1, cur->f2};
-      hipLaunchKernelGGL((downsweep_kernel<1, RecSrc>), dim3(G), dim3(kBlock), 0, s, rs, *nxt, nullptr, nullptr,
-                         nullptr, n, per, nullptr, G, p * kRB, cnt, dbase);
+      hipLaunchKernelGGL((downsweep_kernel<1, RecSrc>), dim3(G), dim3(kBlock), 0, s, RecSrc{cur}, nxt, nullptr, n, per,
+                         nullptr, G, p * kRB, cnt, dbase);
       tmark("key_pass");
       std::swap(cur, nxt);
     }
     if (tm) SM_HIP(hipEventRecord(tm->ev[1], s));
-    wa.k = cur->k;
-    wa.f0 = cur->f0;
-    wa.f1 = cur->f1;
-    wa.f2 = cur->f2;
-    // staging in the dead record buffer; j ping-pong: nxt->f1 (2n u32) and, after the walk, cur->k / cur->f0
-    stj = nxt->k;
-    sti = nxt->f0;
-    pj = (uint32_t*)nxt->f1;
-    pi = (uint32_t*)nxt->f1 + n;
-    qj = cur->k;
-    qi = cur->f0;
-    launch_walk<true>(spec, Gw, s, wa, perw, stj, sti, mcount, cnt);
+    wa.rec = cur;
+    // staging + one ping-pong buffer in the dead record buffer (2 x 8n of its 16n bytes); the other in `cur`
+    // once the walk is done
+    stq = (uint64_t*)nxt;
+    pq = (uint64_t*)nxt + n;
+    qq = (uint64_t*)cur;
+    launch_walk<true>(spec, Gw, s, wa, perw, stq, mcount, cnt);
   } else {
     if (tm) SM_HIP(hipEventRecord(tm->ev[1], s));
-    stj = (uint32_t*)sc.take(n * 4);
-    sti = (uint32_t*)sc.take(n * 4);
-    pj = (uint32_t*)sc.take(n * 4);
-    pi = (uint32_t*)sc.take(n * 4);
-    qj = (uint32_t*)sc.take(n * 4);
-    qi = (uint32_t*)sc.take(n * 4);
-    launch_walk<false>(spec, Gw, s, wa, perw, stj, sti, mcount, cnt);
+    stq = (uint64_t*)sc.take(n * 8);
+    pq = (uint64_t*)sc.take(n * 8);
+    qq = (uint64_t*)sc.take(n * 8);
+    launch_walk<false>(spec, Gw, s, wa, perw, stq, mcount, cnt);
   }
   tmark("walk");
   if (tm) SM_HIP(hipEventRecord(tm->ev[2], s));
 
-  // order by j: LSD passes over (j, i); the first reads the walk's chunk-local staging (its digit-0 counts
-  // came from the walk), the last writes the interleaved output
+  // order by j: LSD passes over the (j, i) pairs; the first reads the walk's chunk-local staging (its digit-0
+  // counts came from the walk), the last writes the output
   std::vector<uint32_t> hm(Gw);
   SM_HIP(hipMemcpyAsync(hm.data(), mcount, sizeof(uint32_t) * Gw, hipMemcpyDeviceToHost, s));
   scan_counts(Gw);
@@ -1041,12 +1208,12 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   }
   if (M > 0) {
     const int64_t perM = round_up((M + G - 1) / G, kTile);
-    uint32_t *cj = stj, *ci = sti;
-    uint32_t* outs[2][2] = {{pj, pi}, {qj, qi}};
+    const uint64_t* cq = stq;
+    uint64_t* outs[2] = {pq, qq};
     for (int p = 0; p < jpass; ++p) {
       const bool last = p == jpass - 1;
       if (p > 0) {
-        hipLaunchKernelGGL((upsweep_kernel<U32Digits>), dim3(G), dim3(kBlock), 0, s, U32Digits{cj}, M, perM, G,
+        hipLaunchKernelGGL((upsweep_kernel<PairDigits>), dim3(G), dim3(kBlock), 0, s, PairDigits{cq}, M, perM, G,
                            p * kRB, cnt);
         tmark("j_up");
         scan_counts(G);
@@ -1055,20 +1222,11 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
       const int64_t pp = p == 0 ? perw : perM;
       const uint32_t* seg = p == 0 ? mcount : nullptr;
       const int gg = p == 0 ? Gw : G;
-      PairSrc ps{cj, ci};
-      if (last) {
-        hipLaunchKernelGGL((downsweep_kernel<3, PairSrc>), dim3(gg), dim3(kBlock), 0, s, ps, RecSoA{}, nullptr, nullptr,
-                           (uint64_t*)pairs_out, nn, pp, seg, gg, p * kRB, cnt, dbase);
-        tmark("j_pass_last");
-      } else {
-        uint32_t* nj = outs[p & 1][0];
-        uint32_t* ni = outs[p & 1][1];
-        hipLaunchKernelGGL((downsweep_kernel<2, PairSrc>), dim3(gg), dim3(kBlock), 0, s, ps, RecSoA{}, nj, ni, nullptr,
-                           nn, pp, seg, gg, p * kRB, cnt, dbase);
-        tmark("j_pass");
-        cj = nj;
-        ci = ni;
-      }
+      uint64_t* nq = last ? (uint64_t*)pairs_out : outs[p & 1];
+      hipLaunchKernelGGL((downsweep_kernel<2, PairSrc>), dim3(gg), dim3(kBlock), 0, s, PairSrc{cq}, nullptr, nq, nn,
+                         pp, seg, gg, p * kRB, cnt, dbase);
+      tmark(last ? "j_pass_last" : "j_pass");
+      cq = nq;
     }
   }
   if (tm) SM_HIP(hipEventRecord(tm->ev[3], s));

@@ -99,6 +99,7 @@ def test_variants_match_oracle(variant):
         kw["c1"] = "[price > 30 and volume < 1500]"
     elif variant == "c2_const":
         kw["c2"] = "price > e1.price + 5.0"
+        expect_path = 1  # not a fixed compare of the carried attribute: general kernels
     elif variant == "no_within":
         kw["within"] = ""
     elif variant == "no_c1":
