@@ -164,3 +164,50 @@ def test_full_size_properties():
         seg = np.arange(a + 1, b)
         seg = seg[sym[seg] == sym[a]]
         assert not (price[seg] > price[a]).any()
+
+
+VALUE_KINDS = ["double_ties", "double_special", "float", "int", "long_narrow", "long_wide"]
+
+
+def value_column(kind, n, rng):
+    """Compared-attribute columns that exercise the keyed records' value codes: exact codes (INT, FLOAT, narrow
+    LONG), high-half codes with ties resolved from the exact column values (DOUBLE, wide LONG), NaN and -0.0."""
+    if kind == "double_ties":  # many values share the high 32 bits of their order-preserving image
+        return ("double", 50.0 + rng.integers(0, 9, n).astype(np.float64) * 1e-9)
+    if kind == "double_special":
+        pool = np.array([np.nan, -0.0, 0.0, 1.0, -1.0, np.inf, -np.inf, 2.5], dtype=np.float64)
+        return ("double", pool[rng.integers(0, len(pool), n)])
+    if kind == "float":
+        pool = np.array([np.nan, -0.0, 0.0, 1.5, -2.25, 3.0, np.inf], dtype=np.float32)
+        return ("float", np.where(rng.random(n) < 0.5, pool[rng.integers(0, len(pool), n)],
+                                  rng.normal(0, 10, n)).astype(np.float32))
+    if kind == "int":
+        return ("int", rng.integers(-50, 50, n).astype(np.int32))
+    if kind == "long_narrow":
+        return ("long", (rng.integers(0, 1000, n) + (1 << 40)).astype(np.int64))
+    # wide LONG range (> 2^32) with ties in the high 32 bits
+    return ("long", np.where(rng.random(n) < 0.5, rng.integers(0, 7, n), rng.integers(0, 7, n) + (1 << 45))
+            .astype(np.int64) * np.where(rng.random(n) < 0.3, -1, 1))
+
+
+@pytest.mark.parametrize("op", [">", ">=", "==", "!="])
+@pytest.mark.parametrize("kind", VALUE_KINDS)
+def test_value_codes_match_oracle(kind, op):
+    n, K, div = 40000, 300, 20
+    rng = np.random.default_rng(hash((kind, op)) % (1 << 32))
+    vt, price = value_column(kind, n, rng)
+    sym = rng.integers(0, K, n).astype(np.int32)
+    vol = rng.integers(0, 2000, n).astype(np.int64)
+    tsa = np.arange(n, dtype=np.int64)
+    ts = tsa // div
+    text = (f"define stream StockStream (symbol int, price {vt}, volume long, timestamp long); "
+            + PART.format(q=Q.format(c1="", c2=f"price {op} e1.price", within=" within 1 sec")))
+    cols = [sym, price, vol, tsa]
+    exp = oracle_pairs(text, cols, ts)
+    got, path = device_pairs(text, cols, ts)
+    assert path == 2
+    np.testing.assert_array_equal(got, exp)
+    # one rank of a key-sharded run: the exact fallback finds rows through the (sorted) ordinals
+    sel = np.nonzero(sym % 2 == 1)[0]
+    got, _ = device_pairs(text, [c[sel] for c in cols], ts[sel], ordinals=sel.astype(np.int64))
+    np.testing.assert_array_equal(got, exp[sym[exp[:, 0]] % 2 == 1])
