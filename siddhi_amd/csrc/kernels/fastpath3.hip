@@ -37,9 +37,15 @@ namespace sm {
 
 namespace {
 
-constexpr int kBlock = 512;
+#ifndef SM_SB
+#define SM_SB 512
+#endif
+#ifndef SM_SI
+#define SM_SI 8
+#endif
+constexpr int kBlock = SM_SB;
 constexpr int kWaves = kBlock / 64;
-constexpr int kItems = 8;
+constexpr int kItems = SM_SI;
 constexpr int kTile = kBlock * kItems;  // 4096 elements per down-sweep tile
 #ifndef SM_RB
 #define SM_RB 10
@@ -49,8 +55,14 @@ constexpr int kBins = 1 << kRB;
 constexpr int kBinsPerThread = kBins >= kBlock ? kBins / kBlock : 1;  // digits owned per thread
 constexpr uint32_t kKeyMask = 0x7fffffffu;
 constexpr int kUpUnroll = 8;  // independent loads in flight per thread in the up-sweeps
-constexpr int kWalkBlock = 256;
-constexpr int kWalkItems = 4;
+#ifndef SM_WB
+#define SM_WB 512
+#endif
+#ifndef SM_WI
+#define SM_WI 4
+#endif
+constexpr int kWalkBlock = SM_WB;
+constexpr int kWalkItems = SM_WI;
 constexpr int kWalkTile = kWalkBlock * kWalkItems;  // 1024 records per walk tile
 constexpr int kWalkHalo = 256;                      // records staged past the tile for scans that leave it
 constexpr int kWalkLds = kWalkTile + kWalkHalo;
@@ -722,10 +734,7 @@ template <bool KEYED>
 struct WalkLds;
 template <>
 struct WalkLds<true> {
-  uint32_t k[kWalkLds];
-  uint32_t o[kWalkLds];
-  uint32_t c[kWalkLds];
-  uint32_t t[kWalkLds];
+  uint4 r[kWalkLds];  // {key | c1 << 31, ordinal, value code, ts}: one ds_read_b128 per record
 };
 template <>
 struct WalkLds<false> {
@@ -774,8 +783,10 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
     }
   };
   if constexpr (KEYED) prefetch(lo);
+  SM_STAMP_DECL;
 
   for (int64_t base = lo; base < hi; base += kWalkTile) {
+    SM_STAMP(0);
     lds_barrier();  // previous tile's LDS readers are done
     const int nload = (int)((n - base) < kWalkLds ? (n - base) : kWalkLds);
     if constexpr (KEYED) {
@@ -783,10 +794,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       for (int q = 0; q < kPre; ++q) {
         const int e = q * kWalkBlock + threadIdx.x;
         if (e < nload) {
-          L.k[e] = pre[q].x;
-          L.o[e] = pre[q].y;
-          L.c[e] = pre[q].z;
-          L.t[e] = pre[q].w;
+          L.r[e] = pre[q];
         }
       }
       if (base + kWalkTile < hi) prefetch(base + kWalkTile);
@@ -798,6 +806,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       }
     }
     lds_barrier();
+    SM_STAMP(1);
     const int lend = nload;  // staged positions are [0, lend) relative to base
     uint32_t c1m = 0;        // c1 of each item (bit k)
 #pragma unroll 1
@@ -805,65 +814,61 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       const int lu = w * 64 * kWalkItems + k * 64 + lane;
       if (base + lu < hi) {
         bool c;
-        if constexpr (KEYED) c = (L.k[lu] >> 31) != 0;
+        if constexpr (KEYED) c = (L.r[lu].x >> 31) != 0;
         else c = (a.c1mask[(base + lu) >> 6] >> ((base + lu) & 63)) & 1ull;
         if (c) c1m |= 1u << k;
       }
     }
-    // lane-private queue over the items with c1
+    // lane-private queue over the items with c1. The loop body is written branch-light (selects, one
+    // predicated take): every live lane advances its scan by one record per iteration.
     uint32_t hasm = 0, openm = 0;
     uint32_t todo = c1m;
-    int k = -1, v = 0;
+    int k = 0, v = 0;
     uint64_t vu = 0;
     int64_t tu = 0;
     uint32_t key = 0, cu = 0, ou = 0;
-    auto take = [&]() -> bool {
-      if (!todo) return false;
-      k = __ffs(todo) - 1;
+    bool live = false;
+    auto take = [&]() {
+      live = todo != 0;
+      k = live ? __ffs(todo) - 1 : 0;
       todo &= todo - 1;
       const int lu = w * 64 * kWalkItems + k * 64 + lane;
-      tu = L.t[lu];
       if constexpr (KEYED) {
-        key = L.k[lu] & kKeyMask;
-        cu = L.c[lu];
-        ou = L.o[lu];
+        const uint4 r = L.r[lu];
+        key = r.x & kKeyMask;
+        ou = r.y;
+        cu = r.z;
+        tu = r.w;
       } else {
+        tu = L.t[lu];
         vu = L.v[lu];
       }
       v = lu + 1;
-      return true;
     };
-    bool live = take();
+    SM_STAMP(2);
+    take();
     while (__any(live)) {
-      if (live) {
-        if (v >= lend) {  // leaves the staged records: finish from global memory below
-          if (base + v < n) {
-            openm |= 1u << k;
-            sj[k][threadIdx.x] = (uint32_t)v;
-          }
-          live = take();
-        } else {
-          bool stop, hit;
-          if constexpr (KEYED) {
-            stop = (L.k[v] & kKeyMask) != key || (a.within >= 0 && (int64_t)(L.t[v] - (uint32_t)tu) > a.within);
-            hit = !stop && cc(cu, ou, L.c[v], L.o[v]);
-          } else {
-            const int64_t d = L.t[v] - tu;
-            stop = a.within >= 0 && (d < 0 ? -d : d) > a.within;
-            hit = !stop && c2(vu, L.v[v]);
-          }
-          if (stop) {
-            live = take();
-          } else if (hit) {
-            hasm |= 1u << k;
-            sj[k][threadIdx.x] = (uint32_t)v;
-            live = take();
-          } else {
-            ++v;
-          }
-        }
+      const bool inb = v < lend;
+      const int vv = inb ? v : lend - 1;
+      bool stop, hit;
+      if constexpr (KEYED) {
+        const uint4 r = L.r[vv];
+        stop = !inb || (r.x & kKeyMask) != key || (a.within >= 0 && (int64_t)(r.w - (uint32_t)tu) > a.within);
+        hit = live && !stop && cc(cu, ou, r.z, r.y);
+      } else {
+        const int64_t d = L.t[vv] - tu;
+        stop = !inb || (a.within >= 0 && (d < 0 ? -d : d) > a.within);
+        hit = live && !stop && c2(vu, L.v[vv]);
       }
+      const bool open = live && !inb && base + v < n;  // leaves the staged records: finished from global below
+      hasm |= hit ? (1u << k) : 0u;
+      openm |= open ? (1u << k) : 0u;
+      if (hit || open) sj[k][threadIdx.x] = (uint32_t)v;
+      const bool done = live && (stop || hit);
+      ++v;
+      if (done) take();
     }
+    SM_STAMP(3);
     // scans that ran past the staged records
 #pragma unroll 1
     while (openm) {
@@ -874,9 +879,9 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
         bool hit;
         if constexpr (KEYED) {
           const uint4 r = a.rec[p];
-          if ((r.x & kKeyMask) != (L.k[luu] & kKeyMask) || (a.within >= 0 && (int64_t)(r.w - L.t[luu]) > a.within))
-            break;
-          hit = cc(L.c[luu], L.o[luu], r.z, r.y);
+          const uint4 ru = L.r[luu];
+          if ((r.x & kKeyMask) != (ru.x & kKeyMask) || (a.within >= 0 && (int64_t)(r.w - ru.w) > a.within)) break;
+          hit = cc(ru.z, ru.y, r.z, r.y);
         } else {
           const int64_t d = a.ts[p] - L.t[luu];
           if (a.within >= 0 && (d < 0 ? -d : d) > a.within) break;
@@ -889,6 +894,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
         }
       }
     }
+    SM_STAMP(4);
     uint32_t mine = 0;
 #pragma unroll 1
     for (int q = 0; q < kWalkItems; ++q) {
@@ -898,6 +904,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
     }
     if (lane == 0) wtot[w] = mine;
     lds_barrier();
+    SM_STAMP(5);
     uint32_t ob = sh_run, tot = 0;
     for (int q = 0; q < kWalkWaves; ++q) {
       if (q < w) ob += wtot[q];
@@ -912,8 +919,8 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
         const uint32_t jv = sj[q][threadIdx.x];
         uint32_t jo, io;
         if constexpr (KEYED) {
-          jo = jv < (uint32_t)lend ? L.o[jv] : ((const uint32_t*)(a.rec + base + jv))[1];
-          io = L.o[luq];
+          jo = jv < (uint32_t)lend ? L.r[jv].y : ((const uint32_t*)(a.rec + base + jv))[1];
+          io = L.r[luq].y;
         } else {
           const int64_t vj = base + jv, ui = base + luq;
           jo = a.ord ? (uint32_t)(a.ord[vj] - a.obase) : (uint32_t)vj;
@@ -926,7 +933,9 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
     }
     lds_barrier();  // every wave read sh_run / wtot
     if (threadIdx.x == 0) sh_run += tot;
+    SM_STAMP(6);
   }
+  SM_STAMP_FLUSH;
   __syncthreads();
   if (threadIdx.x == 0) mcount[blockIdx.x] = sh_run;
   for (int d = threadIdx.x; d < kBins; d += kWalkBlock) jcnt[(int64_t)d * G + blockIdx.x] = jh[d];

@@ -24,6 +24,22 @@ __global__ void fill_kernel(uint4* r, int64_t n, int kbits) {
                     (uint32_t)(z >> 32), (uint32_t)(i / 10000));
 }
 
+// sorted keyed records shaped like config 4 after the key sort: runs of R records per key, ordinals increasing
+// within a run, ts = ordinal / 10000, random value codes, c1 on ~80 %
+__global__ void fill_sorted(uint4* r, int64_t n, int64_t K) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t R = n / K;
+  const int64_t key = i / R, j = i % R;
+  const uint64_t ord = (uint64_t)(j * K + key);
+  uint64_t z = ord * 0x9E3779B97F4A7C15ull + 99;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 31;
+  const bool c1 = (z % 100) >= 20;
+  r[i] = make_uint4((uint32_t)key | (c1 ? 0x80000000u : 0u), (uint32_t)ord, (uint32_t)(z >> 32),
+                    (uint32_t)(ord / 10000));
+}
+
 __global__ void fill_pairs(uint64_t* q, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -34,6 +50,8 @@ __global__ void fill_pairs(uint64_t* q, int64_t n) {
 }
 
 static const char* kPhase[6] = {"loads+zero", "rank", "digit scan", "key xchg+store", "payload xchg", "tail"};
+static const char* kWalkPhase[6] = {"stage", "c1", "scan", "open scans", "ballots", "output"};
+static const char** gPhase = kPhase;
 
 static void report_stamps(const char* what) {
 #ifdef SM_STAMPS
@@ -42,7 +60,7 @@ static void report_stamps(const char* what) {
   unsigned long long tot = 0;
   for (int i = 0; i < 6; ++i) tot += h[i];
   printf("  %s phase shares:", what);
-  for (int i = 0; i < 6; ++i) printf(" %s %.1f%%", kPhase[i], tot ? 100.0 * h[i] / tot : 0.0);
+  for (int i = 0; i < 6; ++i) printf(" %s %.1f%%", gPhase[i], tot ? 100.0 * h[i] / tot : 0.0);
   printf("\n");
   unsigned long long z[16] = {};
   CK(hipMemcpyToSymbol(HIP_SYMBOL(sm_stamps), z, sizeof(z)));
@@ -113,6 +131,52 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&dn, e2, e3));
     printf("pair pass: down %.3f ms (%.0f GB/s)\n", dn, n * 16 / (dn * 1e-3) / 1e9);
     report_stamps("pair");
+  }
+  // walk over sorted records (keyed, c2 = e2 > e1 on exact codes)
+  {
+    const int64_t K = 1000000;
+    hipLaunchKernelGGL(fill_sorted, dim3((n + 255) / 256), dim3(256), 0, 0, A, n, K);
+    int wwpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&wwpc, walk_kernel<true, CMP_GT, false>, kWalkBlock, 0));
+    const int Gw = (int)std::min<int64_t>((n + kWalkTile - 1) / kWalkTile, (int64_t)wwpc * cus);
+    const int64_t perw = round_up((n + Gw - 1) / Gw, kWalkTile);
+    uint32_t *mcount, *jcnt;  // per walk chunk (Gw may exceed the sort grid G the count buffer above is sized for)
+    CK(hipMalloc(&mcount, 4ull * Gw));
+    CK(hipMalloc(&jcnt, 4ull * kBins * Gw));
+    NfaStream hs{};
+    hs.nattr = 4;
+    hs.types[1] = T_LONG;
+    hs.cols[1] = A;  // never read: exact codes
+    NfaStream* ds;
+    CK(hipMalloc(&ds, sizeof(NfaStream)));
+    CK(hipMemcpy(ds, &hs, sizeof(hs), hipMemcpyHostToDevice));
+    WalkArgs wa{};
+    wa.rec = A;
+    wa.st = ds;
+    wa.vattr = 1;
+    wa.vtype = T_LONG;
+    wa.within = 1000;
+    wa.n = n;
+    wa.exact_codes = true;
+    gPhase = kWalkPhase;
+    printf("walk: G=%d per=%lld wgs/cu=%d\n", Gw, (long long)perw, wwpc);
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipEventRecord(e2));
+      if ((int64_t)Gw * perw < n) throw std::runtime_error("walk chunks do not cover the records");
+      hipLaunchKernelGGL((walk_kernel<true, CMP_GT, false>), dim3(Gw), dim3(kWalkBlock), 0, 0, wa, perw, Gw, P, mcount,
+                         jcnt);
+      CK(hipEventRecord(e3));
+      CK(hipDeviceSynchronize());
+      float dn = 0;
+      CK(hipEventElapsedTime(&dn, e2, e3));
+      std::vector<uint32_t> hm(Gw);
+      CK(hipMemcpy(hm.data(), mcount, 4ull * Gw, hipMemcpyDeviceToHost));
+      long long M = 0;
+      for (auto x : hm) M += x;
+      printf("walk: %.3f ms, %lld matches (%.0f GB/s of 16 B/record + 8 B/match)\n", dn, M,
+             (n * 16.0 + M * 8.0) / (dn * 1e-3) / 1e9);
+      report_stamps("walk");
+    }
   }
   return 0;
 }
