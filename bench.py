@@ -217,13 +217,12 @@ def main():
 
 # Kernels of the device pipeline (labels recorded by kernels/fastpath2.hip) and their ALGORITHMIC bytes per
 # launch for a batch of n events with m matches: what each launch must read and write at minimum.
-KERNELS = ["prep", "c1_mask", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last"]
+KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last"]
 
 
 def alg_bytes(label, n, m):
-    return {"prep": 12 * n,                 # key i32 + ts i64
-            "c1_mask": 8 * n + n // 8,      # price f64 in (c1 = price > 20), one bit out
-            "key_up": 4 * n,                # key digits (i32)
+    return {"prep": 20 * n + n // 8,        # key i32 + ts i64 + price f64 (c1 = price > 20) in, c1 bit out
+            "key_up": 16 * n,               # pass-1 digits: one 16-B record per event (the key word of each)
             "scan": 0,                      # per-chunk digit counts (O(chunks x 1024), not per event)
             "key_pass0": 20 * n + 16 * n,   # key i32 + price f64 + ts i64 in, 16-B keyed record out
             "key_pass": 16 * n + 16 * n,    # 16-B record in and out

@@ -338,42 +338,72 @@ __device__ __forceinline__ void chunk_range(int g, int64_t n, int64_t per, const
 
 // ---------------------------------------------------------------- prep
 
-__global__ void prep_kernel(const void* __restrict__ kcol, int ktype, const int64_t* __restrict__ vlong,
-                            const int64_t* __restrict__ ts, const int64_t* __restrict__ ord, int64_t obase, int64_t n,
-                            Ctrl* __restrict__ c) {
+// One read of the key, ts (and ordinal / LONG attribute) columns per event, per chunk of the sort grid:
+//   * key min/max, ts monotonicity, max relative ordinal, ordinals increasing, LONG attribute range → Ctrl
+//   * c1 of every event as a bit mask (bit p & 63 of word p >> 6; ballot per wave)
+//   * per-chunk counts of the pass-0 digit. Keys are rebased by kmin rounded down to a multiple of kBins, so
+//     the low digit of the rebased key is the low digit of the key itself and needs no kmin yet.
+template <typename KT>
+__global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kcol, const int64_t* __restrict__ vlong,
+                                                      const int64_t* __restrict__ ts, const int64_t* __restrict__ ord,
+                                                      int64_t obase, int64_t n, int64_t per, int G,
+                                                      const NfaStream* __restrict__ st, const Instr* __restrict__ c1code,
+                                                      int c1len, const DVal* __restrict__ consts,
+                                                      uint64_t* __restrict__ c1mask, uint32_t* __restrict__ cnt,
+                                                      Ctrl* __restrict__ c) {
+  __shared__ uint32_t h[kBins];
+  for (int d = threadIdx.x; d < kBins; d += kBlock) h[d] = 0;
+  __syncthreads();
+  const Cond c1 = make_cond(c1code, c1len, consts);
+  const int lane = threadIdx.x & 63;
+  int64_t lo0, len;
+  chunk_range(blockIdx.x, n, per, nullptr, lo0, len);
+  const int64_t hi0 = lo0 + len;
   unsigned long long lo = ~0ull, hi = 0, om = 0, vlo = ~0ull, vhi = 0;
   unsigned int bad = 0, bado = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (kcol) {
-      int64_t k = ktype == T_INT ? (int64_t)((const int32_t*)kcol)[i] : ((const int64_t*)kcol)[i];
-      unsigned long long u = (unsigned long long)k ^ 0x8000000000000000ull;
-      lo = u < lo ? u : lo;
-      hi = u > hi ? u : hi;
+  constexpr int kU = 4;  // elements per thread per iteration (independent loads in flight)
+  for (int64_t b = lo0 + threadIdx.x; b - lane < hi0; b += kBlock * kU)  // wave-uniform trip count
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int64_t p = b + u * kBlock;
+    if (p - lane >= hi0) break;
+    const bool in = p < hi0;
+    if (in) {
+      if (kcol) {
+        const int64_t k = (int64_t)kcol[p];
+        const unsigned long long u = (unsigned long long)k ^ 0x8000000000000000ull;
+        lo = u < lo ? u : lo;
+        hi = u > hi ? u : hi;
+        atomicAdd(&h[(uint32_t)k & (kBins - 1)], 1u);
+      }
+      if (vlong) {
+        const unsigned long long u = (unsigned long long)vlong[p] ^ 0x8000000000000000ull;
+        vlo = u < vlo ? u : vlo;
+        vhi = u > vhi ? u : vhi;
+      }
+      if (p > 0 && ts[p] < ts[p - 1]) bad = 1;
+      if (ord) {
+        const unsigned long long o = (unsigned long long)(ord[p] - obase);
+        om = o > om ? o : om;
+        if (p > 0 && ord[p] <= ord[p - 1]) bado = 1;
+      }
     }
-    if (vlong) {
-      unsigned long long u = (unsigned long long)vlong[i] ^ 0x8000000000000000ull;
-      vlo = u < vlo ? u : vlo;
-      vhi = u > vhi ? u : vhi;
-    }
-    if (i > 0 && ts[i] < ts[i - 1]) bad = 1;
-    if (ord) {
-      unsigned long long o = (unsigned long long)(ord[i] - obase);
-      om = o > om ? o : om;
-      if (i > 0 && ord[i] <= ord[i - 1]) bado = 1;
-    }
+    const bool cv = in && eval(c1, RowLoader{st, p});
+    const uint64_t bal = __ballot(cv);
+    if (lane == 0 && p < hi0) c1mask[p >> 6] = bal;
   }
   for (int o = 32; o > 0; o >>= 1) {
-    unsigned long long a = __shfl_down(lo, o, 64), b = __shfl_down(hi, o, 64), d = __shfl_down(om, o, 64);
+    unsigned long long x = __shfl_down(lo, o, 64), y = __shfl_down(hi, o, 64), z = __shfl_down(om, o, 64);
     unsigned long long e = __shfl_down(vlo, o, 64), f = __shfl_down(vhi, o, 64);
-    lo = a < lo ? a : lo;
-    hi = b > hi ? b : hi;
-    om = d > om ? d : om;
+    lo = x < lo ? x : lo;
+    hi = y > hi ? y : hi;
+    om = z > om ? z : om;
     vlo = e < vlo ? e : vlo;
     vhi = f > vhi ? f : vhi;
   }
   bad = __any(bad) ? 1u : 0u;
   bado = __any(bado) ? 1u : 0u;
-  if ((threadIdx.x & 63) == 0) {
+  if (lane == 0) {
     if (kcol) {
       atomicMin(&c->kmin, lo);
       atomicMax(&c->kmax, hi);
@@ -391,20 +421,9 @@ __global__ void prep_kernel(const void* __restrict__ kcol, int ktype, const int6
     c->ts_last = ts[n - 1];
     if (!ord) c->omax = (unsigned long long)(n - 1);
   }
-}
-
-// c1 of every event as a bit mask (bit p & 63 of word p >> 6): one lane per event, ballot per wave. Evaluated
-// once here, at full occupancy, instead of inside the sort tiles (where its loads would be serialised).
-__global__ void __launch_bounds__(256) c1_mask_kernel(const NfaStream* __restrict__ st, int64_t n,
-                                                      const Instr* __restrict__ code, int len,
-                                                      const DVal* __restrict__ consts, uint64_t* __restrict__ mask) {
-  const Cond c1 = make_cond(code, len, consts);
-  const int lane = threadIdx.x & 63;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p - lane < n; p += (int64_t)gridDim.x * blockDim.x) {
-    const bool c = p < n && eval(c1, RowLoader{st, p});
-    const uint64_t bal = __ballot(c);
-    if (lane == 0) mask[p >> 6] = bal;
-  }
+  __syncthreads();
+  if (kcol)
+    for (int d = threadIdx.x; d < kBins; d += kBlock) cnt[(int64_t)d * G + blockIdx.x] = h[d];
 }
 
 // ---------------------------------------------------------------- up-sweeps and scans
@@ -1050,7 +1069,6 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   }
   const void* kcol = keyed ? hi.cols[hi.key_col] : nullptr;
   const int64_t* vlong = (keyed && hi.vtype == T_LONG) ? (const int64_t*)hi.cols[hi.vattr] : nullptr;
-  const unsigned grid_rd = (unsigned)std::min<int64_t>(2048, (n + 511) / 512);
   if (tm) {
     SM_HIP(hipEventRecord(tm->ev[0], s));
     tm->nmk = 0;
@@ -1059,48 +1077,6 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   auto tmark = [&](const char* l) {
     if (tm) tm->mark(l, s);
   };
-  hipLaunchKernelGGL(prep_kernel, dim3(grid_rd), dim3(512), 0, s, kcol, hi.key_type, vlong, a.ts, a.ordinals,
-                     a.ordinal_base, n, c);
-  tmark("prep");
-  Ctrl hc;
-  SM_HIP(hipMemcpyAsync(&hc, c, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
-  SM_HIP(hipStreamSynchronize(s));
-  if (a.within >= 0) {
-    if (hc.bad_ts) {
-      sc.used = mark;
-      throw std::runtime_error("fast path requires non-decreasing event timestamps within a device batch");
-    }
-    if ((unsigned long long)(hc.ts_last - hc.ts0) >= 0xffffffffull) return bail();
-  }
-  if (hc.omax >= 0x7fffffffull || hc.bad_ord) return bail();
-  int kbits = 0;
-  int64_t kmin = 0;
-  if (keyed) {
-    const uint64_t span = hc.kmax - hc.kmin;
-    kbits = std::max(1, bits_for(span));
-    if (kbits > 30) return bail();
-    kmin = (int64_t)(hc.kmin ^ 0x8000000000000000ull);
-  }
-  // value code of the compared attribute
-  int vmode = VC_I32;
-  int64_t vmin = 0;
-  bool exact_codes = true;
-  switch (hi.vtype) {
-    case T_INT: vmode = VC_I32; break;
-    case T_FLOAT: vmode = VC_F32; break;
-    case T_DOUBLE: vmode = VC_F64; exact_codes = false; break;
-    default:
-      if (keyed && hc.vmax - hc.vmin <= 0xffffffffull) {
-        vmode = VC_I64R;
-        vmin = (int64_t)(hc.vmin ^ 0x8000000000000000ull);
-      } else {
-        vmode = VC_I64H;
-        exact_codes = false;
-      }
-  }
-  const int fpass = keyed ? (kbits + kRB - 1) / kRB : 0;
-  const int jbits = std::max(1, bits_for(hc.omax));
-  const int jpass = (jbits + kRB - 1) / kRB;
 
   // persistent chunking: G workgroups (as many as the down-sweep keeps resident), chunks of whole sort tiles
   if (fs.cus == 0) {
@@ -1128,17 +1104,64 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   uint32_t* cnt = (uint32_t*)sc.take(sizeof(uint32_t) * kBins * std::max(G, Gw));
   uint32_t* dbase = (uint32_t*)sc.take(sizeof(uint32_t) * kBins);
   uint32_t* mcount = (uint32_t*)sc.take(sizeof(uint32_t) * Gw);
+  uint64_t* c1mask = (uint64_t*)sc.take(((n + 63) / 64) * 8);
   auto scan_counts = [&](int g) {
     hipLaunchKernelGGL(scan_chunks_kernel, dim3(kBins), dim3(256), 0, s, cnt, g, dbase);
     hipLaunchKernelGGL(digit_base_kernel, dim3(1), dim3(kBlock), 0, s, dbase);
     tmark("scan");
   };
 
-  // c1 of every event, once
-  uint64_t* c1mask = (uint64_t*)sc.take(((n + 63) / 64) * 8);
-  hipLaunchKernelGGL(c1_mask_kernel, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, s, a.st,
-                     n, a.code + a.c1_off, a.c1_len, a.consts, c1mask);
-  tmark("c1_mask");
+  // column facts + c1 mask + pass-0 digit counts, one pass
+  if (hi.key_type == T_LONG && keyed)
+    hipLaunchKernelGGL((prep_kernel<int64_t>), dim3(G), dim3(kBlock), 0, s, (const int64_t*)kcol, vlong, a.ts,
+                       a.ordinals, a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt,
+                       c);
+  else
+    hipLaunchKernelGGL((prep_kernel<int32_t>), dim3(G), dim3(kBlock), 0, s, (const int32_t*)kcol, vlong, a.ts,
+                       a.ordinals, a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt,
+                       c);
+  tmark("prep");
+  Ctrl hc;
+  SM_HIP(hipMemcpyAsync(&hc, c, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  if (a.within >= 0) {
+    if (hc.bad_ts) {
+      sc.used = mark;
+      throw std::runtime_error("fast path requires non-decreasing event timestamps within a device batch");
+    }
+    if ((unsigned long long)(hc.ts_last - hc.ts0) >= 0xffffffffull) return bail();
+  }
+  if (hc.omax >= 0x7fffffffull || hc.bad_ord) return bail();
+  int kbits = 0;
+  int64_t kmin = 0;
+  if (keyed) {
+    kmin = (int64_t)(hc.kmin ^ 0x8000000000000000ull);
+    kmin &= ~(int64_t)(kBins - 1);  // rebase on a digit boundary (prep counted digit 0 of the raw key)
+    const uint64_t span = (uint64_t)((int64_t)(hc.kmax ^ 0x8000000000000000ull) - kmin);
+    kbits = std::max(1, bits_for(span));
+    if (kbits > 30) return bail();
+  }
+  // value code of the compared attribute
+  int vmode = VC_I32;
+  int64_t vmin = 0;
+  bool exact_codes = true;
+  switch (hi.vtype) {
+    case T_INT: vmode = VC_I32; break;
+    case T_FLOAT: vmode = VC_F32; break;
+    case T_DOUBLE: vmode = VC_F64; exact_codes = false; break;
+    default:
+      if (keyed && hc.vmax - hc.vmin <= 0xffffffffull) {
+        vmode = VC_I64R;
+        vmin = (int64_t)(hc.vmin ^ 0x8000000000000000ull);
+      } else {
+        vmode = VC_I64H;
+        exact_codes = false;
+      }
+  }
+  const int fpass = keyed ? (kbits + kRB - 1) / kRB : 0;
+  const int jbits = std::max(1, bits_for(hc.omax));
+  const int jpass = (jbits + kRB - 1) / kRB;
+
   uint64_t* stq = nullptr;                // walk staging (chunk-local compaction), (j << 32) | i
   uint64_t *pq = nullptr, *qq = nullptr;  // j-sort ping-pong
   WalkArgs wa{};
@@ -1160,14 +1183,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   if (keyed) {
     uint4* A = (uint4*)sc.take(n * 16);
     uint4* B = (uint4*)sc.take(n * 16);
-    // key pass 0 from the original columns
-    if (hi.key_type == T_INT)
-      hipLaunchKernelGGL((upsweep_kernel<KeyColDigits<int32_t>>), dim3(G), dim3(kBlock), 0, s,
-                         KeyColDigits<int32_t>{(const int32_t*)kcol, kmin}, n, per, G, 0, cnt);
-    else
-      hipLaunchKernelGGL((upsweep_kernel<KeyColDigits<int64_t>>), dim3(G), dim3(kBlock), 0, s,
-                         KeyColDigits<int64_t>{(const int64_t*)kcol, kmin}, n, per, G, 0, cnt);
-    tmark("key_up");
+    // key pass 0 from the original columns (its digit counts came from prep)
     scan_counts(G);
     if (hi.key_type == T_INT)
       launch_down0_k<int32_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
