@@ -317,9 +317,13 @@ struct C2Code {
     }
   }
   __device__ __forceinline__ bool operator()(uint32_t c1, uint32_t o1, uint32_t c2, uint32_t o2) const {
-    const bool nan = FP && (c1 == kNanCode || c2 == kNanCode);
-    if (!nan && (exact_codes || c1 != c2)) return cmp_fixed<OP>(c2, c1);
+    if (!needs_exact(c1, c2)) return cmp_fixed<OP>(c2, c1);
     return exact(o1, o2);
+  }
+  // the codes alone do not decide the comparison (equal inexact codes, or a NaN)
+  __device__ __forceinline__ bool needs_exact(uint32_t c1, uint32_t c2) const {
+    const bool nan = FP & ((c1 == kNanCode) | (c2 == kNanCode));
+    return nan | (!exact_codes & (c1 == c2));
   }
 };
 
@@ -871,9 +875,15 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       const int vv = inb ? v : lend - 1;
       bool stop, hit;
       if constexpr (KEYED) {
+        // straight-line step: one ds_read_b128, conditions combined without short-circuit branches; the rare
+        // exact comparisons run afterwards for the lanes that need them
         const uint4 r = L.r[vv];
-        stop = !inb || (r.x & kKeyMask) != key || (a.within >= 0 && (int64_t)(r.w - (uint32_t)tu) > a.within);
-        hit = live && !stop && cc(cu, ou, r.z, r.y);
+        const bool expired = (a.within >= 0) & ((int64_t)(r.w - (uint32_t)tu) > a.within);
+        stop = (!inb) | (((r.x ^ key) & kKeyMask) != 0u) | expired;
+        const bool ex = live & !stop & cc.needs_exact(cu, r.z);
+        hit = live & !stop & !ex & cmp_fixed<OP>(r.z, cu);
+        if (__any(ex))
+          if (ex) hit = cc.exact(ou, r.y);
       } else {
         const int64_t d = L.t[vv] - tu;
         stop = !inb || (a.within >= 0 && (d < 0 ? -d : d) > a.within);
