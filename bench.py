@@ -215,7 +215,7 @@ def main():
         dist.destroy_process_group()
 
 
-# Kernels of the device pipeline (labels recorded by kernels/fastpath2.hip) and their ALGORITHMIC bytes per
+# Kernels of the device pipeline (labels recorded by kernels/fastpath3.hip) and their ALGORITHMIC bytes per
 # launch for a batch of n events with m matches: what each launch must read and write at minimum.
 KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last"]
 

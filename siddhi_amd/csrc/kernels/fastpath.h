@@ -1,5 +1,5 @@
 // Host entry of the closed-form `every e1 -> e2 within T` kernels (fastpath.hip: general form;
-// fastpath2.hip: onesweep/bandwidth form for single-column keys and a single compared attribute).
+// fastpath3.hip: keyed bandwidth form for single-column keys and a single compared attribute).
 #pragma once
 #include "nfa.h"
 #include "primitives.h"
