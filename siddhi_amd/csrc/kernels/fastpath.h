@@ -30,6 +30,8 @@ struct FastHostInfo {
   int vtype = 0;
   const Instr* c2_host = nullptr;  // host copy of the c2 program (specialisation of the walk's compare)
   int c2_len = 0;
+  const Instr* c1_host = nullptr;  // host copy of the c1 program (c1 on the compared attribute: no bit mask)
+  int c1_len = 0;
 };
 
 // Device facts cached across batches by the v2 kernels.

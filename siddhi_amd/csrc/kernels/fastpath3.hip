@@ -27,6 +27,7 @@
 // (and wide LONG) it is the high half of the order-preserving 64-bit image, so `code2 != code1` decides any
 // comparison and equal codes (or NaN) fall back to the exact column values (rare; the record's ordinal gives
 // the row).
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -121,6 +122,21 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// Lanes of this wave whose kRB-bit digit equals this lane's (valid lanes only): one ballot per bit, and per
+// bit one v_bitop3 per half, peers &= bit ? ballot : ~ballot  ==  peers & ~(ballot ^ sext(bit)).
+__device__ __forceinline__ uint64_t peer_mask(uint32_t d, bool valid) {
+  const uint64_t v = __ballot(valid);
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+  for (int bb = 0; bb < kRB; ++bb) {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)d, bb, 1);  // 0 or ~0
+    const uint64_t bal = __ballot(m != 0u);
+    lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)bal, m, 0x90);  // a & ~(b ^ c), a = 0xF0, b = 0xCC, c = 0xAA
+    hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(bal >> 32), m, 0x90);
+  }
+  return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -228,6 +244,16 @@ __device__ __forceinline__ bool eval(const Cond& c, const Ld& ld) {
     return do_compare(c.op, l, r);
   }
   return truthy(eval_prog(c.code, c.len, c.consts, ld));
+}
+
+// c.simple (or empty) conditions only: no interpreter stack in the caller
+template <typename Ld>
+__device__ __forceinline__ bool eval_simple(const Cond& c, const Ld& ld) {
+  if (c.len == 0) return true;
+  const StackVal l = c.a.op == OP_CONST ? c.ka : ld.var(c.a);
+  const StackVal r = c.b.op == OP_CONST ? c.kb : ld.var(c.b);
+  if (l.null || r.null) return c.op.sub == CMP_NE;
+  return do_compare(c.op, l, r);
 }
 
 template <int OP, typename T>
@@ -344,10 +370,12 @@ __device__ __forceinline__ void chunk_range(int g, int64_t n, int64_t per, const
 
 // One read of the key, ts (and ordinal / LONG attribute) columns per event, per chunk of the sort grid:
 //   * key min/max, ts monotonicity, max relative ordinal, ordinals increasing, LONG attribute range → Ctrl
-//   * c1 of every event as a bit mask (bit p & 63 of word p >> 6; ballot per wave)
+//   * MASK: c1 of every event as a bit mask (bit p & 63 of word p >> 6; ballot per wave). Keyed batches whose
+//     c1 reads only the compared attribute skip it: the pass-0 down-sweep evaluates c1 on the value it loads.
 //   * per-chunk counts of the pass-0 digit. Keys are rebased by kmin rounded down to a multiple of kBins, so
 //     the low digit of the rebased key is the low digit of the key itself and needs no kmin yet.
-template <typename KT>
+// Tiles of kTile events (kItems per thread, every load of the tile issued before any is used).
+template <typename KT, bool MASK>
 __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kcol, const int64_t* __restrict__ vlong,
                                                       const int64_t* __restrict__ ts, const int64_t* __restrict__ ord,
                                                       int64_t obase, int64_t n, int64_t per, int G,
@@ -358,43 +386,68 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
   __shared__ uint32_t h[kBins];
   for (int d = threadIdx.x; d < kBins; d += kBlock) h[d] = 0;
   __syncthreads();
-  const Cond c1 = make_cond(c1code, c1len, consts);
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int64_t lo0, len;
   chunk_range(blockIdx.x, n, per, nullptr, lo0, len);
   const int64_t hi0 = lo0 + len;
   unsigned long long lo = ~0ull, hi = 0, om = 0, vlo = ~0ull, vhi = 0;
   unsigned int bad = 0, bado = 0;
-  constexpr int kU = 4;  // elements per thread per iteration (independent loads in flight)
-  for (int64_t b = lo0 + threadIdx.x; b - lane < hi0; b += kBlock * kU)  // wave-uniform trip count
+  for (int64_t base = lo0; base < hi0; base += kTile) {
+    KT kk[kItems];
+    int64_t tt[kItems], oo[kItems], vv[kItems], tp[kItems], op[kItems];
 #pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    const int64_t p = b + u * kBlock;
-    if (p - lane >= hi0) break;
-    const bool in = p < hi0;
-    if (in) {
-      if (kcol) {
-        const int64_t k = (int64_t)kcol[p];
-        const unsigned long long u = (unsigned long long)k ^ 0x8000000000000000ull;
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t p = base + w * 64 * kItems + k * 64 + lane;
+      if (p < hi0) {
+        if (kcol) kk[k] = __builtin_nontemporal_load(kcol + p);
+        tt[k] = __builtin_nontemporal_load(ts + p);
+        if (ord) oo[k] = ord[p];
+        if (vlong) vv[k] = vlong[p];
+        if (lane == 0 && p > 0) {  // the element before each wave-item (other lanes take it from lane - 1)
+          tp[k] = ts[p - 1];
+          if (ord) op[k] = ord[p - 1];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t p = base + w * 64 * kItems + k * 64 + lane;
+      const bool in = p < hi0;
+      int64_t pt = __shfl_up(tt[k], 1, 64);
+      if (lane == 0) pt = p > 0 ? tp[k] : tt[k];
+      if (in && tt[k] < pt) bad = 1;
+      if (ord) {
+        int64_t po = __shfl_up(oo[k], 1, 64);
+        if (lane == 0) po = p > 0 ? op[k] : oo[k] - 1;
+        if (in) {
+          const unsigned long long o = (unsigned long long)(oo[k] - obase);
+          om = o > om ? o : om;
+          if (oo[k] <= po) bado = 1;
+        }
+      }
+      if (in && kcol) {
+        const unsigned long long u = (unsigned long long)(int64_t)kk[k] ^ 0x8000000000000000ull;
         lo = u < lo ? u : lo;
         hi = u > hi ? u : hi;
-        atomicAdd(&h[(uint32_t)k & (kBins - 1)], 1u);
+        atomicAdd(&h[(uint32_t)kk[k] & (kBins - 1)], 1u);
       }
-      if (vlong) {
-        const unsigned long long u = (unsigned long long)vlong[p] ^ 0x8000000000000000ull;
+      if (in && vlong) {
+        const unsigned long long u = (unsigned long long)vv[k] ^ 0x8000000000000000ull;
         vlo = u < vlo ? u : vlo;
         vhi = u > vhi ? u : vhi;
       }
-      if (p > 0 && ts[p] < ts[p - 1]) bad = 1;
-      if (ord) {
-        const unsigned long long o = (unsigned long long)(ord[p] - obase);
-        om = o > om ? o : om;
-        if (p > 0 && ord[p] <= ord[p - 1]) bado = 1;
+    }
+    if constexpr (MASK) {
+      const Cond c1 = make_cond(c1code, c1len, consts);
+#pragma unroll 1
+      for (int k = 0; k < kItems; ++k) {
+        const int64_t p = base + w * 64 * kItems + k * 64 + lane;
+        if (p - lane >= hi0) break;
+        const bool cv = p < hi0 && eval(c1, RowLoader{st, p});
+        const uint64_t bal = __ballot(cv);
+        if (lane == 0) c1mask[p >> 6] = bal;
       }
     }
-    const bool cv = in && eval(c1, RowLoader{st, p});
-    const uint64_t bal = __ballot(cv);
-    if (lane == 0 && p < hi0) c1mask[p >> 6] = bal;
   }
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long x = __shfl_down(lo, o, 64), y = __shfl_down(hi, o, 64), z = __shfl_down(om, o, 64);
@@ -528,11 +581,26 @@ __global__ void __launch_bounds__(kBlock) digit_base_kernel(uint32_t* __restrict
 
 // ---------------------------------------------------------------- down-sweep
 
+// c1 over the compared attribute's value alone (slot-0 variables and stream columns all read that attribute)
+template <typename VT>
+struct ValLoader {
+  VT v;
+  __device__ StackVal var(const Instr&) const {
+    StackVal r;
+    r.i = 0;
+    r.d = 0;
+    r.null = 0;
+    if constexpr (std::is_floating_point<VT>::value) r.d = (double)v;
+    else r.i = (int64_t)v;
+    return r;
+  }
+};
+
 // Pass 0 of the keyed sort: builds the record from the original columns. Key and compared-attribute column
-// types are template parameters; c1 is evaluated once per event in a rolled loop.
+// types are template parameters. c1 comes from prep's bit mask, or (c1_inline: c1 reads only the compared
+// attribute) is evaluated here on the loaded value.
 template <typename KT, typename VT>
 struct OrigSrc {
-  static constexpr bool kC1 = true;
   const NfaStream* st;
   const KT* kcol;
   const VT* vcol;
@@ -544,25 +612,73 @@ struct OrigSrc {
   int64_t ts0;
   const int64_t* ord;
   int64_t obase;
+  const Instr* c1code;
+  int c1len;
+  const DVal* consts;
+  bool c1_inline;
+  Cond c1;
+  __device__ void init() {
+    if (c1_inline) c1 = make_cond(c1code, c1len, consts);
+  }
+  __device__ uint32_t c1_bit(VT v, uint64_t m, int64_t p) const {
+    if (c1_inline) return eval_simple(c1, ValLoader<VT>{v}) ? 1u : 0u;
+    return (uint32_t)(m >> (p & 63)) & 1u;
+  }
   __device__ uint4 rec(int64_t p) const {
     uint4 r;
-    r.x = (uint32_t)((int64_t)kcol[p] - kmin);
+    const VT v = vcol[p];
+    const uint64_t m = c1_inline ? 0ull : c1mask[p >> 6];
+    r.x = (uint32_t)((int64_t)kcol[p] - kmin) | (c1_bit(v, m, p) << 31);
     r.y = ord ? (uint32_t)(ord[p] - obase) : (uint32_t)p;
-    r.z = vcode<VT>(vcol[p], vmode, vmin);
+    r.z = vcode<VT>(v, vmode, vmin);
     r.w = (uint32_t)(ts[p] - ts0);
     return r;
+  }
+  // raw column values of one event (loads in flight until split() uses them) + its c1 mask word
+  struct Raw {
+    KT k;
+    VT v;
+    int64_t t, o;
+    uint64_t m;
+  };
+  __device__ Raw load(int64_t p) const {
+    Raw r;
+    r.k = kcol[p];
+    r.v = vcol[p];
+    r.t = ts[p];
+    r.o = ord ? ord[p] - obase : p;
+    r.m = c1_inline ? 0ull : c1mask[p >> 6];
+    return r;
+  }
+  __device__ void split(const Raw& r, int64_t p, uint64_t& a, uint64_t& b) const {
+    const uint32_t c1 = c1_bit(r.v, r.m, p);
+    a = (uint64_t)((uint32_t)((int64_t)r.k - kmin) | (c1 << 31)) | ((uint64_t)(uint32_t)r.o << 32);
+    b = (uint64_t)vcode<VT>(r.v, vmode, vmin) | ((uint64_t)(uint32_t)(r.t - ts0) << 32);
   }
 };
 
 struct RecSrc {
-  static constexpr bool kC1 = false;
   const uint4* r;
-  __device__ uint4 rec(int64_t p) const { return r[p]; }
+  __device__ void init() {}
+  typedef unsigned int Raw __attribute__((ext_vector_type(4)));
+  // read-once stream: nontemporal loads keep the L2 for the scattered stores (PMC: -10 % pass time)
+  __device__ uint4 rec(int64_t p) const {
+    const Raw v = __builtin_nontemporal_load((const Raw*)r + p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  __device__ Raw load(int64_t p) const { return __builtin_nontemporal_load((const Raw*)r + p); }
+  __device__ void split(const Raw& v, int64_t, uint64_t& a, uint64_t& b) const {
+    a = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    b = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  }
 };
 
 struct PairSrc {  // (j << 32) | i
-  static constexpr bool kC1 = false;
   const uint64_t* q;
+  __device__ void init() {}
+  using Raw = uint64_t;
+  __device__ Raw load(int64_t p) const { return __builtin_nontemporal_load(q + p); }
+  __device__ void split(const Raw& v, int64_t, uint64_t& a, uint64_t&) const { a = v; }
 };
 
 // Down-sweep of one LSD pass over chunk blockIdx.x (persistent: tile by tile, running per-digit offsets).
@@ -582,6 +698,7 @@ downsweep_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dpair
 
   int64_t lo, len;
   chunk_range(blockIdx.x, n, per, seg_len, lo, len);
+  src.init();
   for (int d = threadIdx.x; d < kBins; d += kBlock) run[d] = dbase[d] + cnt[(int64_t)d * G + blockIdx.x];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = lanemask_lt();
@@ -602,19 +719,12 @@ downsweep_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dpair
           a[k] = (uint64_t)r.x | ((uint64_t)r.y << 32);
           b[k] = (uint64_t)r.z | ((uint64_t)r.w << 32);
         } else {
-          a[k] = src.q[p];
+          a[k] = __builtin_nontemporal_load(src.q + p);
         }
       }
     }
     lds_barrier();  // previous tile's readers of wcnt / xb64 / run are done
     for (int k = threadIdx.x; k < kWaves * kBins; k += kBlock) (&wcnt[0][0])[k] = 0;
-    if constexpr (Src::kC1) {  // c1 flag of each item → key bit 31 (one mask word per wave-item)
-#pragma unroll
-      for (int k = 0; k < kItems; ++k) {
-        const int e = w * 64 * kItems + k * 64 + lane;
-        if (e < tile_n && ((src.c1mask[(base + e) >> 6] >> ((base + e) & 63)) & 1ull)) a[k] |= 0x80000000ull;
-      }
-    }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every load of the tile retired (known to the compiler, so no
                                          // later vmcnt wait for them lands behind this tile's stores)
     lds_barrier();
@@ -627,13 +737,7 @@ downsweep_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dpair
       const bool valid = e < tile_n;
       const uint32_t key = MODE <= 1 ? (uint32_t)a[k] : (uint32_t)(a[k] >> 32);
       const uint32_t d = valid ? ((key & kKeyMask) >> shift) & (kBins - 1) : 0u;
-      uint64_t peers = __ballot(valid);
-#pragma unroll
-      for (int bb = 0; bb < kRB; ++bb) {
-        const bool bit = (d >> bb) & 1u;
-        const uint64_t bal = __ballot(bit);
-        peers &= bit ? bal : ~bal;
-      }
+      const uint64_t peers = peer_mask(d, valid);
       uint32_t old = 0;
       if (valid) old = wcnt[w][d];
       const uint32_t below = (uint32_t)__popcll(peers & lt);
@@ -733,6 +837,238 @@ downsweep_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dpair
   SM_STAMP_FLUSH;
 }
 
+// Write-combining down-sweep (same pass semantics as downsweep_kernel). A tile sends about 4 elements to each of
+// its kBins digit runs, so plain scattered stores leave most 64-byte segments of the output partly written by
+// one tile and finished by the next; with 64 workgroups per XCD each holding 1024 runs open, the L2 evicts those
+// partial lines in between and the pass writes ~1.7x its bytes (PMC: TCC_EA0_WRREQ / _64B). Here a tile stores
+// only elements whose 64-byte segment is complete in this chunk's view; the tail of each run (< one segment) is
+// carried in LDS to the next tile, and the last tile of the chunk flushes everything. Loads of tile t+1 are
+// issued as soon as tile t's elements are in LDS, so they overlap tile t's stores.
+#ifndef SM_WCB
+#define SM_WCB 1024
+#endif
+constexpr int kWcBlock = SM_WCB;
+constexpr int kWcWaves = kWcBlock / 64;
+constexpr int kWcItems = kTile / kWcBlock;
+constexpr int kWcBPT = kBins >= kWcBlock ? kBins / kWcBlock : 1;  // digits owned per thread
+static_assert(kTile % kWcBlock == 0, "write-combining tile");
+
+template <int MODE, typename Src>
+__global__ void __launch_bounds__(kWcBlock)
+downsweep_wc_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dpairs, int64_t n, int64_t per,
+                    const uint32_t* seg_len, int G, int shift, const uint32_t* __restrict__ cnt,
+                    const uint32_t* __restrict__ dbase) {
+  constexpr int S = MODE <= 1 ? 4 : 8;   // elements per 64-byte segment
+  constexpr int CW = MODE <= 1 ? 2 : 1;  // 64-bit words per element
+  __shared__ uint64_t xb64[kTile];
+  __shared__ uint16_t wcnt[kWcWaves][kBins];
+  __shared__ uint32_t tstart[kBins + 1];
+  __shared__ uint32_t run[kBins];  // next output position of each digit for this chunk
+  __shared__ uint32_t cst[kBins];  // first carried position of each digit: carry = [cst, run)
+  __shared__ uint64_t carry[kBins * (S - 1) * CW];
+  __shared__ uint32_t lw[kWcWaves];
+
+  int64_t lo, len;
+  chunk_range(blockIdx.x, n, per, seg_len, lo, len);
+  src.init();
+  for (int d = threadIdx.x; d < kBins; d += kWcBlock) {
+    const uint32_t r0 = dbase[d] + cnt[(int64_t)d * G + blockIdx.x];
+    run[d] = r0;
+    cst[d] = r0;
+  }
+  if (threadIdx.x == 0) tstart[kBins] = 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = lanemask_lt();
+  SM_STAMP_DECL;
+
+  typename Src::Raw raw[kWcItems];
+  auto load_tile = [&](int64_t base) {
+    const int64_t rem = lo + len - base;
+    const int tn = rem < kTile ? (int)rem : kTile;
+#pragma unroll
+    for (int k = 0; k < kWcItems; ++k) {
+      const int e = w * 64 * kWcItems + k * 64 + lane;
+      if (e < tn) raw[k] = src.load(base + e);
+    }
+  };
+  if (len > 0) load_tile(lo);
+
+  for (int64_t base = lo; base < lo + len; base += kTile) {
+    SM_STAMP(0);
+    const int tile_n = (int)((lo + len - base) < kTile ? (lo + len - base) : kTile);
+    const bool last = base + kTile >= lo + len;
+    uint64_t a[kWcItems], b[kWcItems];
+#pragma unroll
+    for (int k = 0; k < kWcItems; ++k) {
+      const int e = w * 64 * kWcItems + k * 64 + lane;
+      if (e < tile_n) src.split(raw[k], base + e, a[k], b[k]);
+    }
+    lds_barrier();  // previous tile's readers of wcnt / xb64 / run / tstart are done
+    for (int k = threadIdx.x; k < kWcWaves * kBins; k += kWcBlock) (&wcnt[0][0])[k] = 0;
+    lds_barrier();
+    SM_STAMP(1);
+
+    uint32_t lp[kWcItems];  // rank within (wave, digit), then local sorted position
+#pragma unroll
+    for (int k = 0; k < kWcItems; ++k) {
+      const int e = w * 64 * kWcItems + k * 64 + lane;
+      const bool valid = e < tile_n;
+      const uint32_t key = MODE <= 1 ? (uint32_t)a[k] : (uint32_t)(a[k] >> 32);
+      const uint32_t d = valid ? ((key & kKeyMask) >> shift) & (kBins - 1) : 0u;
+      const uint64_t peers = peer_mask(d, valid);
+      uint32_t old = 0;
+      if (valid) old = wcnt[w][d];
+      const uint32_t below = (uint32_t)__popcll(peers & lt);
+      if (valid && below == 0) wcnt[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
+      lp[k] = old + below;
+    }
+    lds_barrier();
+    SM_STAMP(2);
+
+    // per digit: wave offsets (exclusive, in place) and the tile count
+    uint32_t cnt_t[kWcBPT];
+    uint32_t csum = 0;
+#pragma unroll
+    for (int bb = 0; bb < kWcBPT; ++bb) {
+      const int d = threadIdx.x * kWcBPT + bb;
+      uint32_t r = 0;
+      if (d < kBins)
+        for (int q = 0; q < kWcWaves; ++q) {
+          const uint32_t c = wcnt[q][d];
+          wcnt[q][d] = (uint16_t)r;
+          r += c;
+        }
+      cnt_t[bb] = r;
+      csum += r;
+    }
+    {  // block exclusive scan of the tile counts over digits → tstart
+      uint32_t inc = csum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+      }
+      if (lane == 63) lw[w] = inc;
+      lds_barrier();
+      uint32_t r = inc - csum;
+      for (int q = 0; q < w; ++q) r += lw[q];
+#pragma unroll
+      for (int bb = 0; bb < kWcBPT; ++bb) {
+        if (threadIdx.x * kWcBPT + bb < kBins) tstart[threadIdx.x * kWcBPT + bb] = r;
+        r += cnt_t[bb];
+      }
+      if (threadIdx.x == kWcBlock - 1) tstart[kBins] = r;
+    }
+    lds_barrier();
+    SM_STAMP(3);
+
+    // local sorted positions; the first exchange carries the key, so each sorted slot learns its digit,
+    // its destination and whether its segment completes in this tile
+#pragma unroll
+    for (int k = 0; k < kWcItems; ++k) {
+      const int e = w * 64 * kWcItems + k * 64 + lane;
+      if (e < tile_n) {
+        const uint32_t key = MODE <= 1 ? (uint32_t)a[k] : (uint32_t)(a[k] >> 32);
+        const uint32_t d = ((key & kKeyMask) >> shift) & (kBins - 1);
+        lp[k] += tstart[d] + wcnt[w][d];
+        xb64[lp[k]] = a[k];
+      }
+    }
+    if constexpr (MODE == 2)
+      if (!last) load_tile(base + kTile);  // a[] is in LDS: the next tile's loads overlap this tile's stores
+    lds_barrier();
+    uint32_t dest[kWcItems], lim[kWcItems], ncs[kWcItems], dg[kWcItems];
+    uint64_t sa[kWcItems];
+#pragma unroll
+    for (int r = 0; r < kWcItems; ++r) {
+      const int s = r * kWcBlock + threadIdx.x;
+      if (s < tile_n) {
+        const uint64_t x = xb64[s];
+        const uint32_t key = MODE <= 1 ? (uint32_t)x : (uint32_t)(x >> 32);
+        const uint32_t d = ((key & kKeyMask) >> shift) & (kBins - 1);
+        const uint32_t ts_ = tstart[d], rn = run[d];
+        dest[r] = rn + (uint32_t)s - ts_;
+        const uint32_t l = last ? 0xffffffffu : ((rn + tstart[d + 1] - ts_) & ~(uint32_t)(S - 1));
+        lim[r] = l;
+        const uint32_t c0 = cst[d];
+        ncs[r] = c0 > l ? c0 : l;
+        dg[r] = d;
+        sa[r] = x;
+      }
+    }
+    // carried elements of each digit whose segment completes now (or the chunk ends) leave first; the slots they
+    // free are refilled only after the next barrier
+    auto flush_old = [&]() {
+#pragma unroll
+      for (int bb = 0; bb < kWcBPT; ++bb) {
+        const int d = threadIdx.x * kWcBPT + bb;
+        if (d < kBins) {
+          const uint32_t c0 = cst[d], rn = run[d];
+          const uint32_t l = (rn + cnt_t[bb]) & ~(uint32_t)(S - 1);
+          if (rn != c0 && (last || l > c0)) {
+            for (uint32_t q = 0; q < rn - c0; ++q) {
+              const uint64_t* cw = &carry[((uint32_t)d * (S - 1) + q) * CW];
+              if constexpr (MODE <= 1) drec[c0 + q] = make_uint4((uint32_t)cw[0], (uint32_t)(cw[0] >> 32),
+                                                                 (uint32_t)cw[1], (uint32_t)(cw[1] >> 32));
+              else dpairs[c0 + q] = cw[0];
+            }
+          }
+        }
+      }
+    };
+    SM_STAMP(4);
+    if constexpr (MODE <= 1) {  // second half, then one 16-byte store (or carry) per record
+      lds_barrier();
+#pragma unroll
+      for (int k = 0; k < kWcItems; ++k) {
+        const int e = w * 64 * kWcItems + k * 64 + lane;
+        if (e < tile_n) xb64[lp[k]] = b[k];
+      }
+      if (!last) load_tile(base + kTile);
+      flush_old();
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < kWcItems; ++r) {
+        const int s = r * kWcBlock + threadIdx.x;
+        if (s < tile_n) {
+          const uint64_t y = xb64[s];
+          if (dest[r] < lim[r]) {
+            drec[dest[r]] = make_uint4((uint32_t)sa[r], (uint32_t)(sa[r] >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+          } else {
+            uint64_t* cw = &carry[(dg[r] * (S - 1) + (dest[r] - ncs[r])) * CW];
+            cw[0] = sa[r];
+            cw[1] = y;
+          }
+        }
+      }
+    } else {
+      flush_old();
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < kWcItems; ++r) {
+        const int s = r * kWcBlock + threadIdx.x;
+        if (s < tile_n) {
+          if (dest[r] < lim[r]) dpairs[dest[r]] = sa[r];
+          else carry[dg[r] * (S - 1) + (dest[r] - ncs[r])] = sa[r];
+        }
+      }
+    }
+    SM_STAMP(5);
+    lds_barrier();  // every destination computed from run[] / cst[] before they advance
+#pragma unroll
+    for (int bb = 0; bb < kWcBPT; ++bb) {
+      const int d = threadIdx.x * kWcBPT + bb;
+      if (d < kBins) {
+        const uint32_t rn = run[d] + cnt_t[bb];
+        const uint32_t l = rn & ~(uint32_t)(S - 1);
+        run[d] = rn;
+        if (l > cst[d]) cst[d] = l;
+      }
+    }
+    SM_STAMP(6);
+  }
+  SM_STAMP_FLUSH;
+}
+
 // ---------------------------------------------------------------- walk
 
 struct WalkArgs {
@@ -802,7 +1138,11 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
 #pragma unroll
     for (int q = 0; q < kPre; ++q) {
       const int64_t p = b + q * kWalkBlock + threadIdx.x;
-      if (q * kWalkBlock + threadIdx.x < kWalkLds && p < n) pre[q] = a.rec[p];
+      if (q * kWalkBlock + threadIdx.x < kWalkLds && p < n) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)a.rec + p);
+        pre[q] = make_uint4(v.x, v.y, v.z, v.w);
+      }
     }
   };
   if constexpr (KEYED) prefetch(lo);
@@ -1028,14 +1368,44 @@ void launch_walk(int spec, int G, hipStream_t s, const WalkArgs& wa, int64_t per
 #undef SM_WALK
 }
 
+// record passes with the write-combining down-sweep (SM_SORT_WC=0 selects the plain one, for comparison)
+bool sort_wc() {
+  static const bool on = [] {
+    const char* e = getenv("SM_SORT_WC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// c1 reads only the compared attribute (slot-0 variables / stream columns of vattr): evaluated in pass 0
+bool c1_inline(const FastHostInfo& hi, const FastArgs& a) {
+  if (!hi.c1_host || hi.c1_len != a.c1_len) return false;
+  if (hi.c1_len != 0) {  // the device side evaluates `x CMP y` (make_cond's simple form) only
+    const Instr* c = hi.c1_host;
+    auto leaf = [](const Instr& in) { return in.op != OP_CMP && in.op != OP_MATH && in.op != OP_NOT; };
+    if (hi.c1_len != 3 || c[2].op != OP_CMP || !leaf(c[0]) || !leaf(c[1])) return false;
+  }
+  for (int k = 0; k < hi.c1_len; ++k) {
+    const Instr& in = hi.c1_host[k];
+    if (in.op == OP_TS) return false;
+    if (in.op == OP_VAR && (in.a != 0 || in.c != hi.vattr)) return false;
+    if (in.op == OP_COL && in.a != hi.vattr) return false;
+  }
+  return true;
+}
+
 template <typename KT, typename VT>
 void launch_down0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int vmode, int64_t vmin,
                     const uint64_t* c1mask, int64_t ts0, int G, int64_t per, hipStream_t s, uint4* dst,
                     const uint32_t* cnt, const uint32_t* dbase) {
   OrigSrc<KT, VT> os{a.st, (const KT*)kcol, (const VT*)hi.cols[hi.vattr], kmin, vmode, vmin, c1mask, a.ts, ts0,
-                     a.ordinals, a.ordinal_base};
-  hipLaunchKernelGGL((downsweep_kernel<0, OrigSrc<KT, VT>>), dim3(G), dim3(kBlock), 0, s, os, dst, nullptr, a.n, per,
-                     nullptr, G, 0, cnt, dbase);
+                     a.ordinals, a.ordinal_base, a.code + a.c1_off, a.c1_len, a.consts, c1_inline(hi, a)};
+  if (sort_wc())
+    hipLaunchKernelGGL((downsweep_wc_kernel<0, OrigSrc<KT, VT>>), dim3(G), dim3(kWcBlock), 0, s, os, dst, nullptr, a.n,
+                       per, nullptr, G, 0, cnt, dbase);
+  else
+    hipLaunchKernelGGL((downsweep_kernel<0, OrigSrc<KT, VT>>), dim3(G), dim3(kBlock), 0, s, os, dst, nullptr, a.n, per,
+                       nullptr, G, 0, cnt, dbase);
 }
 
 template <typename KT>
@@ -1096,7 +1466,8 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   }
   if (fs.sort_wgs_per_cu == 0) {
     int b = 0;
-    SM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, downsweep_kernel<1, RecSrc>, kBlock, 0));
+    if (sort_wc()) SM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, downsweep_wc_kernel<1, RecSrc>, kWcBlock, 0));
+    else SM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, downsweep_kernel<1, RecSrc>, kBlock, 0));
     fs.sort_wgs_per_cu = std::max(1, b);
     b = 0;
     SM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, walk_kernel<true, CMP_GT, true>, kWalkBlock, 0));
@@ -1122,14 +1493,18 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   };
 
   // column facts + c1 mask + pass-0 digit counts, one pass
-  if (hi.key_type == T_LONG && keyed)
-    hipLaunchKernelGGL((prep_kernel<int64_t>), dim3(G), dim3(kBlock), 0, s, (const int64_t*)kcol, vlong, a.ts,
-                       a.ordinals, a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt,
-                       c);
-  else
-    hipLaunchKernelGGL((prep_kernel<int32_t>), dim3(G), dim3(kBlock), 0, s, (const int32_t*)kcol, vlong, a.ts,
-                       a.ordinals, a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt,
-                       c);
+  const bool mask = !keyed || !c1_inline(hi, a);
+#define SM_PREP(KT, M)                                                                                              \
+  hipLaunchKernelGGL((prep_kernel<KT, M>), dim3(G), dim3(kBlock), 0, s, (const KT*)kcol, vlong, a.ts, a.ordinals,    \
+                     a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt, c)
+  if (hi.key_type == T_LONG && keyed) {
+    if (mask) SM_PREP(int64_t, true);
+    else SM_PREP(int64_t, false);
+  } else {
+    if (mask) SM_PREP(int32_t, true);
+    else SM_PREP(int32_t, false);
+  }
+#undef SM_PREP
   tmark("prep");
   Ctrl hc;
   SM_HIP(hipMemcpyAsync(&hc, c, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
@@ -1206,8 +1581,12 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
                          p * kRB, cnt);
       tmark("key_up");
       scan_counts(G);
-      hipLaunchKernelGGL((downsweep_kernel<1, RecSrc>), dim3(G), dim3(kBlock), 0, s, RecSrc{cur}, nxt, nullptr, n, per,
-                         nullptr, G, p * kRB, cnt, dbase);
+      if (sort_wc())
+        hipLaunchKernelGGL((downsweep_wc_kernel<1, RecSrc>), dim3(G), dim3(kWcBlock), 0, s, RecSrc{cur}, nxt, nullptr, n,
+                           per, nullptr, G, p * kRB, cnt, dbase);
+      else
+        hipLaunchKernelGGL((downsweep_kernel<1, RecSrc>), dim3(G), dim3(kBlock), 0, s, RecSrc{cur}, nxt, nullptr, n,
+                           per, nullptr, G, p * kRB, cnt, dbase);
       tmark("key_pass");
       std::swap(cur, nxt);
     }

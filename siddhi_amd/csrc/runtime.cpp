@@ -955,6 +955,8 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
       hi.vattr = fast_vattr(cq, types);
       hi.c2_host = (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.fast_c2_off;
       hi.c2_len = cq.fast_c2_len;
+      hi.c1_host = (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.fast_c1_off;
+      hi.c1_len = cq.fast_c1_len;
       if (hi.vattr >= 0) hi.vtype = types[hi.vattr];
       if (fa.key) {
         const CompiledPartition& cp = *q.part;

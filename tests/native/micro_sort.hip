@@ -112,6 +112,45 @@ int main(int argc, char** argv) {
       report_stamps("record");
     }
   }
+  // write-combining record passes
+  {
+    int wwc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&wwc, downsweep_wc_kernel<1, RecSrc>, kWcBlock, 0));
+    const int Gc = (int)std::min<int64_t>((n + kTile - 1) / kTile, 2LL * wwc * cus);
+    const int64_t perc = round_up((n + Gc - 1) / Gc, kTile);
+    printf("wc: wgs/cu=%d G=%d per=%lld\n", wwc, Gc, (long long)perc);
+    for (int shift = 0; shift < kbits; shift += kRB) {
+      for (int rep = 0; rep < 3; ++rep) {
+        hipLaunchKernelGGL((upsweep_kernel<RecDigits>), dim3(Gc), dim3(kBlock), 0, 0, RecDigits{A}, n, perc, Gc, shift,
+                           cnt);
+        hipLaunchKernelGGL(scan_chunks_kernel, dim3(kBins), dim3(256), 0, 0, cnt, Gc, dbase);
+        hipLaunchKernelGGL(digit_base_kernel, dim3(1), dim3(kBlock), 0, 0, dbase);
+        CK(hipEventRecord(e2));
+        hipLaunchKernelGGL((downsweep_wc_kernel<1, RecSrc>), dim3(Gc), dim3(kWcBlock), 0, 0, RecSrc{A}, B, nullptr, n,
+                           perc, nullptr, Gc, shift, cnt, dbase);
+        CK(hipEventRecord(e3));
+        CK(hipDeviceSynchronize());
+        float dn = 0;
+        CK(hipEventElapsedTime(&dn, e2, e3));
+        printf("wc record pass shift %d: down %.3f ms (%.0f GB/s)\n", shift, dn, n * 32 / (dn * 1e-3) / 1e9);
+        report_stamps("wc record");
+      }
+      if (shift == 0) {  // check: B is A stably ordered by the digit
+        std::vector<uint4> ha(n), hb(n);
+        CK(hipMemcpy(ha.data(), A, n * 16, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hb.data(), B, n * 16, hipMemcpyDeviceToHost));
+        std::vector<int64_t> pos(kBins + 1, 0);
+        for (int64_t i = 0; i < n; ++i) pos[((ha[i].x & kKeyMask) & (kBins - 1)) + 1]++;
+        for (int d = 0; d < kBins; ++d) pos[d + 1] += pos[d];
+        int64_t bad = 0;
+        for (int64_t i = 0; i < n; ++i) {
+          const uint4 r = ha[i], q = hb[pos[(r.x & kKeyMask) & (kBins - 1)]++];
+          bad += q.x != r.x || q.y != r.y || q.z != r.z || q.w != r.w;
+        }
+        printf("wc record pass check: %lld mismatches\n", (long long)bad);
+      }
+    }
+  }
   // pairs pass
   uint64_t *P, *Q;
   CK(hipMalloc(&P, n * 8));
@@ -131,6 +170,35 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&dn, e2, e3));
     printf("pair pass: down %.3f ms (%.0f GB/s)\n", dn, n * 16 / (dn * 1e-3) / 1e9);
     report_stamps("pair");
+  }
+  {
+    int wwc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&wwc, downsweep_wc_kernel<2, PairSrc>, kWcBlock, 0));
+    const int Gc = (int)std::min<int64_t>((n + kTile - 1) / kTile, 2LL * wwc * cus);
+    const int64_t perc = round_up((n + Gc - 1) / Gc, kTile);
+    for (int rep = 0; rep < 3; ++rep) {
+      hipLaunchKernelGGL((upsweep_kernel<PairDigits>), dim3(Gc), dim3(kBlock), 0, 0, PairDigits{P}, n, perc, Gc, 0, cnt);
+      hipLaunchKernelGGL(scan_chunks_kernel, dim3(kBins), dim3(256), 0, 0, cnt, Gc, dbase);
+      hipLaunchKernelGGL(digit_base_kernel, dim3(1), dim3(kBlock), 0, 0, dbase);
+      CK(hipEventRecord(e2));
+      hipLaunchKernelGGL((downsweep_wc_kernel<2, PairSrc>), dim3(Gc), dim3(kWcBlock), 0, 0, PairSrc{P}, nullptr, Q, n,
+                         perc, nullptr, Gc, 0, cnt, dbase);
+      CK(hipEventRecord(e3));
+      CK(hipDeviceSynchronize());
+      float dn = 0;
+      CK(hipEventElapsedTime(&dn, e2, e3));
+      printf("wc pair pass: down %.3f ms (%.0f GB/s)\n", dn, n * 16 / (dn * 1e-3) / 1e9);
+      report_stamps("wc pair");
+    }
+    std::vector<uint64_t> hp(n), hq(n);
+    CK(hipMemcpy(hp.data(), P, n * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hq.data(), Q, n * 8, hipMemcpyDeviceToHost));
+    std::vector<int64_t> pos(kBins + 1, 0);
+    for (int64_t i = 0; i < n; ++i) pos[((hp[i] >> 32) & (kBins - 1)) + 1]++;
+    for (int d = 0; d < kBins; ++d) pos[d + 1] += pos[d];
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) bad += hq[pos[(hp[i] >> 32) & (kBins - 1)]++] != hp[i];
+    printf("wc pair pass check: %lld mismatches\n", (long long)bad);
   }
   // walk over sorted records (keyed, c2 = e2 > e1 on exact codes)
   {
