@@ -12,6 +12,12 @@ then the closed-form pattern kernels producing the ordered (e1, e2) match tuples
 
 Scaling is strong (N is the whole job at every GPU count). Launch: python bench.py [--gpus N --steps K
 --warmup W]; for N > 1 the driver uses torch.distributed.run (one rank per GPU).
+
+The other §8(d) configurations are parity/measurement side lines, selected with --config:
+  --config 2   filter-only `StockStream[price > 70 and volume < 1000]`, N = 1e9 (bandwidth roofline);
+               multi-GPU: contiguous index ranges per rank, no exchange (strong scaling)
+  --config 3   non-partitioned `every e1 -> e2 within 1 sec`, N = 1e8, ts_i = i ms; does not shard:
+               --gpus N runs N independent replicas (weak scaling, replicas only)
 """
 import argparse
 import ctypes
@@ -24,13 +30,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-APP = ("define stream StockStream (symbol int, price double, volume long, timestamp long); "
-       "partition with (symbol of StockStream) begin "
+SCHEMA = "define stream StockStream (symbol int, price double, volume long, timestamp long); "
+APP = (SCHEMA + "partition with (symbol of StockStream) begin "
        "@info(name='q') from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
        "select e1.timestamp as i, e2.timestamp as j insert into OutputStream; end;")
-SEED = 0x5EED0000 + 4
+APP2 = SCHEMA + "@info(name='q') from StockStream[price > 70 and volume < 1000] select timestamp insert into Out;"
+APP3 = (SCHEMA + "@info(name='q') from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] "
+        "within 1 sec select e1.timestamp as i, e2.timestamp as j insert into OutputStream;")
 HBM_PEAK = 8.0e12
 GAMMA = 0x9E3779B97F4A7C15
+METRIC = "input events/sec + % HBM peak, partitioned pattern query, 1/2/4/8 MI355X"
+
+
+def seed_for(config):
+    return 0x5EED0000 + config
 
 
 def _i64(x):
@@ -40,18 +53,17 @@ def _i64(x):
 
 def splitmix_torch(v):
     """splitmix64 finaliser of (v + gamma) on int64 tensors (wrap-around arithmetic, logical shifts)."""
-    import torch
     z = v + _i64(GAMMA)
     z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * _i64(0xBF58476D1CE4E5B9)
     z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * _i64(0x94D049BB133111EB)
     return z ^ ((z >> 31) & ((1 << 33) - 1))
 
 
-def gen_stock(lo, hi, K, ts_div, device):
+def gen_stock(lo, hi, K, ts_div, device, seed):
     """Events [lo, hi) of the synthetic stream: h(i,f) = splitmix64(seed + 4i + f)."""
     import torch
     i = torch.arange(lo, hi, dtype=torch.int64, device=device)
-    base = SEED + 4 * i
+    base = seed + 4 * i
     h0 = splitmix_torch(base)
     symbol = (((h0 >> 32) & 0xFFFFFFFF) % K).to(torch.int32)
     del h0
@@ -65,13 +77,13 @@ def gen_stock(lo, hi, K, ts_div, device):
     return symbol, price, volume, i, ts
 
 
-def gen_stock_numpy(lo, hi, K, ts_div):
+def gen_stock_numpy(lo, hi, K, ts_div, seed):
     import numpy as np
     with np.errstate(over="ignore"):
         i = np.arange(lo, hi, dtype=np.uint64)
         out = []
         for f in range(3):
-            z = np.uint64(SEED) + np.uint64(4) * i + np.uint64(f) + np.uint64(GAMMA)
+            z = np.uint64(seed) + np.uint64(4) * i + np.uint64(f) + np.uint64(GAMMA)
             z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
             z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
             out.append(z ^ (z >> np.uint64(31)))
@@ -82,12 +94,12 @@ def gen_stock_numpy(lo, hi, K, ts_div):
     return symbol, price, volume, idx, idx // ts_div
 
 
-def cpu_baseline(sample, K, ts_div):
+def cpu_baseline(sample, K, ts_div, app_text, seed, out_stream):
     """The CPU oracle (literal restatement of the reference engine, 1 thread) on the first `sample` events."""
     from oracle_lib import OracleApp, lib
     import numpy as np
-    sym, price, vol, ts_attr, ts = gen_stock_numpy(0, sample, K, ts_div)
-    app = OracleApp(APP)
+    sym, price, vol, ts_attr, ts = gen_stock_numpy(0, sample, K, ts_div, seed)
+    app = OracleApp(app_text)
     app.set_collect(False)
     cols = [np.ascontiguousarray(c) for c in (sym, price, vol, ts_attr)]
     ptrs = (ctypes.c_void_p * 4)(*[c.ctypes.data for c in cols])
@@ -97,7 +109,7 @@ def cpu_baseline(sample, K, ts_div):
     dt = time.perf_counter() - t0
     if rc != 0:
         raise RuntimeError(err.value.decode())
-    m = app.output_count("OutputStream")
+    m = app.output_count(out_stream)
     app.close()
     return sample / dt, dt, m
 
@@ -106,17 +118,35 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+# Per configuration: app, default N, event-time divisor, whether the path shards, whole-job algorithmic bytes
+#  and the kernels of its device pipeline.
+CONFIGS = {
+    2: dict(app=APP2, events=1e9, ts_div=1, out="Out", shards=True, scaling="strong",
+            workload="config 2: StockStream[price > 70 and volume < 1000] select timestamp (filter roofline)",
+            job_bytes=lambda n, m: 16 * n + 4 * m, cpu_sample=20_000_000),
+    3: dict(app=APP3, events=1e8, ts_div=1, out="OutputStream", shards=False, scaling="weak",
+            workload="config 3: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
+                     "(non-partitioned; replicas only)",
+            job_bytes=lambda n, m: 16 * n + 8 * m, cpu_sample=4_000_000),
+    4: dict(app=APP, events=1e9, ts_div=10_000, out="OutputStream", shards=True, scaling="strong",
+            workload="config 4: partition with (symbol of StockStream) every e1 -> e2 within 1 sec",
+            job_bytes=lambda n, m: 20 * n + 8 * m, cpu_sample=4_000_000),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--events", type=float, default=1e9)
+    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS))
+    ap.add_argument("--events", type=float, default=None)
     ap.add_argument("--keys", type=int, default=1_000_000)
-    ap.add_argument("--ts-div", type=int, default=10_000)
-    ap.add_argument("--cpu-sample", type=int, default=4_000_000)
+    ap.add_argument("--ts-div", type=int, default=None)
+    ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
 
     import torch
     import torch.distributed as dist
@@ -130,31 +160,41 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    N = int(args.events)
+    N = int(args.events if args.events is not None else cfg["events"])
     K = args.keys
-    lo, hi = N * rank // world, N * (rank + 1) // world
-    symbol, price, volume, tsattr, ts = gen_stock(lo, hi, K, args.ts_div, dev)
-    del volume, tsattr  # not referenced by the query: the exchange ships only what the plan reads
-    ordinals = torch.arange(lo, hi, dtype=torch.int64, device=dev)
+    ts_div = args.ts_div if args.ts_div is not None else cfg["ts_div"]
+    seed = seed_for(args.config)
+    if cfg["shards"]:
+        lo, hi = N * rank // world, N * (rank + 1) // world
+    else:  # replicas: every rank runs the whole workload
+        lo, hi = 0, N
+    symbol, price, volume, tsattr, ts = gen_stock(lo, hi, K, ts_div, dev, seed)
+    if args.config != 2:
+        del volume  # not referenced by the pattern: the exchange ships only what the plan reads
+        volume = price
+    ordinals = torch.arange(lo, hi, dtype=torch.int64, device=dev) if args.config == 4 else None
     torch.cuda.synchronize()
 
-    app = ProductApp(APP)
+    app = ProductApp(cfg["app"])
     stream = torch.cuda.current_stream(dev)
     hip_stream = ctypes.c_void_p(stream.cuda_stream)
     n_local = [hi - lo]
 
     def step():
-        if world > 1:
+        if args.config == 4 and world > 1:
             (s_sym, s_price, s_ts, s_ord), _ = exchange_by_key(symbol, [symbol, price, ts, ordinals], world)
+        elif args.config == 4:
+            s_sym, s_price, s_ts, s_ord = symbol, price, ts, None
         else:
             s_sym, s_price, s_ts, s_ord = symbol, price, ts, None
         n_local[0] = s_ts.numel()
-        # columns: symbol, price, volume, timestamp (volume/timestamp are not read by the plan)
-        app.process_device_batch("StockStream", s_ts, [s_sym, s_price, s_price, s_price], ordinals=s_ord,
-                                 ordinal_base=0, hip_stream=hip_stream)
+        # columns: symbol, price, volume, timestamp (attributes the plan does not read are aliased)
+        cols = [s_sym, s_price, volume if args.config == 2 else s_price, tsattr if args.config == 2 else s_price]
+        app.process_device_batch("StockStream", s_ts, cols, ordinals=s_ord, ordinal_base=lo if args.config == 2 else 0,
+                                 hip_stream=hip_stream)
         return app.device_matches("q")[1]
 
-    log(f"rank {rank}: {hi - lo} events resident; warmup {args.warmup}")
+    log(f"rank {rank}: config {args.config}, {hi - lo} events resident; warmup {args.warmup}")
     for _ in range(args.warmup):
         step()
     # per-launch HIP events inside the library, on the launch stream (a few event records per step)
@@ -179,60 +219,79 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    path = app.get_stat("fast_path:q")
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     m = torch.tensor([nm], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(m)
+        if cfg["shards"]:
+            dist.all_reduce(m)
     dt = t.item()
     total_matches = m.item()
     ms_per_step = dt / args.steps * 1e3
-    value = N / (dt / args.steps)
+    units = N if cfg["shards"] else N * world  # replicas: every rank processed the whole stream
+    value = units / (dt / args.steps)
 
-    roof = roofline(ktot, n_local[0], nm, args.steps)
+    roof = roofline(ktot, n_local[0], nm, args.steps, args.config)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        log(f"cpu baseline on {args.cpu_sample} events")
-        v, sec, mm = cpu_baseline(args.cpu_sample, K, args.ts_div)
+        sample = args.cpu_sample or cfg["cpu_sample"]
+        log(f"cpu baseline on {sample} events")
+        v, sec, mm = cpu_baseline(sample, K, ts_div, cfg["app"], seed, cfg["out"])
         cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port",
-               "sample": f"first {args.cpu_sample} events of the same stream through oracle/cpu_ref "
+               "sample": f"first {sample} events of the same stream through oracle/cpu_ref "
                          f"(C++ restatement of the reference engine, 1 thread): {sec:.2f} s, {mm} matches"}
     if rank == 0:
-        alg_bytes = 20 * N + 8 * total_matches
+        alg = cfg["job_bytes"](N, total_matches) * (1 if cfg["shards"] else world)
+        conf = {"workload": cfg["workload"], "config": args.config, "events": N,
+                "event_time": f"floor(i/{ts_div}) ms", "matches": total_matches,
+                "parallelism": (f"key-sharded x{world}" if args.config == 4 else
+                                f"index-range-sharded x{world}" if cfg["shards"] else f"replicas x{world}"),
+                "device_path": {1: "general closed form", 2: "onesweep closed form", 3: "filter interpreter",
+                                4: "filter typed conjunction"}.get(int(path), str(path)),
+                "step_hbm_fraction": alg / (ms_per_step * 1e-3) / HBM_PEAK}
+        if args.config == 4:
+            conf["keys"] = K
         line = {
-            "metric": "input events/sec + % HBM peak, partitioned pattern query, 1/2/4/8 MI355X",
+            "metric": METRIC if args.config == 4 else f"input events/sec + % HBM peak, {cfg['workload']}",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": cfg["scaling"], "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (counter-based splitmix64 StockStream, device-resident)",
-            "config": {"workload": "config 4: partition with (symbol of StockStream) every e1 -> e2 within 1 sec",
-                       "events": N, "keys": K, "event_time": f"floor(i/{args.ts_div}) ms",
-                       "matches": total_matches, "parallelism": f"key-sharded x{world}",
-                       "step_hbm_fraction": alg_bytes / (ms_per_step * 1e-3) / HBM_PEAK},
-            "roofline": roof, "cpu_baseline": cpu,
+            "config": conf, "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-# Kernels of the device pipeline (labels recorded by kernels/fastpath3.hip) and their ALGORITHMIC bytes per
-# launch for a batch of n events with m matches: what each launch must read and write at minimum.
-KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last"]
+# Kernels of the device pipelines (labels recorded by kernels/fastpath3.hip and kernels/filter.hip) and their
+# ALGORITHMIC bytes per launch for a batch of n events with m matches: what each launch must read
+# and write at minimum.
+KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last",
+           "filter_count", "filter_scan", "filter_write"]
 
 
-def alg_bytes(label, n, m):
-    return {"prep": 20 * n + n // 8,        # key i32 + ts i64 + price f64 (c1 = price > 20) in, c1 bit out
+def alg_bytes(label, n, m, config):
+    keyed = config == 4
+    return {"prep": (12 * n) if keyed else (16 * n + n // 8),  # keyed: key i32 + ts i64 (c1 = price > 20 is
+                                                              # evaluated in pass 0); unkeyed: ts + price in,
+                                                              # c1 bit out
             "key_up": 16 * n,               # pass-1 digits: one 16-B record per event (the key word of each)
             "scan": 0,                      # per-chunk digit counts (O(chunks x 1024), not per event)
             "key_pass0": 20 * n + 16 * n,   # key i32 + price f64 + ts i64 in, 16-B keyed record out
             "key_pass": 16 * n + 16 * n,    # 16-B record in and out
-            "walk": 16 * n + 8 * m,         # records in, (j, i) u32 pairs out
+            "walk": (16 * n + 8 * m) if keyed else (16 * n + n // 8 + 8 * m),  # records (unkeyed: price + ts +
+                                                                               # c1 bits) in, (j, i) pairs out
             "j_up": 4 * m,
             "j_pass": 16 * m,               # (j, i) in and out
-            "j_pass_last": 16 * m}[label]
+            "j_pass_last": 16 * m,
+            "filter_count": 16 * n + n // 8,  # price f64 + volume i64 in, one mask bit per event out
+            "filter_scan": 0,
+            "filter_write": n // 8 + 4 * m,   # mask in, u32 row per kept event out
+            }[label]
 
 
-def roofline(ktot, n, m, steps):
+def roofline(ktot, n, m, steps, config):
     """Dominant kernel (largest total time over the timed steps): algorithmic bytes per launch / average launch
     duration, against HBM peak. Also the per-kernel breakdown."""
     if not ktot:
@@ -240,10 +299,10 @@ def roofline(ktot, n, m, steps):
     dom = max(ktot, key=lambda k: ktot[k][0])
     tot_ms, calls = ktot[dom]
     avg_ms = tot_ms / calls
-    per_launch = alg_bytes(dom, n, m)
+    per_launch = alg_bytes(dom, n, m, config)
     ach = per_launch / (avg_ms * 1e-3)
     brk = {k: {"avg_ms": v[0] / v[1], "calls_per_step": v[1] / steps,
-               "gbps": alg_bytes(k, n, m) / (v[0] / v[1] * 1e-3) / 1e9} for k, v in ktot.items()}
+               "gbps": alg_bytes(k, n, m, config) / (v[0] / v[1] * 1e-3) / 1e9} for k, v in ktot.items()}
     return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
             "traffic": None, "kernel": dom, "avg_launch_ms": avg_ms, "alg_bytes_per_launch": per_launch,
             "breakdown": brk}

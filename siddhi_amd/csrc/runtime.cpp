@@ -24,6 +24,7 @@
 #include "../../include/siddhi_amd.h"
 #include "compiler.h"
 #include "kernels/fastpath.h"
+#include "kernels/filter.h"
 #include "kernels/nfa.h"
 #include "kernels/primitives.h"
 #include "kernels/stream_ops.h"
@@ -907,7 +908,13 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
     }
     a->d_streams.ensure(sizeof(NfaStream));
     SM_HIP(hipMemcpyAsync(a->d_streams.p, &d, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
-    ensure_scratch(a, n * 64 + (64 << 20));
+    size_t need = 64 << 20;  // filter queries: mask words + block counts; patterns: records, pairs, counts
+    for (auto& qp : a->queries) {
+      const CompiledQuery& cq = qp->cq;
+      if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
+      need = std::max(need, cq.hdr.kind == 0 ? n / 8 + n / 1024 + (64 << 20) : n * 64 + (64 << 20));
+    }
+    ensure_scratch(a, need);
     for (auto& qp : a->queries) {
       QueryRt& q = *qp;
       const CompiledQuery& cq = q.cq;
@@ -915,14 +922,15 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
       a->sc.used = 0;
       const char* blob = (const char*)q.blob.p;
       if (cq.hdr.kind == 0) {
-        int64_t* rows = (int64_t*)a->sc.take(n * 8);
-        int64_t nm = filter_rows((const NfaStream*)a->d_streams.p, (int64_t)n,
-                                 (const Instr*)(blob + cq.hdr.off_code) + cq.hdr.filt_off, cq.hdr.filt_len,
-                                 (const DVal*)(blob + cq.hdr.off_const), rows, a->sc, hs);
-        q.dev_pairs.ensure(std::max<size_t>(nm * 8, 16));
-        q.dev_n = nm;
-        // rows stay as int64 row indices (ordinal = base + row)
-        SM_HIP(hipMemcpyAsync(q.dev_pairs.p, rows, nm * 8, hipMemcpyDeviceToDevice, hs));
+        q.dev_pairs.ensure(std::max<size_t>(n * 4, 16));
+        bool typed = false;
+        q.dev_n = filter_device(d, (const NfaStream*)a->d_streams.p, (int64_t)n,
+                                (const Instr*)(blob + cq.hdr.off_code) + cq.hdr.filt_off,
+                                (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.hdr.filt_off, cq.hdr.filt_len,
+                                (const DVal*)(blob + cq.hdr.off_const), (const DVal*)(cq.blob.data() + cq.hdr.off_const),
+                                d_ordinals, ordinal_base, (uint32_t*)q.dev_pairs.p, a->sc, hs,
+                                a->fast_timing ? &a->fast_tm : nullptr, &typed);
+        q.fast_path_used = typed ? 4 : 3;
         continue;
       }
       if (!cq.fast_every_within)

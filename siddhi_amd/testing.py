@@ -126,6 +126,15 @@ class ProductApp:
             _hip_memcpy_d2h(out.ctypes.data, p, n * 8)
         return out
 
+    def device_rows_host(self, query):
+        """Kept rows of the last device batch for a filter query: numpy uint32 array (ordinal - base)."""
+        import numpy as np
+        p, n = self.device_matches(query)
+        out = np.empty(n, dtype=np.uint32)
+        if n:
+            _hip_memcpy_d2h(out.ctypes.data, p, n * 4)
+        return out
+
 
 _hip = None
 
