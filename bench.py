@@ -18,6 +18,11 @@ The other §8(d) configurations are parity/measurement side lines, selected with
                multi-GPU: contiguous index ranges per rank, no exchange (strong scaling)
   --config 3   non-partitioned `every e1 -> e2 within 1 sec`, N = 1e8, ts_i = i ms; does not shard:
                --gpus N runs N independent replicas (weak scaling, replicas only)
+  --config 5   `@app:playback`, five streams A..E, partition with (symbol of A..E),
+               `every e1=A, e2=B[price>e1.price]<2:5>, (e3=C or e4=D), not E for 5 sec`, K = 1e6, N = 1e8,
+               ts_i = floor(i / 100) ms (about one event per key every 10 s, so `not E for 5 sec` timers fire);
+               general NFA kernel over an interleaved device batch; multi-GPU: key exchange + the global
+               clock-advance points as heartbeats on every rank (strong scaling)
 """
 import argparse
 import ctypes
@@ -37,6 +42,13 @@ APP = (SCHEMA + "partition with (symbol of StockStream) begin "
 APP2 = SCHEMA + "@info(name='q') from StockStream[price > 70 and volume < 1000] select timestamp insert into Out;"
 APP3 = (SCHEMA + "@info(name='q') from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] "
         "within 1 sec select e1.timestamp as i, e2.timestamp as j insert into OutputStream;")
+STREAMS5 = "ABCDE"
+APP5 = ("@app:playback " + " ".join(f"define stream {x} (symbol int, price double, volume long, timestamp long);"
+                                    for x in STREAMS5) +
+        " partition with (symbol of A, symbol of B, symbol of C, symbol of D, symbol of E) begin "
+        "@info(name='q') from every e1=A, e2=B[price>e1.price]<2:5>, (e3=C or e4=D), not E for 5 sec "
+        "select e1.timestamp as a, e2[0].timestamp as b0, e2[last].timestamp as bl, e3.timestamp as c, "
+        "e4.timestamp as d insert into Out; end;")
 HBM_PEAK = 8.0e12
 GAMMA = 0x9E3779B97F4A7C15
 METRIC = "input events/sec + % HBM peak, partitioned pattern query, 1/2/4/8 MI355X"
@@ -77,6 +89,56 @@ def gen_stock(lo, hi, K, ts_div, device, seed):
     return symbol, price, volume, i, ts
 
 
+def gen_stream_idx(lo, hi, device, seed):
+    """Config 5 stream of each event: h(i, 3) % 5 (A..E)."""
+    import torch
+    i = torch.arange(lo, hi, dtype=torch.int64, device=device)
+    h3 = splitmix_torch(seed + 4 * i + 3)
+    return (((h3 >> 32) & 0xFFFFFFFF) % 5).to(torch.int32)
+
+
+def clock_ticks(ts, lo, world):
+    """Multi-GPU config 5: the playback clock is global (every event advances it, StreamJunction.sendData
+    :232-237) but a rank only receives its keys' events. Each rank finds the clock-advance points of its own
+    contiguous slice (first event of each new event time), all ranks all-gather them, and every rank replays
+    them as heartbeats so that its timers fire at exactly the reference's clock values."""
+    import torch
+    import torch.distributed as dist
+    first = torch.ones_like(ts, dtype=torch.bool)
+    first[1:] = ts[1:] > ts[:-1]
+    pos = torch.nonzero(first).flatten()
+    mine = torch.stack([pos + lo, ts[pos]], 1)  # (global ordinal, clock)
+    cnt = torch.tensor([mine.shape[0]], dtype=torch.int64, device=ts.device)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt)
+    mx = int(max(c.item() for c in cnts))
+    pad = torch.zeros((mx, 2), dtype=torch.int64, device=ts.device)
+    pad[:mine.shape[0]] = mine
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return torch.cat([p[:int(c.item())] for p, c in zip(parts, cnts)])
+
+
+def merge_ticks(sid, ts, cols, ords, ticks):
+    """Insert heartbeat records (stream -1) before the received events, ordered by global ordinal; a tick at
+    the ordinal of an event this rank already holds is dropped (that event advances the clock itself)."""
+    import torch
+    have = torch.zeros(0, dtype=torch.bool, device=ts.device)
+    tpos = ticks[:, 0]
+    idx = torch.searchsorted(ords, tpos)
+    hit = (idx < ords.numel()) & (ords[idx.clamp(max=max(ords.numel() - 1, 0))] == tpos) if ords.numel() else have
+    keep = ~hit if ords.numel() else torch.ones_like(tpos, dtype=torch.bool)
+    tpos, tclk = tpos[keep], ticks[keep, 1]
+    key = torch.cat([ords * 2 + 1, tpos * 2])  # heartbeat first at equal ordinal (it is replayed before it)
+    order = torch.argsort(key)
+    n_t = tpos.numel()
+    sid2 = torch.cat([sid, torch.full((n_t,), -1, dtype=torch.int32, device=ts.device)])[order]
+    ts2 = torch.cat([ts, tclk])[order]
+    cols2 = [torch.cat([c, torch.zeros(n_t, dtype=c.dtype, device=c.device)])[order] for c in cols]
+    ords2 = torch.cat([ords, torch.full((n_t,), -1, dtype=torch.int64, device=ts.device)])[order]
+    return sid2, ts2, cols2, ords2
+
+
 def gen_stock_numpy(lo, hi, K, ts_div, seed):
     import numpy as np
     with np.errstate(over="ignore"):
@@ -94,8 +156,23 @@ def gen_stock_numpy(lo, hi, K, ts_div, seed):
     return symbol, price, volume, idx, idx // ts_div
 
 
-def cpu_baseline(sample, K, ts_div, app_text, seed, out_stream):
+def cpu_baseline(sample, K, ts_div, app_text, seed, out_stream, config=4):
     """The CPU oracle (literal restatement of the reference engine, 1 thread) on the first `sample` events."""
+    if config == 5:
+        import numpy as np
+        import synth
+        from oracle_lib import OracleApp
+        sid, cols, ts = synth.gen5(0, sample, K, ts_div, seed)
+        app = OracleApp(app_text)
+        app.set_collect(False)
+        app.start()
+        t0 = time.perf_counter()
+        app.send_interleaved(sid, ts, cols)
+        app.flush()
+        dt = time.perf_counter() - t0
+        m = app.output_count(out_stream)
+        app.close()
+        return sample / dt, dt, m
     from oracle_lib import OracleApp, lib
     import numpy as np
     sym, price, vol, ts_attr, ts = gen_stock_numpy(0, sample, K, ts_div, seed)
@@ -131,6 +208,11 @@ CONFIGS = {
     4: dict(app=APP, events=1e9, ts_div=10_000, out="OutputStream", shards=True, scaling="strong",
             workload="config 4: partition with (symbol of StockStream) every e1 -> e2 within 1 sec",
             job_bytes=lambda n, m: 20 * n + 8 * m, cpu_sample=4_000_000),
+    5: dict(app=APP5, events=1e8, ts_div=100, out="Out", shards=True, scaling="strong",
+            workload="config 5: @app:playback partition with (symbol of A..E) every e1=A, e2=B[price>e1.price]<2:5>, "
+                     "(e3=C or e4=D), not E for 5 sec",
+            # key i32 + price f64 + event time i64 + stream id (1 B) in; 5 ordinals per output event out
+            job_bytes=lambda n, m: 21 * n + 40 * m, cpu_sample=40_000),
 }
 
 
@@ -172,7 +254,9 @@ def main():
     if args.config != 2:
         del volume  # not referenced by the pattern: the exchange ships only what the plan reads
         volume = price
-    ordinals = torch.arange(lo, hi, dtype=torch.int64, device=dev) if args.config == 4 else None
+    ordinals = torch.arange(lo, hi, dtype=torch.int64, device=dev) if args.config in (4, 5) else None
+    sidx = gen_stream_idx(lo, hi, dev, seed) if args.config == 5 else None
+    ticks = clock_ticks(ts, lo, world) if args.config == 5 and world > 1 else None
     torch.cuda.synchronize()
 
     app = ProductApp(cfg["app"])
@@ -181,6 +265,20 @@ def main():
     n_local = [hi - lo]
 
     def step():
+        if args.config == 5:
+            # a fresh runtime of the app per step (state dropped, device allocations kept), then the batch
+            app.set_option("reset", 1)
+            if world > 1:
+                (s_sym, s_price, s_ts, s_ord, s_sid), _ = exchange_by_key(symbol, [symbol, price, ts, ordinals, sidx],
+                                                                          world)
+                s_sid, s_ts, (s_sym, s_price), s_ord = merge_ticks(s_sid, s_ts, [s_sym, s_price], s_ord, ticks)
+            else:
+                s_sym, s_price, s_ts, s_ord, s_sid = symbol, price, ts, ordinals, sidx
+            n_local[0] = s_ts.numel()
+            # columns: symbol, price, volume (not read: aliased), timestamp attribute = global ordinal
+            app.process_device_events(s_sid, s_ts, [s_sym, s_price, s_price, s_ord], ordinals=s_ord,
+                                      hip_stream=hip_stream)
+            return int(app.get_stat("output_events:q"))
         if args.config == 4 and world > 1:
             (s_sym, s_price, s_ts, s_ord), _ = exchange_by_key(symbol, [symbol, price, ts, ordinals], world)
         elif args.config == 4:
@@ -237,7 +335,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         sample = args.cpu_sample or cfg["cpu_sample"]
         log(f"cpu baseline on {sample} events")
-        v, sec, mm = cpu_baseline(sample, K, ts_div, cfg["app"], seed, cfg["out"])
+        v, sec, mm = cpu_baseline(sample, K, ts_div, cfg["app"], seed, cfg["out"], args.config)
         cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port",
                "sample": f"first {sample} events of the same stream through oracle/cpu_ref "
                          f"(C++ restatement of the reference engine, 1 thread): {sec:.2f} s, {mm} matches"}
@@ -245,12 +343,13 @@ def main():
         alg = cfg["job_bytes"](N, total_matches) * (1 if cfg["shards"] else world)
         conf = {"workload": cfg["workload"], "config": args.config, "events": N,
                 "event_time": f"floor(i/{ts_div}) ms", "matches": total_matches,
-                "parallelism": (f"key-sharded x{world}" if args.config == 4 else
+                "parallelism": (f"key-sharded x{world}" if args.config in (4, 5) else
                                 f"index-range-sharded x{world}" if cfg["shards"] else f"replicas x{world}"),
-                "device_path": {1: "general closed form", 2: "onesweep closed form", 3: "filter interpreter",
-                                4: "filter typed conjunction"}.get(int(path), str(path)),
+                "device_path": ("general NFA (interleaved device events)" if args.config == 5 else
+                                {1: "general closed form", 2: "onesweep closed form", 3: "filter interpreter",
+                                 4: "filter typed conjunction"}.get(int(path), str(path))),
                 "step_hbm_fraction": alg / (ms_per_step * 1e-3) / HBM_PEAK}
-        if args.config == 4:
+        if args.config in (4, 5):
             conf["keys"] = K
         line = {
             "metric": METRIC if args.config == 4 else f"input events/sec + % HBM peak, {cfg['workload']}",
@@ -268,7 +367,8 @@ def main():
 # ALGORITHMIC bytes per launch for a batch of n events with m matches: what each launch must read
 # and write at minimum.
 KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last",
-           "filter_count", "filter_scan", "filter_write"]
+           "filter_count", "filter_scan", "filter_write",
+           "event_index", "nfa_select", "nfa_group", "nfa_setup", "nfa"]
 
 
 def alg_bytes(label, n, m, config):
@@ -288,6 +388,14 @@ def alg_bytes(label, n, m, config):
             "filter_count": 16 * n + n // 8,  # price f64 + volume i64 in, one mask bit per event out
             "filter_scan": 0,
             "filter_write": n // 8 + 4 * m,   # mask in, u32 row per kept event out
+            # config 5 (general NFA over an interleaved batch): index build reads event time + stream id and
+            # writes row / ordinal / clock / advance points; the NFA kernel must at least read each event's key
+            # position, stream id, event time, price and key (and write the output events)
+            "event_index": 8 * n + 4 * n + 8 * 3 * n + 24 * n,
+            "nfa_select": 4 * n + 8 * n,
+            "nfa_group": 4 * n + 8 * n + 8 * n,
+            "nfa_setup": 0,
+            "nfa": 8 * n + 4 * n + 8 * n + 8 * n + 4 * n + 40 * m,
             }[label]
 
 

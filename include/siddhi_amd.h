@@ -13,6 +13,8 @@
  *   sm_app_advance_time             @app:playback heartbeat (EventTimeBasedMillisTimestampGenerator.java:99)
  *   sm_app_process_device_batch     StreamJunction.sendData over a device-resident columnar batch (no Java
  *                                   counterpart: the bulk entry a JNI/Panama receiver would call)
+ *   sm_app_process_device_events    a sequence of InputHandler.send calls over several streams of one
+ *                                   schema (InputHandler.java:53 → StreamJunction.sendData :232), device-resident
  *
  * Threading / delivery: an app handle is single-owner (calls are serialised internally). Events are
  * staged on send and processed on the GPU at sm_app_flush (also at shutdown and when the staging buffer
@@ -110,6 +112,15 @@ int sm_app_set_option(sm_app* app, const char* key, int64_t value);
 int sm_app_process_device_batch(sm_app* app, const char* stream_id, size_t n, const int64_t* d_timestamps,
                                 const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
                                 void* hip_stream);
+/* Interleaved device batch: event i belongs to stream d_stream_idx[i] (the index of sm_app_stream_schema
+ * order = define-stream order); every stream a query reads has the schema of d_cols. Pattern / sequence queries
+ * run on the GPU (general NFA kernel, playback timers included); outputs go to the callbacks in reference
+ * order before the call returns. Ordinals: d_ordinals[i] if given, else ordinal_base + i. d_stream_idx[i] = -1
+ * marks a playback heartbeat (sm_app_advance_time at d_timestamps[i]; no event, no ordinal).
+ * "output_events:<query>" (sm_app_get_stat) = output events of the last such batch. */
+int sm_app_process_device_events(sm_app* app, size_t n, const int32_t* d_stream_idx, const int64_t* d_timestamps,
+                                 const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
+                                 void* hip_stream);
 /* Match tuples of the last device batch for a query: n pairs (e1, e2) of ordinals relative to the batch's
  * ordinal_base, uint32[2*n] in device memory, in reference output order (e2 ordinal, then e1 ordinal). */
 int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** d_pairs, size_t* n);

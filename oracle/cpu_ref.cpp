@@ -1895,29 +1895,50 @@ int cr_send(cr_app* app, int si, int64_t ts, const cr_value* row, char* err, siz
   return 0;
 }
 
+// One columnar row -> a pooled Row (the converters of InputHandler.send copy each attribute value).
+static std::shared_ptr<Row> row_from_columns(OApp* a, const StreamDef* d, const void* const* cols, size_t i) {
+  auto r = std::make_shared<Row>();
+  r->ordinal = a->next_ordinal++;
+  r->vals.resize(d->attrs.size());
+  for (size_t k = 0; k < d->attrs.size(); ++k) {
+    Value& v = r->vals[k];
+    v.t = d->attrs[k].type;
+    v.null = false;
+    switch (v.t) {
+      case AttrType::INT: v.i = ((const int32_t*)cols[k])[i]; break;
+      case AttrType::LONG: v.i = ((const int64_t*)cols[k])[i]; break;
+      case AttrType::FLOAT: v.d = ((const float*)cols[k])[i]; break;
+      case AttrType::DOUBLE: v.d = ((const double*)cols[k])[i]; break;
+      case AttrType::BOOL: v.i = ((const uint8_t*)cols[k])[i] ? 1 : 0; break;
+      case AttrType::STRING: throw RuntimeError("string columns are not supported by cr_send_columns");
+    }
+  }
+  return r;
+}
+
 int cr_send_columns(cr_app* app, int si, size_t n, const int64_t* ts, const void* const* cols, char* err,
                     size_t errlen) {
   OApp* a = static_cast<OApp*>(app);
   try {
     const StreamDef* d = a->streams[si].def;
+    for (size_t i = 0; i < n; ++i) send_row(a, si, ts[i], row_from_columns(a, d, cols, i));
+  } catch (const std::exception& e) {
+    set_err(err, errlen, e.what());
+    return 6;
+  }
+  return 0;
+}
+
+// Interleaved multi-stream batch: event i goes to stream stream_idx[i] exactly as the i-th of a sequence of
+// InputHandler.send calls (InputHandler.java:53) would; every stream in the batch has the columns' schema.
+int cr_send_interleaved(cr_app* app, size_t n, const int32_t* stream_idx, const int64_t* ts, const void* const* cols,
+                        char* err, size_t errlen) {
+  OApp* a = static_cast<OApp*>(app);
+  try {
     for (size_t i = 0; i < n; ++i) {
-      auto r = std::make_shared<Row>();
-      r->ordinal = a->next_ordinal++;
-      r->vals.resize(d->attrs.size());
-      for (size_t k = 0; k < d->attrs.size(); ++k) {
-        Value& v = r->vals[k];
-        v.t = d->attrs[k].type;
-        v.null = false;
-        switch (v.t) {
-          case AttrType::INT: v.i = ((const int32_t*)cols[k])[i]; break;
-          case AttrType::LONG: v.i = ((const int64_t*)cols[k])[i]; break;
-          case AttrType::FLOAT: v.d = ((const float*)cols[k])[i]; break;
-          case AttrType::DOUBLE: v.d = ((const double*)cols[k])[i]; break;
-          case AttrType::BOOL: v.i = ((const uint8_t*)cols[k])[i] ? 1 : 0; break;
-          case AttrType::STRING: throw RuntimeError("string columns are not supported by cr_send_columns");
-        }
-      }
-      send_row(a, si, ts[i], std::move(r));
+      int si = stream_idx[i];
+      if (si < 0 || si >= (int)a->streams.size()) throw RuntimeError("bad stream index");
+      send_row(a, si, ts[i], row_from_columns(a, a->streams[si].def, cols, i));
     }
   } catch (const std::exception& e) {
     set_err(err, errlen, e.what());

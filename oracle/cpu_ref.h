@@ -38,6 +38,9 @@ int cr_send(cr_app* app, int stream_index, int64_t ts, const cr_value* row, char
  * attribute column (int32_t*, int64_t*, float*, double*; strings unsupported here). */
 int cr_send_columns(cr_app* app, int stream_index, size_t n, const int64_t* ts, const void* const* cols,
                     char* err, size_t errlen);
+/* interleaved batch over streams sharing one schema: event i -> stream stream_idx[i] */
+int cr_send_interleaved(cr_app* app, size_t n, const int32_t* stream_idx, const int64_t* ts, const void* const* cols,
+                        char* err, size_t errlen);
 /* Outputs collected since creation, as JSON text:
  * {"streams": {"<id>": [[ts, [values...], [refs...]], ...]},
  *  "queries": {"<name>": [[ts, [[values...], ...]], ...]}}

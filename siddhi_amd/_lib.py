@@ -18,7 +18,7 @@ EXPORTS = [
     "sm_app_start", "sm_app_flush", "sm_app_shutdown", "sm_app_input_handler", "sm_input_send",
     "sm_input_send_columns", "sm_app_stream_schema", "sm_app_advance_time", "sm_app_advance_wallclock",
     "sm_app_add_stream_callback", "sm_app_add_query_callback", "sm_app_set_collect", "sm_app_dump_outputs",
-    "sm_app_set_option", "sm_app_process_device_batch", "sm_app_device_matches",
+    "sm_app_set_option", "sm_app_process_device_batch", "sm_app_process_device_events", "sm_app_device_matches",
     "sm_app_get_stat",
 ]
 
@@ -67,6 +67,7 @@ def lib():
         L.sm_app_dump_outputs.restype = sz
         L.sm_app_set_option.argtypes = [vp, cp, i64]
         L.sm_app_process_device_batch.argtypes = [vp, cp, sz, vp, ctypes.POINTER(vp), vp, i64, vp]
+        L.sm_app_process_device_events.argtypes = [vp, sz, vp, vp, ctypes.POINTER(vp), vp, i64, vp]
         L.sm_app_device_matches.argtypes = [vp, cp, ctypes.POINTER(vp), ctypes.POINTER(sz)]
         L.sm_app_get_stat.argtypes = [vp, cp, ctypes.POINTER(ctypes.c_double)]
         _lib = L

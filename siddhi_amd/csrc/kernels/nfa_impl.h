@@ -1047,6 +1047,29 @@ __device__ StackVal StateLoader::var(const Instr& in) const {
   return v;
 }
 
+// First index a in [from, n) with v[a] >= x (or, with strict, v[a] > x) over a non-decreasing array; n if none.
+// Galloping from `from`: a key lane's successive searches land close to the previous answer, and a batch of N
+// playback events has N advance points, so a linear step per key would make the whole launch O(keys x N).
+template <bool strict>
+__device__ int64_t gallop(const int64_t* __restrict__ v, int64_t from, int64_t n, int64_t x) {
+  auto before = [&](int64_t a) { return strict ? v[a] <= x : v[a] < x; };
+  if (from >= n || !before(from)) return from;
+  int64_t lo = from, step = 1;  // invariant: before(lo)
+  int64_t hi = from + 1;
+  while (hi < n && before(hi)) {
+    lo = hi;
+    step <<= 1;
+    hi = lo + step;
+  }
+  if (hi > n) hi = n;  // answer in (lo, hi]
+  while (hi - lo > 1) {
+    int64_t mid = lo + ((hi - lo) >> 1);
+    if (before(mid)) lo = mid;
+    else hi = mid;
+  }
+  return hi;
+}
+
 __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
                          int32_t heap_half, int32_t key, int32_t* err_out) {
   const DQuery* q = (const DQuery*)blob;
@@ -1109,8 +1132,10 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
         int64_t t;
         if (!L.min_head(t)) break;
         // first advance point at or after search_from whose position <= next_pos and (clock >= t or wall tick)
-        int64_t a = search_from;
-        while (a < b.nadv && b.adv_pos[a] <= next_pos && b.adv_clock[a] < t) ++a;
+        // (both arrays are non-decreasing: positions ascend and the playback clock only moves forward)
+        const int64_t a1 = gallop<true>(b.adv_pos, search_from, b.nadv, next_pos);
+        const int64_t a2 = gallop<false>(b.adv_clock, search_from, b.nadv, t);
+        const int64_t a = a1 < a2 ? a1 : a2;
         if (a >= b.nadv || b.adv_pos[a] > next_pos) {
           search_from = a;
           break;
@@ -1141,7 +1166,7 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
       L.deliver(p);
     }
     // timers scheduled by this event may only fire at later advance points
-    while (search_from < b.nadv && b.adv_pos[search_from] <= p) ++search_from;
+    search_from = gallop<true>(b.adv_pos, search_from, b.nadv, p);
     ++k;
     if (L.err) break;
     L.safe_point();

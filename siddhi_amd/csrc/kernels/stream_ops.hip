@@ -355,6 +355,115 @@ __global__ void rehash_kernel(const int64_t* __restrict__ slot_keys, int64_t nsl
 
 inline dim3 grid_for(int64_t n, int t = 256) { return dim3((unsigned)((n + t - 1) / t)); }
 
+
+// ---- device-resident interleaved batch (sm_app_process_device_events): the per-event arrays the host path
+// builds record by record in stage_record (runtime.cpp) — row, ordinal, playback clock after sendData and the
+// clock-advance points (StreamJunction.sendData :232-237: the clock moves, and listeners fire, only if ts >= clock).
+constexpr int kIxThreads = 256, kIxItems = 16, kIxTile = kIxThreads * kIxItems;
+
+__device__ __forceinline__ int64_t block_max_i64(int64_t v, int64_t* red) {
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t u = __shfl_xor(v, o, 64);
+    v = u > v ? u : v;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  v = red[0];
+  for (int k = 1; k < kIxThreads / 64; ++k) v = red[k] > v ? red[k] : v;
+  __syncthreads();
+  return v;
+}
+
+__global__ __launch_bounds__(kIxThreads) void ts_tile_max_kernel(const int64_t* __restrict__ ts, int64_t n,
+                                                                 int64_t* __restrict__ tile_max) {
+  __shared__ int64_t red[kIxThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * kIxTile;
+  int64_t m = INT64_MIN;
+  for (int k = 0; k < kIxItems; ++k) {
+    int64_t i = base + (int64_t)k * kIxThreads + threadIdx.x;
+    if (i < n) m = ts[i] > m ? ts[i] : m;
+  }
+  m = block_max_i64(m, red);
+  if (threadIdx.x == 0) tile_max[blockIdx.x] = m;
+}
+
+// exclusive running max over the tiles, seeded with the clock before the batch (one workgroup, sequential chunks)
+__global__ __launch_bounds__(kIxThreads) void tile_prefix_max_kernel(int64_t* __restrict__ tile_max, int64_t ntiles,
+                                                                     int64_t clock_in, int64_t* __restrict__ clock_out) {
+  __shared__ int64_t buf[kIxThreads];
+  int64_t carry = clock_in;
+  for (int64_t c = 0; c < ntiles; c += kIxThreads) {
+    int64_t i = c + threadIdx.x;
+    int64_t v = i < ntiles ? tile_max[i] : INT64_MIN;
+    buf[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < kIxThreads; o <<= 1) {  // Hillis-Steele inclusive max
+      int64_t u = threadIdx.x >= o ? buf[threadIdx.x - o] : INT64_MIN;
+      __syncthreads();
+      if (u > buf[threadIdx.x]) buf[threadIdx.x] = u;
+      __syncthreads();
+    }
+    int64_t excl = threadIdx.x ? buf[threadIdx.x - 1] : INT64_MIN;
+    excl = excl > carry ? excl : carry;
+    if (i < ntiles) tile_max[i] = excl;
+    int64_t last = buf[kIxThreads - 1];
+    __syncthreads();
+    carry = last > carry ? last : carry;
+  }
+  if (threadIdx.x == 0) *clock_out = carry;
+}
+
+// per event: row = i, ordinal, clock after sendData, advance flag (playback only)
+__global__ __launch_bounds__(kIxThreads) void event_index_kernel(
+    const int32_t* __restrict__ sid, int32_t nstreams, const int64_t* __restrict__ ts, int64_t n,
+    const int64_t* __restrict__ ord_in, int64_t ord_base, int playback, int64_t clock_in,
+    const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ ev_row, int64_t* __restrict__ ev_ord,
+    int64_t* __restrict__ ev_clock, uint8_t* __restrict__ adv_flag, int32_t* __restrict__ bad) {
+  __shared__ int64_t run[kIxThreads];
+  const int64_t base = (int64_t)blockIdx.x * kIxTile;
+  // each thread owns kIxItems consecutive events: a thread-serial running max, then a block scan of the totals
+  const int64_t first = base + (int64_t)threadIdx.x * kIxItems;
+  int64_t m = INT64_MIN;
+  for (int k = 0; k < kIxItems; ++k) {
+    int64_t i = first + k;
+    if (i < n) m = ts[i] > m ? ts[i] : m;
+  }
+  run[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 1; o < kIxThreads; o <<= 1) {
+    int64_t u = threadIdx.x >= o ? run[threadIdx.x - o] : INT64_MIN;
+    __syncthreads();
+    if (u > run[threadIdx.x]) run[threadIdx.x] = u;
+    __syncthreads();
+  }
+  int64_t clock = tile_prefix[blockIdx.x];
+  if (threadIdx.x) clock = run[threadIdx.x - 1] > clock ? run[threadIdx.x - 1] : clock;
+  for (int k = 0; k < kIxItems; ++k) {
+    int64_t i = first + k;
+    if (i >= n) break;
+    int64_t t = ts[i];
+    bool adv = playback && t >= clock;
+    if (playback && t > clock) clock = t;
+    const int32_t st = sid[i];
+    if (st < NFA_TICK || st >= nstreams) *bad = 1;  // plain vector store: any offender sets the flag
+    ev_row[i] = i;
+    ev_ord[i] = st < 0 ? -1 : ord_in ? ord_in[i] : ord_base + i;  // heartbeats carry no event ordinal
+    ev_clock[i] = playback ? clock : clock_in;
+    adv_flag[i] = adv;
+  }
+}
+
+__global__ void advance_points_kernel(const uint8_t* __restrict__ flag, const uint32_t* __restrict__ excl, int64_t n,
+                                      const int64_t* __restrict__ ts, int64_t* __restrict__ adv_pos,
+                                      int64_t* __restrict__ adv_clock, int64_t* __restrict__ adv_wall) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !flag[i]) return;
+  uint32_t o = excl[i];
+  adv_pos[o] = i;
+  adv_clock[o] = ts[i];
+  adv_wall[o] = -1;
+}
 }  // namespace
 
 void KeyTable::release() {
@@ -545,6 +654,48 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
   *key_pos_out = key_pos;
   *key_off_out = key_off;
   return hv;
+}
+
+
+int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const int64_t* ts, const int64_t* ord_in,
+                          int64_t ord_base, bool playback, int64_t clock_in, int64_t* ev_row, int64_t* ev_ord,
+                          int64_t* ev_clock, int64_t* adv_pos, int64_t* adv_clock, int64_t* adv_wall,
+                          int64_t* clock_out, Scratch& sc, hipStream_t s) {
+  *clock_out = clock_in;
+  if (n == 0) return 0;
+  if (n >= (int64_t)UINT32_MAX) throw std::runtime_error("device event batch too large (>= 2^32 events)");
+  size_t mark = sc.used;
+  const int64_t ntiles = (n + kIxTile - 1) / kIxTile;
+  int64_t* tile_max = (int64_t*)sc.take(ntiles * 8);
+  int64_t* dclock = (int64_t*)sc.take(8);
+  uint8_t* flag = (uint8_t*)sc.take(n);
+  uint32_t* ex = (uint32_t*)sc.take(n * 4);
+  uint32_t* total = (uint32_t*)sc.take(4);
+  int32_t* bad = (int32_t*)sc.take(4);
+  SM_HIP(hipMemsetAsync(bad, 0, 4, s));
+  hipLaunchKernelGGL(ts_tile_max_kernel, dim3((unsigned)ntiles), dim3(kIxThreads), 0, s, ts, n, tile_max);
+  hipLaunchKernelGGL(tile_prefix_max_kernel, dim3(1), dim3(kIxThreads), 0, s, tile_max, ntiles, clock_in, dclock);
+  hipLaunchKernelGGL(event_index_kernel, dim3((unsigned)ntiles), dim3(kIxThreads), 0, s, sid, nstreams, ts, n, ord_in,
+                     ord_base, (int)playback, clock_in, tile_max, ev_row, ev_ord, ev_clock, flag, bad);
+  int64_t nadv = 0;
+  if (playback) {
+    hipLaunchKernelGGL(u8_to_u32_kernel, grid_for(n), dim3(256), 0, s, flag, n, ex);
+    exclusive_scan_u32(ex, n, sc, s, total);
+    hipLaunchKernelGGL(advance_points_kernel, grid_for(n), dim3(256), 0, s, flag, ex, n, ts, adv_pos, adv_clock,
+                       adv_wall);
+    uint32_t h = 0;
+    SM_HIP(hipMemcpyAsync(&h, total, 4, hipMemcpyDeviceToHost, s));
+    nadv = h;
+  }
+  int64_t hc = clock_in;
+  int32_t hbad = 0;
+  SM_HIP(hipMemcpyAsync(&hc, dclock, 8, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  if (hbad) throw std::invalid_argument("stream index out of range in device event batch");
+  if (playback) *clock_out = hc > clock_in ? hc : clock_in;
+  sc.used = mark;
+  return nadv;
 }
 
 }  // namespace sm

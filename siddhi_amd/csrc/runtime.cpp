@@ -188,6 +188,7 @@ struct sm_app {
   bool shut = false;
   int64_t batch_events = 1 << 20;
   int32_t heap_half = 1024;
+  int64_t out_records = 0;  // option "output_records" (0 = automatic)
   bool collect = false;
   std::map<std::string, std::vector<std::string>> collected_streams;  // JSON fragments
   std::map<std::string, std::vector<std::string>> collected_queries;
@@ -471,6 +472,98 @@ void upload(sm_app* a, DBuf& d, const std::vector<T>& v) {
   if (!v.empty()) SM_HIP(hipMemcpyAsync(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, a->stream));
 }
 
+// Device-side view of one batch in arrival order (uploaded by flush, or built on the device by
+// sm_app_process_device_events).
+struct EvArrays {
+  const int32_t* ev_stream;
+  const int64_t* ev_row;
+  const int64_t* ev_ts;
+  const int64_t* ev_clock;
+  const int64_t* ev_ord;
+  const NfaStream* streams;
+  const int64_t* adv_pos;
+  const int64_t* adv_clock;
+  const int64_t* adv_wall;
+  int64_t nadv;
+  int64_t clock_in;
+};
+
+// One pattern / sequence query over a batch: select its streams' records, group them by partition key, run the
+// NFA kernel (one lane per key) and read its output records back for ordered delivery.
+void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::vector<HostOut>& outs, hipStream_t hs,
+                       FastTimings* tm = nullptr) {
+  QueryRt& q = *a->queries[qi];
+  const DQuery& h = q.cq.hdr;
+  size_t stride = sizeof(OutRec) + h.nsel * sizeof(DVal) + h.nrefs * sizeof(int64_t);
+  uint64_t mask = 0;
+  for (int s : q.cq.streams) mask |= (1ull << s);
+  bool partitioned = h.partitioned;
+  int64_t* pos = (int64_t*)a->sc.take(N * 8);
+  int64_t nq = select_records(ev.ev_stream, N, mask, !partitioned, pos, a->sc, hs);
+  if (tm) tm->mark("nfa_select", hs);
+  int64_t* key_pos = pos;
+  int64_t* key_off = nullptr;
+  int64_t nkeys = 1;
+  if (partitioned) {
+    int64_t nv = group_by_key(q.keys, pos, nq, ev.ev_stream, ev.ev_row,
+                              ev.streams, (const KeyProg*)q.keyprogs.p, q.nkeyprogs, &key_pos,
+                              &key_off, a->sc, hs);
+    nq = nv;
+    nkeys = q.keys.nslots;
+  } else {
+    key_off = (int64_t*)a->sc.take(16);
+    int64_t ho[2] = {0, nq};
+    SM_HIP(hipMemcpyAsync(key_off, ho, 16, hipMemcpyHostToDevice, hs));
+  }
+  if (tm) tm->mark("nfa_group", hs);
+  if (nkeys == 0) return;
+  ensure_state(a, q, nkeys);
+  // output record capacity: option "output_records", else 8 per record (capped at 2^26 records); overflow
+  // is detected by the kernel and reported as an error naming the option
+  int64_t cap = a->out_records > 0 ? a->out_records : std::min<int64_t>(std::max<int64_t>(4096, 8 * nq + 1024), 1 << 26);
+  q.out.ensure((size_t)cap * stride);
+  NfaBatch b{};
+  b.ev_stream = ev.ev_stream;
+  b.ev_row = ev.ev_row;
+  b.ev_ts = ev.ev_ts;
+  b.ev_clock = ev.ev_clock;
+  b.ev_ord = ev.ev_ord;
+  b.streams = ev.streams;
+  b.adv_pos = ev.adv_pos;
+  b.adv_clock = ev.adv_clock;
+  b.adv_wall = ev.adv_wall;
+  b.nadv = ev.nadv;
+  b.clock_in = ev.clock_in;
+  b.key_off = key_off;
+  b.key_pos = key_pos;
+  b.create_all = !partitioned;
+  b.out = q.out.p;
+  b.out_count = (uint32_t*)a->d_count.p;
+  b.out_cap = (uint32_t)cap;
+  b.out_stride = (uint32_t)stride;
+  SM_HIP(hipMemsetAsync(a->d_count.p, 0, 4, hs));
+  SM_HIP(hipMemsetAsync(a->d_err.p, 0, 4, hs));
+  if (tm) tm->mark("nfa_setup", hs);
+  launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, (int32_t)nkeys,
+             (int32_t*)a->d_err.p, hs);
+  SM_HIP(hipGetLastError());
+  if (tm) tm->mark("nfa", hs);
+  uint32_t hc = 0;
+  int32_t he = 0;
+  SM_HIP(hipMemcpyAsync(&hc, a->d_count.p, 4, hipMemcpyDeviceToHost, hs));
+  SM_HIP(hipMemcpyAsync(&he, a->d_err.p, 4, hipMemcpyDeviceToHost, hs));
+  SM_HIP(hipStreamSynchronize(hs));
+  if (he) {
+    std::string why;
+    if (he & NFA_ERR_ARENA) why += " per-key partial-match arena exhausted (raise option heap_words);";
+    if (he & NFA_ERR_TIMERS) why += " timer queue full;";
+    if (he & NFA_ERR_OUTPUT) why += " output buffer full (raise option output_records);";
+    if (he & NFA_ERR_NPE) why += " NullPointerException/IllegalStateException path of the reference;";
+    throw std::runtime_error("query '" + q.cq.name + "':" + why);
+  }
+  read_outputs(a, qi, q.out.p, std::min<int64_t>(hc, cap), outs);
+}
+
 void flush(sm_app* a) {
   const int64_t N = (int64_t)a->ev_stream.size();
   if (N == 0) return;
@@ -505,6 +598,10 @@ void flush(sm_app* a) {
   a->d_count.ensure(16);
   ensure_scratch(a, (size_t)N * 96 + (64 << 20));
   std::vector<HostOut> outs;
+  const EvArrays ev{(const int32_t*)a->d_ev_stream.p, (const int64_t*)a->d_ev_row.p, (const int64_t*)a->d_ev_ts.p,
+                    (const int64_t*)a->d_ev_clock.p, (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p,
+                    (const int64_t*)a->d_adv_pos.p, (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p,
+                    (int64_t)a->adv_pos.size(), a->clock_batch_in};
   for (size_t qi = 0; qi < a->queries.size(); ++qi) {
     QueryRt& q = *a->queries[qi];
     const DQuery& h = q.cq.hdr;
@@ -525,68 +622,7 @@ void flush(sm_app* a) {
       read_outputs(a, (int)qi, q.out.p, nm, outs);
       continue;
     }
-    // ---- pattern / sequence query
-    uint64_t mask = 0;
-    for (int s : q.cq.streams) mask |= (1ull << s);
-    bool partitioned = h.partitioned;
-    int64_t* pos = (int64_t*)a->sc.take(N * 8);
-    int64_t nq = select_records((const int32_t*)a->d_ev_stream.p, N, mask, !partitioned, pos, a->sc, a->stream);
-    int64_t* key_pos = pos;
-    int64_t* key_off = nullptr;
-    int64_t nkeys = 1;
-    if (partitioned) {
-      int64_t nv = group_by_key(q.keys, pos, nq, (const int32_t*)a->d_ev_stream.p, (const int64_t*)a->d_ev_row.p,
-                                (const NfaStream*)a->d_streams.p, (const KeyProg*)q.keyprogs.p, q.nkeyprogs, &key_pos,
-                                &key_off, a->sc, a->stream);
-      nq = nv;
-      nkeys = q.keys.nslots;
-    } else {
-      key_off = (int64_t*)a->sc.take(16);
-      int64_t ho[2] = {0, nq};
-      SM_HIP(hipMemcpyAsync(key_off, ho, 16, hipMemcpyHostToDevice, a->stream));
-    }
-    if (nkeys == 0) continue;
-    ensure_state(a, q, nkeys);
-    int64_t cap = std::max<int64_t>(4096, 8 * nq + 1024);
-    q.out.ensure((size_t)cap * stride);
-    NfaBatch b{};
-    b.ev_stream = (const int32_t*)a->d_ev_stream.p;
-    b.ev_row = (const int64_t*)a->d_ev_row.p;
-    b.ev_ts = (const int64_t*)a->d_ev_ts.p;
-    b.ev_clock = (const int64_t*)a->d_ev_clock.p;
-    b.ev_ord = (const int64_t*)a->d_ev_ord.p;
-    b.streams = (const NfaStream*)a->d_streams.p;
-    b.adv_pos = (const int64_t*)a->d_adv_pos.p;
-    b.adv_clock = (const int64_t*)a->d_adv_clock.p;
-    b.adv_wall = (const int64_t*)a->d_adv_wall.p;
-    b.nadv = (int64_t)a->adv_pos.size();
-    b.clock_in = a->clock_batch_in;
-    b.key_off = key_off;
-    b.key_pos = key_pos;
-    b.create_all = !partitioned;
-    b.out = q.out.p;
-    b.out_count = (uint32_t*)a->d_count.p;
-    b.out_cap = (uint32_t)cap;
-    b.out_stride = (uint32_t)stride;
-    SM_HIP(hipMemsetAsync(a->d_count.p, 0, 4, a->stream));
-    SM_HIP(hipMemsetAsync(a->d_err.p, 0, 4, a->stream));
-    launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, (int32_t)nkeys,
-               (int32_t*)a->d_err.p, a->stream);
-    SM_HIP(hipGetLastError());
-    uint32_t hc = 0;
-    int32_t he = 0;
-    SM_HIP(hipMemcpyAsync(&hc, a->d_count.p, 4, hipMemcpyDeviceToHost, a->stream));
-    SM_HIP(hipMemcpyAsync(&he, a->d_err.p, 4, hipMemcpyDeviceToHost, a->stream));
-    SM_HIP(hipStreamSynchronize(a->stream));
-    if (he) {
-      std::string why;
-      if (he & NFA_ERR_ARENA) why += " per-key partial-match arena exhausted (raise option heap_words);";
-      if (he & NFA_ERR_TIMERS) why += " timer queue full;";
-      if (he & NFA_ERR_OUTPUT) why += " output buffer full;";
-      if (he & NFA_ERR_NPE) why += " NullPointerException/IllegalStateException path of the reference;";
-      throw std::runtime_error("query '" + q.cq.name + "':" + why);
-    }
-    read_outputs(a, (int)qi, q.out.p, std::min<int64_t>(hc, cap), outs);
+    run_pattern_query(a, (int)qi, ev, N, outs, a->stream);
   }
   // ---- batch done
   a->ordinal_base += N;
@@ -882,6 +918,34 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
         a->fast_tm_ready = true;
       }
       a->fast_timing = value != 0;
+    } else if (k == "reset") {
+      // drop every partition instance, partial match, pending timer and the playback clock, keeping the device
+      // allocations: the state of a freshly created runtime of the same app (bench / test helper)
+      a->ev_stream.clear();
+      a->ev_row.clear();
+      a->ev_ts.clear();
+      a->ev_clock.clear();
+      a->ev_ord.clear();
+      a->adv_pos.clear();
+      a->adv_clock.clear();
+      a->adv_wall.clear();
+      for (auto& st : a->streams) st.clear();
+      for (auto& q : a->queries) {
+        if (q->keys.tslots) SM_HIP(hipMemsetAsync(q->keys.tslots, 0, (size_t)q->keys.cap * 4, a->stream));
+        q->keys.nslots = 0;
+        if (q->state_slots) SM_HIP(hipMemsetAsync(q->ks.p, 0, (size_t)q->state_slots * q->cq.hdr.ks_words * 8, a->stream));
+        q->dev_n = 0;
+      }
+      SM_HIP(hipStreamSynchronize(a->stream));
+      a->clock = a->clock_batch_in = 0;
+      a->next_ordinal = a->ordinal_base = 0;
+      a->started = false;
+      if (value) {  // reset and start again
+        a->started = true;
+        stage_record(a, NFA_START, -1, a->clock, 0);
+      }
+    } else if (k == "output_records") {
+      a->out_records = std::max<int64_t>(0, value);
     } else if (k == "batch_events") {
       a->batch_events = std::max<int64_t>(1, value);
     } else {
@@ -988,10 +1052,98 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
   });
 }
 
+// Interleaved multi-stream batch already resident in HBM: the device form of a sequence of InputHandler.send
+// calls (InputHandler.java:53 → StreamJunction.sendData :232) over streams that share one schema. Staged host
+// events are flushed first, so arrival order across both entry points is kept. Pattern / sequence queries run
+// through the general NFA kernel exactly as in flush(); outputs are delivered to callbacks in reference order.
+int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_idx, const int64_t* d_ts,
+                                 const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
+                                 void* hip_stream) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    flush(a);
+    if (n == 0) return;
+    hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
+    // every stream a query reads must carry the batch schema (the schema of the first such stream)
+    const std::vector<sql::Attribute>* schema = nullptr;
+    for (auto& qp : a->queries) {
+      if (qp->cq.hdr.kind == 0)
+        throw sql::UnsupportedError("interleaved device batches run pattern / sequence queries; filter query '" +
+                                    qp->cq.name + "' takes sm_app_process_device_batch");
+      for (int s : qp->cq.streams) {
+        const auto& at = a->streams[s].def->attrs;
+        if (!schema) schema = &at;
+        bool same = at.size() == schema->size();
+        for (size_t k = 0; same && k < at.size(); ++k) same = at[k].type == (*schema)[k].type;
+        if (!same)
+          throw sql::ValidationError("stream '" + a->streams[s].def->id +
+                                     "' does not share the interleaved batch schema");
+      }
+    }
+    if (!schema) return;
+    std::vector<NfaStream> nst(a->streams.size());
+    for (size_t s = 0; s < a->streams.size(); ++s) {
+      NfaStream& d = nst[s];
+      memset(&d, 0, sizeof(d));
+      const auto& at = a->streams[s].def->attrs;
+      bool same = at.size() == schema->size();
+      for (size_t k = 0; same && k < at.size(); ++k) same = at[k].type == (*schema)[k].type;
+      if (!same) continue;  // never read: no query of this app selects it
+      d.nattr = (int)at.size();
+      for (int k = 0; k < d.nattr; ++k) {
+        d.types[k] = (int)at[k].type;
+        d.cols[k] = d_cols[k];
+      }
+    }
+    a->d_streams.ensure(nst.size() * sizeof(NfaStream));
+    SM_HIP(hipMemcpyAsync(a->d_streams.p, nst.data(), nst.size() * sizeof(NfaStream), hipMemcpyHostToDevice, hs));
+    const int64_t N = (int64_t)n;
+    for (DBuf* d : {&a->d_ev_row, &a->d_ev_clock, &a->d_ev_ord, &a->d_adv_pos, &a->d_adv_clock, &a->d_adv_wall})
+      d->ensure((size_t)N * 8);
+    a->d_err.ensure(16);
+    a->d_count.ensure(16);
+    ensure_scratch(a, (size_t)N * 96 + (64 << 20));
+    a->sc.used = 0;
+    FastTimings* tm = a->fast_timing ? &a->fast_tm : nullptr;
+    if (tm) {
+      tm->nmk = 0;
+      tm->mark("start", hs);
+    }
+    int64_t clock_out = a->clock;
+    const int64_t nadv = build_event_index(
+        N, d_stream_idx, (int32_t)a->streams.size(), d_ts, d_ordinals, ordinal_base, a->ast.playback, a->clock, (int64_t*)a->d_ev_row.p, (int64_t*)a->d_ev_ord.p,
+        (int64_t*)a->d_ev_clock.p, (int64_t*)a->d_adv_pos.p, (int64_t*)a->d_adv_clock.p, (int64_t*)a->d_adv_wall.p,
+        &clock_out, a->sc, hs);
+    if (tm) tm->mark("event_index", hs);
+    const EvArrays ev{d_stream_idx, (const int64_t*)a->d_ev_row.p, d_ts, (const int64_t*)a->d_ev_clock.p,
+                      (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p, (const int64_t*)a->d_adv_pos.p,
+                      (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p, nadv, a->clock};
+    std::vector<HostOut> outs;
+    for (size_t qi = 0; qi < a->queries.size(); ++qi) {
+      a->sc.used = 0;
+      run_pattern_query(a, (int)qi, ev, N, outs, hs, tm);
+      a->queries[qi]->dev_n = 0;
+    }
+    for (auto& h : outs) a->queries[h.qidx]->dev_n++;
+    a->clock = clock_out;
+    a->clock_batch_in = a->clock;
+    if (!d_ordinals) a->next_ordinal = std::max<int64_t>(a->next_ordinal, ordinal_base + N);
+    deliver(a, outs);
+  });
+}
+
 int sm_app_get_stat(sm_app* a, const char* key, double* out) {
   std::lock_guard<std::mutex> g(a->mu);
   return guarded([&] {
     std::string k = key ? key : "";
+    if (k.rfind("output_events:", 0) == 0) {  // output events of the last device batch
+      for (auto& q : a->queries)
+        if (q->cq.name == k.substr(14)) {
+          *out = (double)q->dev_n;
+          return;
+        }
+      throw sql::ValidationError("No query with name " + k.substr(14));
+    }
     if (k.rfind("fast_path:", 0) == 0) {
       for (auto& q : a->queries)
         if (q->cq.name == k.substr(10)) {

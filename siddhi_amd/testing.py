@@ -106,6 +106,14 @@ class ProductApp:
                                                 ordinals.data_ptr() if ordinals is not None else None,
                                                 int(ordinal_base), hip_stream))
 
+    def process_device_events(self, stream_idx, ts_tensor, col_tensors, ordinals=None, ordinal_base=0,
+                              hip_stream=None):
+        """Interleaved batch over streams of one schema (event i -> stream stream_idx[i], int32 tensor)."""
+        ptrs = (ctypes.c_void_p * len(col_tensors))(*[t.data_ptr() for t in col_tensors])
+        _call(lib().sm_app_process_device_events(self.h, ts_tensor.numel(), stream_idx.data_ptr(), ts_tensor.data_ptr(),
+                                                 ptrs, ordinals.data_ptr() if ordinals is not None else None,
+                                                 int(ordinal_base), hip_stream))
+
     def device_matches(self, query):
         p = ctypes.c_void_p()
         n = ctypes.c_size_t()

@@ -31,6 +31,8 @@ def lib():
                               ctypes.c_size_t]
         L.cr_send_columns.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p,
                                       ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_size_t]
+        L.cr_send_interleaved.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_size_t]
         L.cr_advance_time.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_size_t]
         L.cr_advance_wallclock.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_size_t]
         L.cr_dump_outputs.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
@@ -102,6 +104,18 @@ class OracleApp:
                 arr[k].i = int(v)
         err = ctypes.create_string_buffer(2048)
         rc = lib().cr_send(self.h, self.stream_index(sid), int(ts), arr, err, 2048)
+        if rc != 0:
+            raise EngineError(rc, err.value.decode())
+
+    def send_interleaved(self, stream_idx, ts, cols):
+        """numpy arrays: int32 stream index per event, int64 event time, one column per schema attribute."""
+        import numpy as np
+        sidx = np.ascontiguousarray(stream_idx, dtype=np.int32)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        ptrs = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        err = ctypes.create_string_buffer(512)
+        rc = lib().cr_send_interleaved(self.h, len(ts), sidx.ctypes.data, ts.ctypes.data, ptrs, err, 512)
         if rc != 0:
             raise EngineError(rc, err.value.decode())
 
