@@ -32,6 +32,7 @@ struct NfaBatch {
   const int64_t* adv_pos;
   const int64_t* adv_clock;
   const int64_t* adv_wall;   // wall tick target, -1 for playback points
+  const int64_t* adv_upto;   // per record position: advance points at positions <= it (nullable)
   int64_t nadv;
   int64_t clock_in;          // clock before the batch
   // this query's records grouped by key slot: key_pos[key_off[k] .. key_off[k+1]) ascending

@@ -1070,6 +1070,15 @@ __device__ int64_t gallop(const int64_t* __restrict__ v, int64_t from, int64_t n
   return hi;
 }
 
+// First advance point after position x, at or after index `from`: O(1) through the per-position count of
+// advance points (adv_upto[x] = advance points at positions <= x), galloping when the batch has none.
+__device__ __forceinline__ int64_t adv_after(const NfaBatch& b, int64_t from, int64_t x) {
+  if (x == INT64_MAX) return b.nadv > from ? b.nadv : from;
+  if (!b.adv_upto) return gallop<true>(b.adv_pos, from, b.nadv, x);
+  const int64_t u = b.adv_upto[x];
+  return u > from ? u : from;
+}
+
 __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
                          int32_t heap_half, int32_t key, int32_t* err_out) {
   const DQuery* q = (const DQuery*)blob;
@@ -1133,7 +1142,12 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
         if (!L.min_head(t)) break;
         // first advance point at or after search_from whose position <= next_pos and (clock >= t or wall tick)
         // (both arrays are non-decreasing: positions ascend and the playback clock only moves forward)
-        const int64_t a1 = gallop<true>(b.adv_pos, search_from, b.nadv, next_pos);
+        const int64_t a1 = adv_after(b, search_from, next_pos);
+        // quick reject: every advance point up to next_pos has clock <= the clock after next_pos's sendData
+        if (next_pos != INT64_MAX && b.ev_clock[next_pos] < t) {
+          search_from = a1;
+          break;
+        }
         const int64_t a2 = gallop<false>(b.adv_clock, search_from, b.nadv, t);
         const int64_t a = a1 < a2 ? a1 : a2;
         if (a >= b.nadv || b.adv_pos[a] > next_pos) {
@@ -1166,7 +1180,7 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
       L.deliver(p);
     }
     // timers scheduled by this event may only fire at later advance points
-    search_from = gallop<true>(b.adv_pos, search_from, b.nadv, p);
+    search_from = adv_after(b, search_from, p);
     ++k;
     if (L.err) break;
     L.safe_point();

@@ -42,6 +42,6 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
 int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const int64_t* ts, const int64_t* ord_in,
                           int64_t ord_base, bool playback, int64_t clock_in, int64_t* ev_row, int64_t* ev_ord,
                           int64_t* ev_clock, int64_t* adv_pos, int64_t* adv_clock, int64_t* adv_wall,
-                          int64_t* clock_out, Scratch& sc, hipStream_t s);
+                          int64_t* adv_upto, int64_t* clock_out, Scratch& sc, hipStream_t s);
 
 }  // namespace sm

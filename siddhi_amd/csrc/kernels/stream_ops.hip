@@ -307,11 +307,11 @@ __global__ void gather_i64_kernel(const int64_t* __restrict__ src, const uint32_
   if (i < n) dst[i] = src[idx[i]];
 }
 
-__global__ void slot_to_u32_kernel(const int32_t* __restrict__ slot, int64_t n, uint32_t* __restrict__ key,
-                                   uint32_t* __restrict__ idx) {
+__global__ void slot_to_u32_kernel(const int32_t* __restrict__ slot, int64_t n, uint32_t nslots,
+                                   uint32_t* __restrict__ key, uint32_t* __restrict__ idx) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    key[i] = (uint32_t)slot[i];
+    key[i] = slot[i] < 0 ? nslots : (uint32_t)slot[i];  // records without a key (null) sort last
     idx[i] = (uint32_t)i;
   }
 }
@@ -420,46 +420,50 @@ __global__ __launch_bounds__(kIxThreads) void event_index_kernel(
     const int64_t* __restrict__ ord_in, int64_t ord_base, int playback, int64_t clock_in,
     const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ ev_row, int64_t* __restrict__ ev_ord,
     int64_t* __restrict__ ev_clock, uint8_t* __restrict__ adv_flag, int32_t* __restrict__ bad) {
-  __shared__ int64_t run[kIxThreads];
+  __shared__ int64_t wmax[kIxThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t base = (int64_t)blockIdx.x * kIxTile;
-  // each thread owns kIxItems consecutive events: a thread-serial running max, then a block scan of the totals
-  const int64_t first = base + (int64_t)threadIdx.x * kIxItems;
-  int64_t m = INT64_MIN;
+  int64_t carry = tile_prefix[blockIdx.x];  // clock before this tile (clock_in folded in)
+  // kIxItems rounds of 256 consecutive events (coalesced): block inclusive max-scan per round, carried over
   for (int k = 0; k < kIxItems; ++k) {
-    int64_t i = first + k;
-    if (i < n) m = ts[i] > m ? ts[i] : m;
-  }
-  run[threadIdx.x] = m;
-  __syncthreads();
-  for (int o = 1; o < kIxThreads; o <<= 1) {
-    int64_t u = threadIdx.x >= o ? run[threadIdx.x - o] : INT64_MIN;
+    const int64_t i = base + (int64_t)k * kIxThreads + threadIdx.x;
+    const bool in = i < n;
+    const int64_t t = in ? ts[i] : INT64_MIN;
+    int64_t v = t;
+    for (int o = 1; o < 64; o <<= 1) {
+      int64_t u = __shfl_up(v, o, 64);
+      if (lane >= o && u > v) v = u;
+    }
+    if (lane == 63) wmax[w] = v;
     __syncthreads();
-    if (u > run[threadIdx.x]) run[threadIdx.x] = u;
+    int64_t before = carry;  // max of everything before this event (exclusive)
+    for (int q = 0; q < w; ++q) before = wmax[q] > before ? wmax[q] : before;
+    int64_t up = __shfl_up(v, 1, 64);
+    if (lane > 0 && up > before) before = up;
+    int64_t round_max = carry;
+    for (int q = 0; q < kIxThreads / 64; ++q) round_max = wmax[q] > round_max ? wmax[q] : round_max;
     __syncthreads();
-  }
-  int64_t clock = tile_prefix[blockIdx.x];
-  if (threadIdx.x) clock = run[threadIdx.x - 1] > clock ? run[threadIdx.x - 1] : clock;
-  for (int k = 0; k < kIxItems; ++k) {
-    int64_t i = first + k;
-    if (i >= n) break;
-    int64_t t = ts[i];
-    bool adv = playback && t >= clock;
-    if (playback && t > clock) clock = t;
+    carry = round_max;
+    if (!in) continue;
     const int32_t st = sid[i];
     if (st < NFA_TICK || st >= nstreams) *bad = 1;  // plain vector store: any offender sets the flag
+    const bool adv = playback && t >= before;
     ev_row[i] = i;
     ev_ord[i] = st < 0 ? -1 : ord_in ? ord_in[i] : ord_base + i;  // heartbeats carry no event ordinal
-    ev_clock[i] = playback ? clock : clock_in;
+    ev_clock[i] = playback ? (t > before ? t : before) : clock_in;
     adv_flag[i] = adv;
   }
 }
 
 __global__ void advance_points_kernel(const uint8_t* __restrict__ flag, const uint32_t* __restrict__ excl, int64_t n,
                                       const int64_t* __restrict__ ts, int64_t* __restrict__ adv_pos,
-                                      int64_t* __restrict__ adv_clock, int64_t* __restrict__ adv_wall) {
+                                      int64_t* __restrict__ adv_clock, int64_t* __restrict__ adv_wall,
+                                      int64_t* __restrict__ adv_upto) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !flag[i]) return;
+  if (i >= n) return;
   uint32_t o = excl[i];
+  adv_upto[i] = (int64_t)o + flag[i];
+  if (!flag[i]) return;
   adv_pos[o] = i;
   adv_clock[o] = ts[i];
   adv_wall[o] = -1;
@@ -629,10 +633,9 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
   uint32_t* sk2 = (uint32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
   uint32_t* si = (uint32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
   uint32_t* si2 = (uint32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
-  if (n > 0) hipLaunchKernelGGL(slot_to_u32_kernel, grid_for(n), dim3(256), 0, s, slot, n, sk, si);
-  int bits = 0;
-  while (bits < 32 && ((uint64_t)0xffffffffu >> bits) != 0 && (((uint64_t)T.nslots + 1) >> bits) != 0) ++bits;
-  bits = 32;  // -2 (invalid) maps to 0xfffffffe: keep all 32 bits so invalid records sort last
+  if (n > 0) hipLaunchKernelGGL(slot_to_u32_kernel, grid_for(n), dim3(256), 0, s, slot, n, (uint32_t)T.nslots, sk, si);
+  int bits = 0;  // sort keys are 0 .. nslots: only their significant bits take radix passes
+  while (bits < 32 && ((uint64_t)T.nslots >> bits) != 0) ++bits;
   bool alt = radix_sort_pairs<uint32_t>(sk, sk2, si, si2, n, 0, bits, sc, s);
   if (alt) {
     std::swap(sk, sk2);
@@ -660,7 +663,7 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
 int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const int64_t* ts, const int64_t* ord_in,
                           int64_t ord_base, bool playback, int64_t clock_in, int64_t* ev_row, int64_t* ev_ord,
                           int64_t* ev_clock, int64_t* adv_pos, int64_t* adv_clock, int64_t* adv_wall,
-                          int64_t* clock_out, Scratch& sc, hipStream_t s) {
+                          int64_t* adv_upto, int64_t* clock_out, Scratch& sc, hipStream_t s) {
   *clock_out = clock_in;
   if (n == 0) return 0;
   if (n >= (int64_t)UINT32_MAX) throw std::runtime_error("device event batch too large (>= 2^32 events)");
@@ -678,11 +681,12 @@ int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const
   hipLaunchKernelGGL(event_index_kernel, dim3((unsigned)ntiles), dim3(kIxThreads), 0, s, sid, nstreams, ts, n, ord_in,
                      ord_base, (int)playback, clock_in, tile_max, ev_row, ev_ord, ev_clock, flag, bad);
   int64_t nadv = 0;
+  if (!playback) SM_HIP(hipMemsetAsync(adv_upto, 0, (size_t)n * 8, s));
   if (playback) {
     hipLaunchKernelGGL(u8_to_u32_kernel, grid_for(n), dim3(256), 0, s, flag, n, ex);
     exclusive_scan_u32(ex, n, sc, s, total);
     hipLaunchKernelGGL(advance_points_kernel, grid_for(n), dim3(256), 0, s, flag, ex, n, ts, adv_pos, adv_clock,
-                       adv_wall);
+                       adv_wall, adv_upto);
     uint32_t h = 0;
     SM_HIP(hipMemcpyAsync(&h, total, 4, hipMemcpyDeviceToHost, s));
     nadv = h;

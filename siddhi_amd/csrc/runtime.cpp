@@ -193,7 +193,8 @@ struct sm_app {
   std::map<std::string, std::vector<std::string>> collected_streams;  // JSON fragments
   std::map<std::string, std::vector<std::string>> collected_queries;
   hipStream_t stream = nullptr;
-  sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_ev_ord, d_adv_pos, d_adv_clock, d_adv_wall, d_streams, d_err, d_count,
+  sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_ev_ord, d_adv_pos, d_adv_clock, d_adv_wall, d_adv_upto, d_streams,
+      d_err, d_count,
       d_keyoff, scratch;
   sm::Scratch sc;
 };
@@ -484,6 +485,7 @@ struct EvArrays {
   const int64_t* adv_pos;
   const int64_t* adv_clock;
   const int64_t* adv_wall;
+  const int64_t* adv_upto;  // per position: advance points at positions <= it
   int64_t nadv;
   int64_t clock_in;
 };
@@ -532,6 +534,7 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.adv_pos = ev.adv_pos;
   b.adv_clock = ev.adv_clock;
   b.adv_wall = ev.adv_wall;
+  b.adv_upto = ev.adv_upto;
   b.nadv = ev.nadv;
   b.clock_in = ev.clock_in;
   b.key_off = key_off;
@@ -594,6 +597,15 @@ void flush(sm_app* a) {
   upload(a, a->d_adv_pos, a->adv_pos);
   upload(a, a->d_adv_clock, a->adv_clock);
   upload(a, a->d_adv_wall, a->adv_wall);
+  {
+    std::vector<int64_t> upto(N);
+    size_t j = 0;
+    for (int64_t p = 0; p < N; ++p) {
+      while (j < a->adv_pos.size() && a->adv_pos[j] <= p) ++j;
+      upto[p] = (int64_t)j;
+    }
+    upload(a, a->d_adv_upto, upto);
+  }
   a->d_err.ensure(16);
   a->d_count.ensure(16);
   ensure_scratch(a, (size_t)N * 96 + (64 << 20));
@@ -601,7 +613,7 @@ void flush(sm_app* a) {
   const EvArrays ev{(const int32_t*)a->d_ev_stream.p, (const int64_t*)a->d_ev_row.p, (const int64_t*)a->d_ev_ts.p,
                     (const int64_t*)a->d_ev_clock.p, (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p,
                     (const int64_t*)a->d_adv_pos.p, (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p,
-                    (int64_t)a->adv_pos.size(), a->clock_batch_in};
+                    (const int64_t*)a->d_adv_upto.p, (int64_t)a->adv_pos.size(), a->clock_batch_in};
   for (size_t qi = 0; qi < a->queries.size(); ++qi) {
     QueryRt& q = *a->queries[qi];
     const DQuery& h = q.cq.hdr;
@@ -1098,7 +1110,8 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
     a->d_streams.ensure(nst.size() * sizeof(NfaStream));
     SM_HIP(hipMemcpyAsync(a->d_streams.p, nst.data(), nst.size() * sizeof(NfaStream), hipMemcpyHostToDevice, hs));
     const int64_t N = (int64_t)n;
-    for (DBuf* d : {&a->d_ev_row, &a->d_ev_clock, &a->d_ev_ord, &a->d_adv_pos, &a->d_adv_clock, &a->d_adv_wall})
+    for (DBuf* d : {&a->d_ev_row, &a->d_ev_clock, &a->d_ev_ord, &a->d_adv_pos, &a->d_adv_clock, &a->d_adv_wall,
+                    &a->d_adv_upto})
       d->ensure((size_t)N * 8);
     a->d_err.ensure(16);
     a->d_count.ensure(16);
@@ -1113,11 +1126,12 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
     const int64_t nadv = build_event_index(
         N, d_stream_idx, (int32_t)a->streams.size(), d_ts, d_ordinals, ordinal_base, a->ast.playback, a->clock, (int64_t*)a->d_ev_row.p, (int64_t*)a->d_ev_ord.p,
         (int64_t*)a->d_ev_clock.p, (int64_t*)a->d_adv_pos.p, (int64_t*)a->d_adv_clock.p, (int64_t*)a->d_adv_wall.p,
-        &clock_out, a->sc, hs);
+        (int64_t*)a->d_adv_upto.p, &clock_out, a->sc, hs);
     if (tm) tm->mark("event_index", hs);
     const EvArrays ev{d_stream_idx, (const int64_t*)a->d_ev_row.p, d_ts, (const int64_t*)a->d_ev_clock.p,
                       (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p, (const int64_t*)a->d_adv_pos.p,
-                      (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p, nadv, a->clock};
+                      (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p, (const int64_t*)a->d_adv_upto.p,
+                      nadv, a->clock};
     std::vector<HostOut> outs;
     for (size_t qi = 0; qi < a->queries.size(); ++qi) {
       a->sc.used = 0;
