@@ -411,9 +411,25 @@ def roofline(ktot, n, m, steps, config):
     ach = per_launch / (avg_ms * 1e-3)
     brk = {k: {"avg_ms": v[0] / v[1], "calls_per_step": v[1] / steps,
                "gbps": alg_bytes(k, n, m, config) / (v[0] / v[1] * 1e-3) / 1e9} for k, v in ktot.items()}
+    traffic, src = pmc_traffic(config, n, dom)
     return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
-            "traffic": None, "kernel": dom, "avg_launch_ms": avg_ms, "alg_bytes_per_launch": per_launch,
-            "breakdown": brk}
+            "traffic": traffic, "traffic_unit": "HBM bytes per launch", "traffic_source": src,
+            "kernel": dom, "avg_launch_ms": avg_ms, "alg_bytes_per_launch": per_launch, "breakdown": brk}
+
+
+def pmc_traffic(config, n, label):
+    """HBM bytes per launch of `label` from the committed PMC summary of this configuration
+    (profiles/pmc_config<C>.json, written by tools/summarize_profile.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench at the same event count), else None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    try:
+        doc = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    ent = doc.get("labels", {}).get(label)
+    if doc.get("events") != n or not ent or not ent.get("hbm_bytes"):
+        return None, None
+    return ent["hbm_bytes"], f"profiles/pmc_config{config}.json ({doc.get('tag')}: {doc.get('method')})"
 
 
 if __name__ == "__main__":

@@ -1,23 +1,38 @@
-"""Condense a tools/round_profile.sh run (gpurun_out/) into a committed profile summary:
-per-kernel rocprofv3 --stats (calls, average duration) and, per launch, FETCH_SIZE x2 (gfx950 wide-read
-correction, MI355X_MICROARCH.md HBM section) and WRITE_SIZE from separate PMC passes, next to the algorithmic
-bytes bench.py prices each kernel at. Usage: python tools/summarize_profile.py <tag> [events]"""
+"""Condense a tools/round_profile.sh run (gpurun_out/) into committed profile files:
+
+  profiles/<tag>.md            per-kernel rocprofv3 --stats (calls, average duration), the bench's own HIP-event
+                               average for the same kernel, and per launch the HBM bytes from the PMC passes
+  profiles/pmc_config<C>.json  per bench kernel label: HBM read / write bytes per launch (bench.py reports the
+                               dominant kernel's sum as roofline.traffic)
+
+HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE come from separate rocprofv3 --pmc
+runs; FETCH_SIZE is doubled (gfx950 tallies 128-B requests of wide streaming reads at 64 B), WRITE_SIZE is taken as
+reported; both are KB (x 1024). Usage: python tools/summarize_profile.py <tag> [config]"""
 import csv
+import glob
 import json
 import os
 import re
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 from bench import alg_bytes  # noqa: E402
 
-OUT = "gpurun_out"
-FAMILIES = [("walk_kernel<true", "walk"), ("walk_kernel<false", "walk"),
-            ("downsweep_kernel<0", "key_pass0"), ("downsweep_kernel<1", "key_pass"),
-            ("downsweep_kernel<2", "j_pass*"), ("upsweep_kernel<sm::(anonymous namespace)::KeyColDigits", "key_up"),
+OUT = os.path.join(ROOT, "gpurun_out")
+# kernel-name fragment -> bench label (first match wins)
+FAMILIES = [("walk_kernel<", "walk"), ("downsweep_wc_kernel<0", "key_pass0"), ("downsweep_kernel<0", "key_pass0"),
+            ("downsweep_wc_kernel<1", "key_pass"), ("downsweep_kernel<1", "key_pass"),
+            ("downsweep_wc_kernel<2", "j_pass*"), ("downsweep_kernel<2", "j_pass*"),
+            ("upsweep_kernel<sm::(anonymous namespace)::KeyColDigits", "key_up"),
             ("upsweep_kernel<sm::(anonymous namespace)::RecDigits", "key_up"),
-            ("upsweep_kernel<sm::(anonymous namespace)::PairDigits", "j_up"), ("c1_mask_kernel", "c1_mask"),
-            ("prep_kernel", "prep"), ("scan_chunks_kernel", "scan"), ("digit_base_kernel", "scan")]
+            ("upsweep_kernel<sm::(anonymous namespace)::PairDigits", "j_up"), ("prep_kernel", "prep"),
+            ("scan_chunks_kernel", "scan"), ("digit_base_kernel", "scan"),
+            ("filter_count", "filter_count"), ("filter_write", "filter_write"), ("filter_block_scan", "filter_scan"),
+            ("nfa_kernel", "nfa"), ("event_index_kernel", "event_index"), ("ts_tile_max_kernel", "event_index"),
+            ("tile_prefix_max_kernel", "event_index"), ("advance_points_kernel", "event_index"),
+            ("select_records_kernel", "nfa_select"), ("key_eval_kernel", "nfa_group"),
+            ("table_lookup_kernel", "nfa_group"), ("rs_upsweep", "nfa_group"), ("rs_downsweep", "nfa_group")]
 
 
 def family(name):
@@ -32,53 +47,76 @@ def short(name):
     return n.split("(")[0][:90]
 
 
+def csv_in(sub, suffix):
+    hits = sorted(glob.glob(os.path.join(OUT, sub, "**", f"*{suffix}"), recursive=True))
+    return hits[0] if hits else None
+
+
 def main():
     tag = sys.argv[1]
+    config = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     bench = None
     for l in open(os.path.join(OUT, "bench_full.log")):
         if l.startswith("{"):
             bench = json.loads(l)
     n = bench["config"]["events"]
     m = bench["config"]["matches"]
-    lines = [f"# rocprofv3 summary — {tag}", "",
-             f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu --steps 3 --warmup 1` "
-             f"(config 4: N = {n}, K = {bench['config']['keys']}, M = {m} matches), MI355X.",
-             "PMC: separate `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of `bench.py --no-cpu --steps 1 "
-             "--warmup 0` (one launch per kernel). FETCH_SIZE is doubled (gfx950 reports half the bytes of wide "
-             "streaming reads), WRITE_SIZE as reported (KB x 1024).", "",
-             "| kernel | calls | avg ms (rocprof) | avg ms (bench HIP events) | alg GB/launch | HBM read GB | "
-             "HBM write GB | alg GB/s |",
-             "|---|---|---|---|---|---|---|---|"]
+    brk = bench["roofline"]["breakdown"]
+    # PMC passes: one step, no warmup -> calls_per_step launches per label
     pmc = {}
     for kind in ("fetch", "write"):
-        p = os.path.join(OUT, f"pmc_{kind}", "run_counter_collection.csv")
-        if not os.path.exists(p):
+        p = csv_in(f"pmc_{kind}", "counter_collection.csv")
+        if not p:
             continue
         for r in csv.DictReader(open(p)):
-            fam = family(r["Kernel_Name"])
-            if fam:
-                key = (short(r["Kernel_Name"]), r["Counter_Name"])
-                pmc[key] = pmc.get(key, 0.0) + float(r["Counter_Value"])
-    brk = bench["roofline"]["breakdown"]
-    for r in csv.DictReader(open(os.path.join(OUT, "prof_stats", "run_kernel_stats.csv"))):
+            nm = short(r["Kernel_Name"])
+            key = (nm, r["Counter_Name"])
+            pmc[key] = pmc.get(key, 0.0) + float(r["Counter_Value"])
+    lines = [f"# rocprofv3 summary — {tag}", "",
+             f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --config {config} --no-cpu --steps 3 "
+             f"--warmup 1` (N = {n}, M = {m} matches), MI355X.",
+             f"PMC: separate `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of `bench.py --config {config} "
+             "--no-cpu --steps 1 --warmup 0`. FETCH_SIZE is doubled (gfx950 reports half the bytes of wide streaming "
+             "reads), WRITE_SIZE as reported (KB x 1024). Bytes per launch.", "",
+             "| kernel | label | calls | avg ms (rocprof) | avg ms (bench HIP events) | alg GB/launch | HBM read GB | "
+             "HBM write GB | alg GB/s |",
+             "|---|---|---|---|---|---|---|---|---|"]
+    traffic = {}
+    stats = csv_in("prof_stats", "kernel_stats.csv")
+    for r in csv.DictReader(open(stats)):
         fam = family(r["Name"])
         if not fam:
             continue
         nm = short(r["Name"])
         avg = float(r["AverageNs"]) / 1e6
         labs = ["j_pass", "j_pass_last"] if fam == "j_pass*" else [fam]
-        ev = "/".join(f"{brk[l]['avg_ms']:.3f}" for l in labs if l in brk)
-        alg = alg_bytes(labs[0], n, m) / 1e9 if labs[0] in brk or labs[0] in ("scan",) else 0
+        labs = [l for l in labs if l in brk]
+        ev = "/".join(f"{brk[l]['avg_ms']:.3f}" for l in labs)
+        alg = alg_bytes(labs[0], n, m, config) / 1e9 if labs else 0.0
+        calls1 = max(1, round(sum(brk[l]["calls_per_step"] for l in labs))) if labs else 1
         fetch = pmc.get((nm, "FETCH_SIZE"))
         write = pmc.get((nm, "WRITE_SIZE"))
-        calls1 = {"key_up": 2, "j_up": 2, "scan": 5, "j_pass*": 3}.get(fam, 1)  # launches in the 1-step PMC run
-        rd = f"{2 * fetch * 1024 / calls1 / 1e9:.2f}" if fetch else "-"
-        wr = f"{write * 1024 / calls1 / 1e9:.2f}" if write else "-"
-        lines.append(f"| `{nm}` | {r['Calls']} | {avg:.3f} | {ev} | {alg:.2f} | {rd} | {wr} | "
+        rd = 2 * fetch * 1024 / calls1 if fetch is not None else None
+        wr = write * 1024 / calls1 if write is not None else None
+        for l in labs:
+            t = traffic.setdefault(l, {"read_bytes": 0.0, "write_bytes": 0.0, "kernels": []})
+            t["read_bytes"] += rd or 0.0
+            t["write_bytes"] += wr or 0.0
+            t["kernels"].append(nm)
+        lines.append(f"| `{nm}` | {fam} | {r['Calls']} | {avg:.3f} | {ev or '-'} | {alg:.2f} | "
+                     f"{rd / 1e9 if rd is not None else float('nan'):.2f} | "
+                     f"{wr / 1e9 if wr is not None else float('nan'):.2f} | "
                      f"{alg / (avg * 1e-3) if avg else 0:.0f} |")
     lines += ["", "bench line:", "", "```", json.dumps(bench), "```"]
-    path = os.path.join("profiles", f"{tag}.md")
-    open(path, "w").write("\n".join(lines) + "\n")
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    open(os.path.join(ROOT, "profiles", f"{tag}.md"), "w").write("\n".join(lines) + "\n")
+    doc = {"config": config, "events": n, "matches": m, "tag": tag,
+           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction) and --pmc WRITE_SIZE, separate "
+                     "passes, 1 step; bytes per launch",
+           "labels": {k: {"read_bytes": v["read_bytes"], "write_bytes": v["write_bytes"],
+                          "hbm_bytes": v["read_bytes"] + v["write_bytes"], "kernels": v["kernels"]}
+                      for k, v in traffic.items()}}
+    json.dump(doc, open(os.path.join(ROOT, "profiles", f"pmc_config{config}.json"), "w"), indent=1)
     print("\n".join(lines[:40]))
 
 
