@@ -1,6 +1,4 @@
 // HIP launch wrapper of the NFA interpreter (implementation in nfa_impl.h).
-#include <cstdlib>
-
 #include "nfa_impl.h"
 
 namespace sm {
@@ -13,16 +11,6 @@ __global__ void nfa_kernel(NfaBatch b, const char* __restrict__ blob, int64_t* k
   nfa_lane(b, blob, ks_all, heap_all, heap_half, key, err_out);
 }
 
-// Same lane program with a 64-thread launch bound: the compiler may then use the whole register file of a wave
-// (no VGPR spills) at half the resident waves per SIMD.
-__global__ __launch_bounds__(64) void nfa_kernel_wide(NfaBatch b, const char* __restrict__ blob, int64_t* ks_all,
-                                                      int64_t* heap_all, int32_t heap_half, int32_t nkeys,
-                                                      int32_t* err_out) {
-  int key = blockIdx.x * blockDim.x + threadIdx.x;
-  if (key >= nkeys) return;
-  nfa_lane(b, blob, ks_all, heap_all, heap_half, key, err_out);
-}
-
 }  // namespace
 
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half,
@@ -30,16 +18,7 @@ void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* h
   if (nkeys <= 0) return;
   int threads = 64;
   int blocks = (nkeys + threads - 1) / threads;
-  static const int variant = [] {
-    const char* e = getenv("SIDDHI_AMD_NFA_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  if (variant == 1)
-    hipLaunchKernelGGL(nfa_kernel_wide, dim3(blocks), dim3(threads), 0, s, b, blob_dev, ks, heap, heap_half, nkeys,
-                       err_dev);
-  else
-    hipLaunchKernelGGL(nfa_kernel, dim3(blocks), dim3(threads), 0, s, b, blob_dev, ks, heap, heap_half, nkeys,
-                       err_dev);
+  hipLaunchKernelGGL(nfa_kernel, dim3(blocks), dim3(threads), 0, s, b, blob_dev, ks, heap, heap_half, nkeys, err_dev);
 }
 
 }  // namespace sm

@@ -194,29 +194,43 @@ __global__ void key_eval_kernel(const int64_t* __restrict__ pos, int64_t n, cons
   }
 }
 
-__global__ void table_lookup_kernel(const int64_t* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t n,
-                                    const int64_t* __restrict__ tkeys, const int32_t* __restrict__ tslots,
-                                    uint64_t mask, int32_t* __restrict__ slot_out, uint32_t* __restrict__ nmissing) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (valid && !valid[i]) {
-    slot_out[i] = -2;
-    return;
+// Grid-stride lookup; misses are counted per workgroup and added once per workgroup (a batch of new keys
+// misses on every record, and atomics on one address serialise in the L2 even when a wave coalesces them).
+__global__ __launch_bounds__(256) void table_lookup_kernel(const int64_t* __restrict__ keys,
+                                                           const uint8_t* __restrict__ valid, int64_t n,
+                                                           const int64_t* __restrict__ tkeys,
+                                                           const int32_t* __restrict__ tslots, uint64_t mask,
+                                                           int32_t* __restrict__ slot_out,
+                                                           uint32_t* __restrict__ nmissing) {
+  __shared__ uint32_t wmiss[4];
+  uint32_t miss = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) {
+      slot_out[i] = -2;
+      continue;
+    }
+    int64_t k = keys[i];
+    uint64_t h = mix64((uint64_t)k) & mask;
+    for (;;) {
+      int32_t s = tslots[h];
+      if (s == 0) {
+        slot_out[i] = -1;
+        ++miss;
+        break;
+      }
+      if (tkeys[h] == k) {
+        slot_out[i] = s - 1;
+        break;
+      }
+      h = (h + 1) & mask;
+    }
   }
-  int64_t k = keys[i];
-  uint64_t h = mix64((uint64_t)k) & mask;
-  for (;;) {
-    int32_t s = tslots[h];
-    if (s == 0) {
-      slot_out[i] = -1;
-      atomicAdd(nmissing, 1u);
-      return;
-    }
-    if (tkeys[h] == k) {
-      slot_out[i] = s - 1;
-      return;
-    }
-    h = (h + 1) & mask;
+  for (int o = 32; o > 0; o >>= 1) miss += __shfl_xor(miss, o, 64);
+  if ((threadIdx.x & 63) == 0) wmiss[threadIdx.x >> 6] = miss;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = wmiss[0] + wmiss[1] + wmiss[2] + wmiss[3];
+    if (t) atomicAdd(nmissing, t);
   }
 }
 
@@ -275,12 +289,26 @@ __global__ void assign_new_slots_kernel(const uint64_t* __restrict__ sk, const u
   uint32_t run = run_excl[i] + (start ? 1u : 0u) - 1u;  // inclusive count - 1
   int32_t slot = base + (int32_t)run;
   uint32_t m = sidx[i];  // index into the missing list
-  slot_out[missing_map[m]] = slot;
+  if (slot_out) slot_out[missing_map[m]] = slot;
   if (start) {
     new_keys[run] = keys_of_missing[m];
     new_slots[run] = slot;
     slot_keys[slot] = keys_of_missing[m];
   }
+}
+
+// every record of the batch carried a new key: the key-sorted missing list already is the per-slot grouping
+// (slots were numbered in key order from `base`), so it becomes key_pos / key_off directly
+__global__ void all_new_csr_kernel(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sidx,
+                                   const uint32_t* __restrict__ run_excl, const uint32_t* __restrict__ missing_map,
+                                   const int64_t* __restrict__ pos, int64_t n, int32_t base,
+                                   int64_t* __restrict__ key_pos, int64_t* __restrict__ key_off) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  key_pos[j] = pos[missing_map[sidx[j]]];
+  const bool start = (j == 0 || sk[j] != sk[j - 1]);
+  if (start) key_off[base + run_excl[j]] = j;
+  if (j == n - 1) key_off[base + run_excl[j] + (start ? 1 : 0)] = n;  // one past the last run
 }
 
 template <typename T>
@@ -326,10 +354,20 @@ __global__ void u32_to_i64_kernel(const uint32_t* __restrict__ a, int64_t n, int
   if (i < n) o[i] = a[i];
 }
 
+// sk is sorted: equal slots are adjacent, so each run inside a wave adds its length with one atomic
 __global__ void count_valid_slots_kernel(const uint32_t* __restrict__ sk, int64_t n, uint32_t nslots,
                                          uint32_t* __restrict__ counts) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && sk[i] < nslots) atomicAdd(&counts[sk[i]], 1u);
+  const int lane = threadIdx.x & 63;
+  const uint32_t key = i < n ? sk[i] : 0xffffffffu;
+  const uint32_t prev = __shfl_up(key, 1, 64);
+  const bool head = i < n && (lane == 0 || prev != key);
+  const uint64_t heads = __ballot(head || i >= n);
+  if (head && key < nslots) {
+    const uint64_t after = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+    const int next = after ? __ffsll((unsigned long long)after) - 1 : 64;
+    atomicAdd(&counts[key], (uint32_t)(next - lane));
+  }
 }
 
 __global__ void gather_pos_kernel(const int64_t* __restrict__ pos, const uint32_t* __restrict__ si, int64_t n,
@@ -573,13 +611,18 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
                        nprogs, keys, valid);
   SM_HIP(hipMemsetAsync(nmiss, 0, 4, s));
   if (n > 0)
-    hipLaunchKernelGGL(table_lookup_kernel, grid_for(n), dim3(256), 0, s, keys, valid, n, T.tkeys, T.tslots, T.mask,
+    hipLaunchKernelGGL(table_lookup_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
+                       keys, valid, n, T.tkeys, T.tslots, T.mask,
                        slot, nmiss);
   uint32_t hm = 0;
   SM_HIP(hipMemcpyAsync(&hm, nmiss, 4, hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));
   if (hm > 0) {
     // new keys: compact, sort by key (stable → first occurrence first), one new slot per distinct key
+    const bool all_new = (int64_t)hm == n;
+    const int32_t base = T.nslots;
+    int64_t* fast_pos = all_new ? (int64_t*)sc.take((size_t)n * 8) : nullptr;
+    int64_t* fast_off = all_new ? (int64_t*)sc.take(((size_t)base + hm + 2) * 8) : nullptr;
     size_t mark = sc.used;
     uint8_t* f = (uint8_t*)sc.take(n);
     uint32_t* ex = (uint32_t*)sc.take(n * 4);
@@ -622,10 +665,19 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
     int64_t* nk = (int64_t*)sc.take(hr * 8);
     int32_t* ns = (int32_t*)sc.take(hr * 4);
     hipLaunchKernelGGL(assign_new_slots_kernel, grid_for(hm), dim3(256), 0, s, sk, si, runs, (int64_t)hm, T.nslots,
-                       mkeys, miss, slot, nk, ns, T.slot_keys);
+                       mkeys, miss, all_new ? nullptr : slot, nk, ns, T.slot_keys);
     hipLaunchKernelGGL(table_insert_kernel, grid_for(hr), dim3(256), 0, s, nk, ns, (int64_t)hr, T.tkeys, T.tslots,
                        T.mask);
     T.nslots += hr;
+    if (all_new) {
+      SM_HIP(hipMemsetAsync(fast_off, 0, ((size_t)base + 1) * 8, s));
+      hipLaunchKernelGGL(all_new_csr_kernel, grid_for(hm), dim3(256), 0, s, sk, si, runs, miss, pos, (int64_t)hm, base,
+                         fast_pos, fast_off);
+      sc.used = mark;
+      *key_pos_out = fast_pos;
+      *key_off_out = fast_off;
+      return hm;
+    }
     sc.used = mark;
   }
   // stable group by slot: sort (slot, record index) pairs; invalid records (-2) sort last and are dropped

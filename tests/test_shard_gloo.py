@@ -92,3 +92,80 @@ def test_merge_keeps_same_trigger_order():
     a = [[1, 5], [0, 5], [2, 9]]
     b = [[3, 4], [4, 7]]
     np.testing.assert_array_equal(merge_matches([a, b]), [[3, 4], [1, 5], [0, 5], [4, 7], [2, 9]])
+
+
+# ---- config 5 (five streams, playback timers): key exchange + global clock-advance heartbeats (bench.py
+# clock_ticks / merge_ticks) must reproduce every output of the single-process run, with the same timestamps,
+# and each rank's outputs in the global relative order.
+N5, K5 = 20000, 400
+BODIES5 = ["every e1=A -> e2=B[price>e1.price]<2:5> -> (e3=C or e4=D) -> not E for 1 sec",
+           "every e1=A, e2=B[price>e1.price]<1:3>, (e3=C or e4=D), not E for 1 sec"]
+
+
+def replay5(text, sid, ts, cols):
+    """Oracle over a rank's merged sequence: events (stream >= 0) and heartbeats (-1 -> advance_time)."""
+    a = OracleApp(text)
+    a.start()
+    i, n = 0, len(ts)
+    while i < n:
+        if sid[i] < 0:
+            a.advance_time(int(ts[i]))
+            i += 1
+            continue
+        j = i
+        while j < n and sid[j] >= 0:
+            j += 1
+        a.send_interleaved(sid[i:j], ts[i:j], [c[i:j] for c in cols])
+        i = j
+    a.flush()
+    out = a.outputs()["streams"].get("Out", [])
+    a.close()
+    return [[r[0], r[1]] for r in out]
+
+
+def _worker5(rank, world, port, outfile, body):
+    from bench import clock_ticks, merge_ticks
+    from siddhi_amd.shard import exchange_by_key
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = N5 * rank // world, N5 * (rank + 1) // world
+        sid, cols, ts = synth.gen5(lo, hi, K5, 1)
+        t = [torch.from_numpy(np.ascontiguousarray(x)) for x in cols]
+        tts = torch.from_numpy(ts)
+        tsid = torch.from_numpy(sid)
+        ords = torch.arange(lo, hi, dtype=torch.int64)
+        ticks = clock_ticks(tts, lo, world)
+        (r_sym, r_price, r_vol, r_tsa, r_ts, r_ord, r_sid), _ = exchange_by_key(t[0], t + [tts, ords, tsid], world)
+        m_sid, m_ts, m_cols, m_ord = merge_ticks(r_sid, r_ts, [r_sym, r_price, r_vol, r_tsa], r_ord, ticks)
+        assert (np.diff(m_ts.numpy()) >= 0).all()
+        local = replay5(synth.app5(body), m_sid.numpy(), m_ts.numpy(), [c.numpy() for c in m_cols])
+        parts = [None] * world
+        dist.all_gather_object(parts, local)
+        if rank == 0:
+            with open(outfile, "w") as f:
+                json.dump(parts, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("body", BODIES5)
+def test_config5_sharded_with_heartbeats_equal_single_process(world, body, tmp_path):
+    out = str(tmp_path / "parts5.json")
+    mp.start_processes(_worker5, args=(world, _free_port(), out, body), nprocs=world, join=True,
+                       start_method="spawn")
+    parts = json.load(open(out))
+    sid, cols, ts = synth.gen5(0, N5, K5, 1)
+    full = replay5(synth.app5(body), sid, ts, cols)
+    assert len(full) > 30
+    key = lambda r: json.dumps(r)  # noqa: E731
+    assert sorted(map(key, full)) == sorted(key(r) for p in parts for r in p)
+    pos = {}
+    for k, r in enumerate(full):
+        pos.setdefault(key(r), []).append(k)
+    for p in parts:
+        idx = [pos[key(r)].pop(0) for r in p]
+        assert idx == sorted(idx), "a rank's outputs are out of the global order"
