@@ -38,7 +38,28 @@ struct Emitter {
   // collects VAR positions (for parity refs)
   std::vector<std::pair<int, int>>* var_refs = nullptr;
 
+  // operand-stack slots the device evaluator (kernels/expr.h eval_prog) needs for x: a binary node keeps its
+  // left value while the right operand is evaluated
+  static int stack_need(const Expr& x) {
+    if (x.ch.empty()) return 1;
+    if (x.ch.size() == 1) return stack_need(*x.ch[0]);
+    return std::max(stack_need(*x.ch[0]), 1 + stack_need(*x.ch[1]));
+  }
+
+  int level = 0;
   int emit(const Expr& x) {  // returns result type
+    if (level == 0 && stack_need(x) > kMaxStack)
+      throw UnsupportedError("expression nests deeper than the device evaluator's " + std::to_string(kMaxStack) +
+                             "-entry operand stack");
+    ++level;
+    struct Leave {
+      int& l;
+      ~Leave() { --l; }
+    } leave{level};
+    return emit_node(x);
+  }
+
+  int emit_node(const Expr& x) {
     Instr in{};
     switch (x.kind) {
       case ExprKind::CONST: {

@@ -12,9 +12,13 @@
 
 namespace sm {
 
+// One operand: integer-typed values live in i, FLOAT / DOUBLE ones in d (the instruction's static types pick
+// the member, see do_compare / do_math), so the two share storage and an operand is 16 bytes.
 struct StackVal {
-  int64_t i;
-  double d;
+  union {
+    int64_t i;
+    double d;
+  };
   int null;
 };
 
@@ -162,8 +166,8 @@ __device__ StackVal eval_prog(const Instr* code, int len, const DVal* consts, co
     switch (in.op) {
       case OP_CONST: {
         const DVal c = consts[in.a];
-        st[sp].i = c.i;
-        st[sp].d = c.d;
+        if (in.t0 == T_FLOAT || in.t0 == T_DOUBLE) st[sp].d = c.d;
+        else st[sp].i = c.i;
         st[sp].null = c.null;
         ++sp;
         break;

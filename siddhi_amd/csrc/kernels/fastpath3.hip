@@ -167,13 +167,8 @@ __device__ __forceinline__ uint64_t canon(const StackVal& v, int type) {
 __device__ __forceinline__ StackVal uncanon(uint64_t bits, int type) {
   StackVal v;
   v.null = 0;
-  if (type == T_FLOAT || type == T_DOUBLE) {
-    v.d = __longlong_as_double((long long)bits);
-    v.i = 0;
-  } else {
-    v.i = (int64_t)bits;
-    v.d = 0;
-  }
+  if (type == T_FLOAT || type == T_DOUBLE) v.d = __longlong_as_double((long long)bits);
+  else v.i = (int64_t)bits;
   return v;
 }
 

@@ -362,13 +362,12 @@ struct Lane {
   // a static stack.
   __device__ void addState(int p0, int32_t r) {
     enum { ACT_ADD = 0, ACT_MIN = 1, ACT_EVERY = 2 };
-    int act[3 * kMaxSlots + 4], arg[3 * kMaxSlots + 4];
+    uint16_t work[3 * kMaxSlots + 4];  // (processor index << 2) | action: a small per-lane (scratch) stack
     int sp = 0;
-    act[sp] = ACT_ADD;
-    arg[sp++] = p0;
+    work[sp++] = (uint16_t)(p0 << 2 | ACT_ADD);
     while (sp > 0) {
       --sp;
-      const int a = act[sp], p = arg[sp];
+      const int a = work[sp] & 3, p = work[sp] >> 2;
       if (a == ACT_EVERY) {
         addEveryState(p, r);
         continue;
@@ -383,14 +382,8 @@ struct Lane {
           err |= NFA_ERR_NPE;
           return;
         }
-        if (O.nextEveryPre >= 0) {
-          act[sp] = ACT_EVERY;
-          arg[sp++] = O.nextEveryPre;
-        }
-        if (O.nextPre >= 0) {
-          act[sp] = ACT_ADD;
-          arg[sp++] = O.nextPre;
-        }
+        if (O.nextEveryPre >= 0) work[sp++] = (uint16_t)(O.nextEveryPre << 2 | ACT_EVERY);
+        if (O.nextPre >= 0) work[sp++] = (uint16_t)(O.nextPre << 2 | ACT_ADD);
         continue;
       }
       const DPre& P = pre[p];
@@ -409,8 +402,7 @@ struct Lane {
             lappend(p, 1, r);
           }
           if (P.minCount == 0 && slot(r, P.stateId) < 0) {
-            act[sp] = ACT_MIN;
-            arg[sp++] = P.post;
+            work[sp++] = (uint16_t)(P.post << 2 | ACT_MIN);
           }
           break;
         case PK_LOGICAL:

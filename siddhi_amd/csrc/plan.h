@@ -52,7 +52,7 @@ struct Instr {
   int32_t a, b, c;
 };
 
-constexpr int kMaxStack = 16;
+constexpr int kMaxStack = 8;  // device operand stack (per lane, scratch): compiler rejects deeper expressions
 constexpr int kMaxSlots = 16;
 constexpr int kMaxProcs = 8;
 

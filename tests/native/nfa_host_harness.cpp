@@ -80,7 +80,7 @@ struct HostColLoader {
   const NfaStream* st;
   int64_t row;
   StackVal var(const Instr& in) const {
-    StackVal v{0, 0, 0};
+    StackVal v{};
     int a = in.a;
     if (st->nulls[a] && st->nulls[a][row]) {
       v.null = 1;
