@@ -46,7 +46,8 @@ struct NfaBatch {
   uint32_t out_stride;
 };
 
-void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int32_t nkeys,
-                int32_t* err_dev, hipStream_t s);
+// ks is lane-interleaved: word w of key k at [w * lanes + k] (lanes = allocated key capacity); heap is key-major
+void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
+                int32_t nkeys, int32_t* err_dev, hipStream_t s);
 
 }  // namespace sm

@@ -28,6 +28,17 @@ struct StateLoader {  // OP_VAR loads for a run record
   __device__ StackVal var(const Instr& in) const;
 };
 
+// The words of one lane inside a lane-interleaved allocation (structure of arrays across lanes): word w of lane k
+// lives at base[w * lanes + k]. The 64 lanes of a wave that touch the same per-key state word (list heads,
+// flags, timer queues: fixed offsets) then share cache lines instead of each pulling its own line.
+// stride 1 = the plain key-major layout (the heap).
+struct LaneWords {
+  int64_t* p;      // &base[lane]
+  int64_t stride;  // lanes per word row
+  __device__ __forceinline__ int64_t& operator[](int64_t w) const { return p[w * stride]; }
+  __device__ __forceinline__ LaneWords at(int64_t w) const { return {p + w * stride, stride}; }
+};
+
 struct Lane {
   // plan
   const DQuery* q;
@@ -41,8 +52,8 @@ struct Lane {
   const int32_t* sel;
   const int32_t* refs;
   // state
-  int64_t* ks;
-  int64_t* heap;
+  LaneWords ks;
+  LaneWords heap;
   int32_t half;  // words per semispace
   // batch
   const NfaBatch* b;
@@ -254,9 +265,9 @@ struct Lane {
   __device__ int64_t& returned(int o) const { return ks[q->ks_post + o]; }
 
   // ------------------------------------------------------------ timers (Scheduler FIFO)
-  __device__ int64_t* sq(int s) const { return ks + q->ks_sched + s * (2 + kSchedCap); }
+  __device__ LaneWords sq(int s) const { return ks.at(q->ks_sched + s * (2 + kSchedCap)); }
   __device__ void notifyAt(int s, int64_t t) {  // Scheduler.notifyAt :66-74
-    int64_t* S = sq(s);
+    LaneWords S = sq(s);
     if (S[1] >= kSchedCap) {
       err |= NFA_ERR_TIMERS;
       return;
@@ -266,11 +277,11 @@ struct Lane {
   }
   __device__ bool qempty(int s) const { return sq(s)[1] == 0; }
   __device__ int64_t qhead(int s) const {
-    const int64_t* S = sq(s);
+    const LaneWords S = sq(s);
     return S[2 + S[0]];
   }
   __device__ void qpop(int s) const {
-    int64_t* S = sq(s);
+    LaneWords S = sq(s);
     S[0] = (S[0] + 1) % kSchedCap;
     S[1]--;
   }
@@ -1072,7 +1083,7 @@ __device__ __forceinline__ int64_t adv_after(const NfaBatch& b, int64_t from, in
 }
 
 __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
-                         int32_t heap_half, int32_t key, int32_t* err_out) {
+                         int32_t heap_half, int64_t lanes, int32_t key, int32_t* err_out) {
   const DQuery* q = (const DQuery*)blob;
   Lane L;
   L.q = q;
@@ -1085,9 +1096,11 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
   L.consts = (const DVal*)(blob + q->off_const);
   L.sel = (const int32_t*)(blob + q->off_sel);
   L.refs = (const int32_t*)(blob + q->off_refs);
-  L.ks = ks_all + (int64_t)key * q->ks_words;
+  L.ks = LaneWords{ks_all + key, lanes};
   L.half = heap_half;
-  L.heap = heap_all + (int64_t)key * (2 * (int64_t)heap_half + 64);
+  // the heap stays key-major: a lane's run records and chain nodes are private, pointer-chased objects, so
+  // keeping each object's words in one line beats sharing lines with other lanes' (unrelated) offsets
+  L.heap = LaneWords{heap_all + (int64_t)key * (2 * (int64_t)heap_half + 64), 1};
   L.b = &b;
   L.key = key;
   L.err = 0;

@@ -453,8 +453,9 @@ void ensure_state(sm_app* a, QueryRt& q, int64_t nkeys) {
   SM_HIP(hipMalloc(&nks, ks_bytes));
   SM_HIP(hipMalloc(&nheap, heap_bytes));
   SM_HIP(hipMemsetAsync(nks, 0, ks_bytes, a->stream));
-  if (q.state_slots > 0) {
-    SM_HIP(hipMemcpyAsync(nks, q.ks.p, (size_t)q.state_slots * h.ks_words * 8, hipMemcpyDeviceToDevice, a->stream));
+  if (q.state_slots > 0) {  // ks: lane-interleaved rows (word-major, one column per key), re-pitched; heap: key-major
+    SM_HIP(hipMemcpy2DAsync(nks, (size_t)cap * 8, q.ks.p, (size_t)q.state_slots * 8, (size_t)q.state_slots * 8,
+                            (size_t)h.ks_words, hipMemcpyDeviceToDevice, a->stream));
     SM_HIP(hipMemcpyAsync(nheap, q.heap.p, (size_t)q.state_slots * heap_words * 8, hipMemcpyDeviceToDevice, a->stream));
   }
   SM_HIP(hipStreamSynchronize(a->stream));
@@ -547,8 +548,8 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   SM_HIP(hipMemsetAsync(a->d_count.p, 0, 4, hs));
   SM_HIP(hipMemsetAsync(a->d_err.p, 0, 4, hs));
   if (tm) tm->mark("nfa_setup", hs);
-  launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, (int32_t)nkeys,
-             (int32_t*)a->d_err.p, hs);
+  launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
+             (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
   SM_HIP(hipGetLastError());
   if (tm) tm->mark("nfa", hs);
   uint32_t hc = 0;

@@ -224,8 +224,14 @@ void flush(HApp* a) {
       key_off = {0, (int64_t)pos.size()};
       key_pos = pos;
     }
-    if (nkeys > q.state_slots) {
-      q.ks.resize((size_t)nkeys * h.ks_words, 0);
+    if (nkeys > q.state_slots) {  // ks rows are lane-interleaved (word-major): re-pitch each row; heap key-major
+      auto grow = [&](std::vector<int64_t>& v, size_t words) {
+        std::vector<int64_t> n((size_t)nkeys * words, 0);
+        for (size_t w = 0; w < words; ++w)
+          for (int64_t k = 0; k < q.state_slots; ++k) n[w * nkeys + k] = v[w * q.state_slots + k];
+        v.swap(n);
+      };
+      grow(q.ks, (size_t)h.ks_words);
       q.heap.resize((size_t)nkeys * (2 * (size_t)a->heap_half + 64), 0);
       q.state_slots = nkeys;
     }
@@ -251,7 +257,7 @@ void flush(HApp* a) {
     b.out_count = &count;
     b.out_cap = (uint32_t)(out.size() / stride);
     b.out_stride = (uint32_t)stride;
-    for (int32_t key = 0; key < nkeys; ++key) nfa_lane(b, blob, q.ks.data(), q.heap.data(), a->heap_half, key, &err);
+    for (int32_t key = 0; key < nkeys; ++key) nfa_lane(b, blob, q.ks.data(), q.heap.data(), a->heap_half, q.state_slots, key, &err);
     if (err) throw std::runtime_error("nfa error flags " + std::to_string(err));
     for (unsigned k = 0; k < count; ++k) {
       const char* r = out.data() + (size_t)k * stride;
