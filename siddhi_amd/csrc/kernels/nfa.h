@@ -20,6 +20,14 @@ struct NfaStream {
   const uint8_t* nulls[kMaxAttrs];  // null flags per attribute or nullptr
 };
 
+// One event of a query's batch in key order (built by the lane-events pass from key_pos and the batch
+// columns): position, stream, clock after sendData, advance points up to it (-1 = unknown), then the chain-node
+// image the NFA copies into a partial (word 0 unused, ts, ordinal, null mask, attribute words).
+struct LaneEv {
+  enum : int { kPos = 0, kStream = 1, kClock = 2, kUpto = 3, kNode = 4 };
+  static __host__ __device__ constexpr int64_t words(int node_words) { return kNode + node_words; }
+};
+
 struct NfaBatch {
   // app batch (all records in arrival order)
   const int32_t* ev_stream;  // stream index or NFA_* marker
@@ -38,6 +46,7 @@ struct NfaBatch {
   // this query's records grouped by key slot: key_pos[key_off[k] .. key_off[k+1]) ascending
   const int64_t* key_off;
   const int64_t* key_pos;
+  const int64_t* lane_ev;    // LaneEv records, one per key_pos entry (filled by launch_lane_events)
   int32_t create_all;        // non-partitioned: the single lane exists from app creation
   // output
   void* out;
@@ -46,6 +55,10 @@ struct NfaBatch {
   uint32_t out_stride;
 };
 
+// LaneEv records for key_pos[0, nq) of a batch of n records: b.lane_ev must point at nq * LaneEv::words(node_words)
+// words, inv_scratch at n int32
+void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_words, int32_t* inv_scratch,
+                        hipStream_t s);
 // ks is lane-interleaved: word w of key k at [w * lanes + k] (lanes = allocated key capacity); heap is key-major
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
                 int32_t nkeys, int32_t* err_dev, hipStream_t s);

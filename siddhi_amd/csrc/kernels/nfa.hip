@@ -1,5 +1,6 @@
 // HIP launch wrapper of the NFA interpreter (implementation in nfa_impl.h).
 #include "nfa_impl.h"
+#include "primitives.h"
 
 namespace sm {
 namespace {
@@ -11,7 +12,35 @@ __global__ void nfa_kernel(NfaBatch b, const char* __restrict__ blob, int64_t* k
   nfa_lane(b, blob, ks_all, heap_all, heap_half, lanes, key, err_out);
 }
 
+// Gather each record of the query's batch, in key order, into its LaneEv record: a lane then reads one
+// contiguous record per event instead of chasing key_pos -> stream / row / ts / clock / ordinal / columns.
+// Key order -> batch position is a permutation (key_pos); build the records in batch-position order instead, so
+// the column reads are coalesced and each record (one line-sized store burst) goes to its key-order slot.
+__global__ void lane_index_kernel(const int64_t* __restrict__ key_pos, int64_t nq, int32_t* __restrict__ inv) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nq) inv[key_pos[k]] = (int32_t)k;
+}
+
+__global__ void lane_events_kernel(NfaBatch b, int64_t n, const int32_t* __restrict__ inv, int32_t node_words,
+                                   int64_t* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t k = inv[p];
+  if (k >= 0) lane_event_record(b, p, k, node_words, out);
+}
+
 }  // namespace
+
+void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_words, int32_t* inv_scratch,
+                        hipStream_t s) {
+  if (nq <= 0) return;
+  if (nq >= INT32_MAX) throw std::runtime_error("query batch too large for the lane-event index (>= 2^31 records)");
+  SM_HIP(hipMemsetAsync(inv_scratch, 0xff, (size_t)n * 4, s));
+  hipLaunchKernelGGL(lane_index_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, b.key_pos, nq,
+                     inv_scratch);
+  hipLaunchKernelGGL(lane_events_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, n,
+                     (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
+}
 
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half,
                 int64_t lanes, int32_t nkeys, int32_t* err_dev, hipStream_t s) {

@@ -127,31 +127,12 @@ struct Lane {
     for (int k = 4; k < q->node_words; ++k) heap[n + k] = 0;
     return n;
   }
-  // the incoming event, materialised as a chain node once per delivery
-  __device__ int32_t event_node(int64_t p) {
-    int s = b->ev_stream[p];
-    int64_t row = b->ev_row[p];
-    const NfaStream& st = b->streams[s];
+  // the incoming event, materialised as a chain node once per delivery: a copy of the node image the
+  // lane-events pass already built (LaneEv, nfa.h)
+  __device__ int32_t event_node(const int64_t* __restrict__ r) {
     int32_t n = alloc(q->node_words);
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
-    heap[n + 1] = b->ev_ts[p];
-    heap[n + 2] = b->ev_ord[p];
-    int64_t nulls = 0;
-    for (int a = 0; a < st.nattr; ++a) {
-      int64_t v = 0;
-      bool isnull = st.nulls[a] && st.nulls[a][row];
-      switch (st.types[a]) {
-        case T_INT: v = ((const int32_t*)st.cols[a])[row]; break;
-        case T_LONG: v = ((const int64_t*)st.cols[a])[row]; break;
-        case T_FLOAT: { double d = (double)((const float*)st.cols[a])[row]; v = __double_as_longlong(d); break; }
-        case T_DOUBLE: v = __double_as_longlong(((const double*)st.cols[a])[row]); break;
-        case T_STRING: v = ((const int32_t*)st.cols[a])[row]; isnull = isnull || v < 0; break;
-        default: v = ((const uint8_t*)st.cols[a])[row]; break;
-      }
-      if (isnull) nulls |= (1ll << a);
-      heap[n + 4 + a] = v;
-    }
-    heap[n + 3] = nulls;
+    for (int w = 1; w < q->node_words; ++w) heap[n + w] = r[LaneEv::kNode + w];
     return n;
   }
   // StateEvent.addEvent :212-222
@@ -966,8 +947,9 @@ struct Lane {
 
   // ------------------------------------------------------------ event delivery
   // MultiProcessStreamReceiver.receive / SingleProcessStreamReceiver.processAndClear + selector dispatch
-  __device__ void deliver(int64_t p) {
-    int s = b->ev_stream[p];
+  __device__ void deliver(const int64_t* __restrict__ r) {
+    const int64_t p = r[LaneEv::kPos];
+    const int s = (int)r[LaneEv::kStream];
     const DReceiver* R = nullptr;
     for (int k = 0; k < q->nrecv; ++k)
       if (recv[k].stream == s) R = &recv[k];
@@ -976,8 +958,8 @@ struct Lane {
     time = 0;
     phase = 1;
     sched = -1;
-    int32_t ev = event_node(p);
-    int64_t now = b->ev_ts[p];
+    int32_t ev = event_node(r);
+    int64_t now = r[LaneEv::kNode + 1];
     // stabilizeStates
     if (q->kind == 2) {
       inner_reset(q->root_inner);
@@ -1073,13 +1055,52 @@ __device__ int64_t gallop(const int64_t* __restrict__ v, int64_t from, int64_t n
   return hi;
 }
 
+// Record k of the query's batch, in key order, as its LaneEv record (nfa.h): a lane then reads one contiguous
+// record per event instead of chasing key_pos -> stream / row / ts / clock / ordinal / columns.
+__device__ __forceinline__ void lane_event_record(const NfaBatch& b, int64_t p, int64_t k, int32_t node_words,
+                                                  int64_t* __restrict__ out) {
+  int64_t* r = out + k * LaneEv::words(node_words);
+  const int s = b.ev_stream[p];
+  r[LaneEv::kPos] = p;
+  r[LaneEv::kStream] = s;
+  r[LaneEv::kClock] = b.ev_clock[p];
+  r[LaneEv::kUpto] = b.adv_upto ? b.adv_upto[p] : -1;
+  int64_t* node = r + LaneEv::kNode;
+  node[0] = 0;
+  node[1] = b.ev_ts[p];
+  node[2] = b.ev_ord[p];
+  int64_t nulls = 0;
+  int na = 0;
+  if (s >= 0) {
+    const NfaStream& st = b.streams[s];
+    const int64_t row = b.ev_row[p];
+    na = st.nattr;
+    for (int a = 0; a < na; ++a) {
+      int64_t v = 0;
+      bool isnull = st.nulls[a] && st.nulls[a][row];
+      switch (st.types[a]) {
+        case T_INT: v = ((const int32_t*)st.cols[a])[row]; break;
+        case T_LONG: v = ((const int64_t*)st.cols[a])[row]; break;
+        case T_FLOAT: { double d = (double)((const float*)st.cols[a])[row]; v = __double_as_longlong(d); break; }
+        case T_DOUBLE: v = __double_as_longlong(((const double*)st.cols[a])[row]); break;
+        case T_STRING: v = ((const int32_t*)st.cols[a])[row]; isnull = isnull || v < 0; break;
+        default: v = ((const uint8_t*)st.cols[a])[row]; break;
+      }
+      if (isnull) nulls |= (1ll << a);
+      node[4 + a] = v;
+    }
+  }
+  node[3] = nulls;
+  for (int w = 4 + na; w < node_words; ++w) node[w] = 0;
+}
+
 // First advance point after position x, at or after index `from`: O(1) through the per-position count of
-// advance points (adv_upto[x] = advance points at positions <= x), galloping when the batch has none.
-__device__ __forceinline__ int64_t adv_after(const NfaBatch& b, int64_t from, int64_t x) {
+// advance points (upto = advance points at positions <= x, carried in the event's LaneEv record), galloping when
+// the batch has none.
+__device__ __forceinline__ int64_t adv_after(const NfaBatch& b, int64_t from, int64_t x, int64_t upto) {
   if (x == INT64_MAX) return b.nadv > from ? b.nadv : from;
-  if (!b.adv_upto) return gallop<true>(b.adv_pos, from, b.nadv, x);
-  const int64_t u = b.adv_upto[x];
-  return u > from ? u : from;
+  if (upto < 0) return gallop<true>(b.adv_pos, from, b.nadv, x);
+  return upto > from ? upto : from;
 }
 
 __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
@@ -1108,6 +1129,7 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
   L.clock = b.clock_in;
 
   const int64_t ebeg = b.key_off[key], eend = b.key_off[key + 1];
+  const int64_t W = LaneEv::words(q->node_words);
   const bool has_timers = q->nsched > 0;
   // lane creation: QueryRuntime constructor → init() seeds the start state (PartitionRuntime.clonePartition)
   if (L.misc(4) == 0) {
@@ -1125,7 +1147,7 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
       L.sq(s)[0] = 0;
       L.sq(s)[1] = 0;
     }
-    L.misc(0) = (ebeg < eend) ? b.ev_ord[b.key_pos[ebeg]] : -1;  // creation ordinal
+    L.misc(0) = (ebeg < eend) ? b.lane_ev[ebeg * W + LaneEv::kNode + 2] : -1;  // creation ordinal
     L.misc(1) = 0;
     L.misc(2) = 0;
     L.misc(3) = 0;
@@ -1139,7 +1161,9 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
   int64_t k = ebeg;
   int64_t search_from = 0;  // advance-point index
   for (;;) {
-    int64_t next_pos = (k < eend) ? b.key_pos[k] : INT64_MAX;
+    // this key's events are consecutive LaneEv records (key order): one contiguous read per event
+    const int64_t* __restrict__ r = b.lane_ev + k * W;
+    const int64_t next_pos = (k < eend) ? r[LaneEv::kPos] : INT64_MAX;
     if (has_timers) {
       for (;;) {
         if (L.err) break;
@@ -1147,9 +1171,9 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
         if (!L.min_head(t)) break;
         // first advance point at or after search_from whose position <= next_pos and (clock >= t or wall tick)
         // (both arrays are non-decreasing: positions ascend and the playback clock only moves forward)
-        const int64_t a1 = adv_after(b, search_from, next_pos);
+        const int64_t a1 = adv_after(b, search_from, next_pos, k < eend ? r[LaneEv::kUpto] : -1);
         // quick reject: every advance point up to next_pos has clock <= the clock after next_pos's sendData
-        if (next_pos != INT64_MAX && b.ev_clock[next_pos] < t) {
+        if (next_pos != INT64_MAX && r[LaneEv::kClock] < t) {
           search_from = a1;
           break;
         }
@@ -1173,19 +1197,19 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
       }
     }
     if (L.err || k >= eend) break;
-    int64_t p = b.key_pos[k];
+    const int64_t p = next_pos;
     // clock as of this event (sendData advanced it before delivery)
-    L.clock = b.ev_clock[p];
-    if (b.ev_stream[p] == NFA_START) {
+    L.clock = r[LaneEv::kClock];
+    if (r[LaneEv::kStream] == NFA_START) {
       // SiddhiAppRuntime.start → AbsentStreamPreStateProcessor.start :261-269 (non-partitioned queries)
       for (int pp = 0; pp < q->npre; ++pp)
         if (L.is_absent(pp) && L.pre[pp].isStart && L.pre[pp].waitingTime != -1 && L.fl(pp, F_ACTIVE))
           L.notifyAt(L.pre[pp].sched, L.clock + L.pre[pp].waitingTime);
     } else {
-      L.deliver(p);
+      L.deliver(r);
     }
     // timers scheduled by this event may only fire at later advance points
-    search_from = adv_after(b, search_from, p);
+    search_from = adv_after(b, search_from, p, r[LaneEv::kUpto]);
     ++k;
     if (L.err) break;
     L.safe_point();

@@ -540,6 +540,7 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.clock_in = ev.clock_in;
   b.key_off = key_off;
   b.key_pos = key_pos;
+  b.lane_ev = (const int64_t*)a->sc.take((size_t)std::max<int64_t>(nq, 1) * LaneEv::words(h.node_words) * 8);
   b.create_all = !partitioned;
   b.out = q.out.p;
   b.out_count = (uint32_t*)a->d_count.p;
@@ -547,6 +548,7 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.out_stride = (uint32_t)stride;
   SM_HIP(hipMemsetAsync(a->d_count.p, 0, 4, hs));
   SM_HIP(hipMemsetAsync(a->d_err.p, 0, 4, hs));
+  launch_lane_events(b, N, nq, h.node_words, (int32_t*)a->sc.take((size_t)std::max<int64_t>(N, 1) * 4), hs);
   if (tm) tm->mark("nfa_setup", hs);
   launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
              (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
@@ -566,6 +568,15 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
     throw std::runtime_error("query '" + q.cq.name + "':" + why);
   }
   read_outputs(a, qi, q.out.p, std::min<int64_t>(hc, cap), outs);
+}
+
+// Scratch of one batch: record selection + key grouping (~96 B per record) and the LaneEv records of the widest
+// pattern query.
+size_t batch_scratch(const sm_app* a, int64_t N) {
+  int64_t lane_words = 0;
+  for (auto& q : a->queries)
+    if (q->cq.hdr.kind != 0) lane_words = std::max<int64_t>(lane_words, LaneEv::words(q->cq.hdr.node_words));
+  return (size_t)N * (100 + 8 * (size_t)lane_words) + (64 << 20);
 }
 
 void flush(sm_app* a) {
@@ -609,7 +620,7 @@ void flush(sm_app* a) {
   }
   a->d_err.ensure(16);
   a->d_count.ensure(16);
-  ensure_scratch(a, (size_t)N * 96 + (64 << 20));
+  ensure_scratch(a, batch_scratch(a, N));
   std::vector<HostOut> outs;
   const EvArrays ev{(const int32_t*)a->d_ev_stream.p, (const int64_t*)a->d_ev_row.p, (const int64_t*)a->d_ev_ts.p,
                     (const int64_t*)a->d_ev_clock.p, (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p,
@@ -1116,7 +1127,7 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
       d->ensure((size_t)N * 8);
     a->d_err.ensure(16);
     a->d_count.ensure(16);
-    ensure_scratch(a, (size_t)N * 96 + (64 << 20));
+    ensure_scratch(a, batch_scratch(a, N));
     a->sc.used = 0;
     FastTimings* tm = a->fast_timing ? &a->fast_tm : nullptr;
     if (tm) {

@@ -257,6 +257,9 @@ void flush(HApp* a) {
     b.out_count = &count;
     b.out_cap = (uint32_t)(out.size() / stride);
     b.out_stride = (uint32_t)stride;
+    std::vector<int64_t> lane_ev(std::max<size_t>(key_pos.size(), 1) * LaneEv::words(h.node_words));
+    b.lane_ev = lane_ev.data();
+    for (size_t k = 0; k < key_pos.size(); ++k) lane_event_record(b, key_pos[k], (int64_t)k, h.node_words, lane_ev.data());
     for (int32_t key = 0; key < nkeys; ++key) nfa_lane(b, blob, q.ks.data(), q.heap.data(), a->heap_half, q.state_slots, key, &err);
     if (err) throw std::runtime_error("nfa error flags " + std::to_string(err));
     for (unsigned k = 0; k < count; ++k) {
