@@ -13,6 +13,7 @@
  *   sm_app_advance_time             @app:playback heartbeat (EventTimeBasedMillisTimestampGenerator.java:99)
  *   sm_app_process_device_batch     StreamJunction.sendData over a device-resident columnar batch (no Java
  *                                   counterpart: the bulk entry a JNI/Panama receiver would call)
+ *   sm_app_snapshot / sm_app_restore  SiddhiAppRuntime.snapshot() / restore(byte[])  :548 / :560
  *   sm_app_process_device_events    a sequence of InputHandler.send calls over several streams of one
  *                                   schema (InputHandler.java:53 → StreamJunction.sendData :232), device-resident
  *
@@ -121,6 +122,14 @@ int sm_app_process_device_batch(sm_app* app, const char* stream_id, size_t n, co
 int sm_app_process_device_events(sm_app* app, size_t n, const int32_t* d_stream_idx, const int64_t* d_timestamps,
                                  const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
                                  void* hip_stream);
+/* Persistence. sm_app_snapshot flushes staged events, then serialises the app's matching state (partition
+ * instances, partial matches with their event chains, pending timers, playback clock, arrival ordinal, string
+ * dictionary) into buf and stores its size in *len; with buf == NULL it only reports the size (a non-NULL buf
+ * smaller than that fails with SM_E_RUNTIME). sm_app_restore loads such a snapshot into an app created from the
+ * same SiddhiQL text (SM_E_RUNTIME, the reference's CannotRestoreSiddhiAppStateException, otherwise); staged
+ * events are discarded. */
+int sm_app_snapshot(sm_app* app, uint8_t* buf, size_t cap, size_t* len);
+int sm_app_restore(sm_app* app, const uint8_t* buf, size_t len);
 /* Match tuples of the last device batch for a query: n pairs (e1, e2) of ordinals relative to the batch's
  * ordinal_base, uint32[2*n] in device memory, in reference output order (e2 ordinal, then e1 ordinal). */
 int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** d_pairs, size_t* n);

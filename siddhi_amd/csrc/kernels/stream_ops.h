@@ -21,6 +21,7 @@ struct KeyTable {
   int64_t slot_cap = 0;
   int32_t nslots = 0;
   void reserve(int64_t total_slots, hipStream_t s);
+  void load(const int64_t* keys_host, int32_t n, hipStream_t s);
   void release();
 };
 

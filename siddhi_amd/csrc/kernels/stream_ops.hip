@@ -520,6 +520,19 @@ void KeyTable::release() {
   nslots = 0;
 }
 
+// Restore: take nslots keys (host array, slot order) and rebuild the hash table from them.
+void KeyTable::load(const int64_t* keys_host, int32_t n, hipStream_t s) {
+  nslots = 0;
+  reserve(n, s);
+  if (tslots) SM_HIP(hipMemsetAsync(tslots, 0, (size_t)cap * 4, s));
+  if (n > 0) {
+    SM_HIP(hipMemcpyAsync(slot_keys, keys_host, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(rehash_kernel, grid_for(n), dim3(256), 0, s, slot_keys, (int64_t)n, tkeys, tslots, mask);
+  }
+  nslots = n;
+  SM_HIP(hipStreamSynchronize(s));
+}
+
 void KeyTable::reserve(int64_t total, hipStream_t s) {
   if (total > INT32_MAX - 1) throw std::runtime_error("too many partition keys");
   if (total > slot_cap) {

@@ -189,6 +189,7 @@ struct sm_app {
   int64_t batch_events = 1 << 20;
   int32_t heap_half = 1024;
   int64_t out_records = 0;  // option "output_records" (0 = automatic)
+  uint64_t text_hash = 0;   // FNV-1a of the SiddhiQL text (snapshots restore only into the same app)
   bool collect = false;
   std::map<std::string, std::vector<std::string>> collected_streams;  // JSON fragments
   std::map<std::string, std::vector<std::string>> collected_queries;
@@ -740,6 +741,37 @@ std::string dump_json(sm_app* a) {
 
 using namespace sm;
 
+// snapshot encoding helpers (sm_app_snapshot / sm_app_restore)
+namespace {
+constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '1'};
+
+struct SnapWriter {
+  std::vector<uint8_t> b;
+  void raw(const void* p, size_t n) { b.insert(b.end(), (const uint8_t*)p, (const uint8_t*)p + n); }
+  template <typename T> void put(T v) { raw(&v, sizeof(T)); }
+};
+struct SnapReader {
+  const uint8_t* p;
+  size_t n, o = 0;
+  void raw(void* d, size_t k) {
+    if (o + k > n) throw std::runtime_error("CannotRestoreSiddhiAppStateException: snapshot truncated");
+    memcpy(d, p + o, k);
+    o += k;
+  }
+  template <typename T> T get() {
+    T v;
+    raw(&v, sizeof(T));
+    return v;
+  }
+};
+
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+}  // namespace
+
 extern "C" {
 
 const char* sm_last_error(void) { return sm::g_err.c_str(); }
@@ -757,6 +789,7 @@ int sm_app_create(sm_manager* m, const char* siddhiql, sm_app** out) {
   auto a = std::make_unique<sm_app>();
   int rc = guarded([&] {
     a->ast = sql::parse_app(siddhiql ? siddhiql : "");
+    a->text_hash = fnv1a(siddhiql ? siddhiql : "");
     build_app(a.get());
     int dev = 0;
     if (hipGetDeviceCount(&dev) != hipSuccess || dev == 0)
@@ -1155,6 +1188,134 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
     a->clock_batch_in = a->clock;
     if (!d_ordinals) a->next_ordinal = std::max<int64_t>(a->next_ordinal, ordinal_base + N);
     deliver(a, outs);
+  });
+}
+
+// ---- persistence: SiddhiAppRuntime.snapshot() :548 / restore(byte[]) :560 (core/SiddhiAppRuntime.java). The
+// snapshot holds what the reference's Snapshotables hold for the hot path: every partition instance (key table),
+// each instance's pending / new-and-every partial matches with their event chains (per-key state words + heap,
+// StreamPreStateProcessor.currentState :339-353), pending scheduler timers (Scheduler.currentState), the
+// playback clock and the arrival ordinal, plus the string dictionary the device values refer to. Staged events
+// are flushed first, so the snapshot is taken at a batch boundary.
+
+int sm_app_snapshot(sm_app* a, uint8_t* buf, size_t cap, size_t* len) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    flush(a);
+    SnapWriter w;
+    w.raw(kSnapMagic, 8);
+    w.put<uint64_t>(a->text_hash);
+    w.put<int64_t>(a->clock);
+    w.put<int64_t>(a->clock_batch_in);
+    w.put<int64_t>(a->next_ordinal);
+    w.put<int64_t>(a->ordinal_base);
+    w.put<uint8_t>(a->started);
+    w.put<int32_t>(a->heap_half);
+    w.put<uint32_t>((uint32_t)a->dict.strs.size());
+    for (auto& str : a->dict.strs) {
+      w.put<uint32_t>((uint32_t)str.size());
+      w.raw(str.data(), str.size());
+    }
+    w.put<uint32_t>((uint32_t)a->queries.size());
+    const size_t heap_words = 2 * (size_t)a->heap_half + 64;
+    for (auto& qp : a->queries) {
+      QueryRt& q = *qp;
+      const int32_t n = q.cq.hdr.kind == 0 ? 0 : q.keys.nslots ? q.keys.nslots : (int32_t)std::min<int64_t>(q.state_slots, 1);
+      const int32_t kw = q.cq.hdr.ks_words;
+      w.put<int32_t>(q.cq.hdr.partitioned ? q.keys.nslots : -1);
+      w.put<int32_t>(n);
+      w.put<int32_t>(kw);
+      if (q.cq.hdr.partitioned && q.keys.nslots) {
+        std::vector<int64_t> keys(q.keys.nslots);
+        SM_HIP(hipMemcpy(keys.data(), q.keys.slot_keys, keys.size() * 8, hipMemcpyDeviceToHost));
+        w.raw(keys.data(), keys.size() * 8);
+      }
+      if (n > 0) {
+        // per-key state words: lane-interleaved with stride state_slots on the device, packed to stride n here
+        std::vector<int64_t> ks((size_t)n * kw);
+        SM_HIP(hipMemcpy2D(ks.data(), (size_t)n * 8, q.ks.p, (size_t)q.state_slots * 8, (size_t)n * 8, (size_t)kw,
+                           hipMemcpyDeviceToHost));
+        w.raw(ks.data(), ks.size() * 8);
+        std::vector<int64_t> heap((size_t)n * heap_words);
+        SM_HIP(hipMemcpy(heap.data(), q.heap.p, heap.size() * 8, hipMemcpyDeviceToHost));
+        w.raw(heap.data(), heap.size() * 8);
+      }
+    }
+    *len = w.b.size();
+    if (buf && cap >= w.b.size()) memcpy(buf, w.b.data(), w.b.size());
+    else if (buf) throw std::invalid_argument("snapshot buffer too small");
+  });
+}
+
+int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    SnapReader r{buf, len};
+    char magic[8];
+    r.raw(magic, 8);
+    if (memcmp(magic, kSnapMagic, 8) != 0) throw std::runtime_error("CannotRestoreSiddhiAppStateException: not a snapshot");
+    if (r.get<uint64_t>() != a->text_hash)
+      throw std::runtime_error("CannotRestoreSiddhiAppStateException: snapshot of a different Siddhi app");
+    // drop staged records (a START marker included): the snapshot's state replaces them
+    a->ev_stream.clear();
+    a->ev_row.clear();
+    a->ev_ts.clear();
+    a->ev_clock.clear();
+    a->ev_ord.clear();
+    a->adv_pos.clear();
+    a->adv_clock.clear();
+    a->adv_wall.clear();
+    for (auto& st : a->streams) st.clear();
+    a->clock = r.get<int64_t>();
+    a->clock_batch_in = r.get<int64_t>();
+    a->next_ordinal = r.get<int64_t>();
+    a->ordinal_base = r.get<int64_t>();
+    a->started = r.get<uint8_t>() != 0;
+    const int32_t half = r.get<int32_t>();
+    const uint32_t nd = r.get<uint32_t>();
+    Dict d;
+    for (uint32_t i = 0; i < nd; ++i) {
+      std::string str(r.get<uint32_t>(), '\0');
+      r.raw(&str[0], str.size());
+      d.intern(str);
+    }
+    for (size_t i = 0; i < a->dict.strs.size(); ++i)  // ids baked into the compiled plan must agree
+      if (i >= d.strs.size() || d.strs[i] != a->dict.strs[i])
+        throw std::runtime_error("CannotRestoreSiddhiAppStateException: string dictionary mismatch");
+    a->dict = d;
+    if (r.get<uint32_t>() != a->queries.size())
+      throw std::runtime_error("CannotRestoreSiddhiAppStateException: query count mismatch");
+    for (auto& qp : a->queries)
+      if (qp->state_slots && half != a->heap_half)
+        throw std::runtime_error("CannotRestoreSiddhiAppStateException: heap_words differs from the running app");
+    a->heap_half = half;
+    const size_t heap_words = 2 * (size_t)a->heap_half + 64;
+    for (auto& qp : a->queries) {
+      QueryRt& q = *qp;
+      const int32_t nkeys = r.get<int32_t>();
+      const int32_t n = r.get<int32_t>();
+      const int32_t kw = r.get<int32_t>();
+      if (kw != q.cq.hdr.ks_words) throw std::runtime_error("CannotRestoreSiddhiAppStateException: plan mismatch");
+      if (nkeys >= 0) {
+        std::vector<int64_t> keys(nkeys);
+        r.raw(keys.data(), keys.size() * 8);
+        q.keys.load(keys.data(), nkeys, a->stream);
+      }
+      if (n > 0) {
+        ensure_state(a, q, n);
+        std::vector<int64_t> ks((size_t)n * kw);
+        r.raw(ks.data(), ks.size() * 8);
+        SM_HIP(hipMemset(q.ks.p, 0, (size_t)q.state_slots * kw * 8));
+        SM_HIP(hipMemcpy2D(q.ks.p, (size_t)q.state_slots * 8, ks.data(), (size_t)n * 8, (size_t)n * 8, (size_t)kw,
+                           hipMemcpyHostToDevice));
+        std::vector<int64_t> heap((size_t)n * heap_words);
+        r.raw(heap.data(), heap.size() * 8);
+        SM_HIP(hipMemcpy(q.heap.p, heap.data(), heap.size() * 8, hipMemcpyHostToDevice));
+      } else if (q.state_slots) {
+        SM_HIP(hipMemset(q.ks.p, 0, (size_t)q.state_slots * kw * 8));
+      }
+    }
+    if (r.o != len) throw std::runtime_error("CannotRestoreSiddhiAppStateException: trailing bytes");
   });
 }
 

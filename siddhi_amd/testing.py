@@ -114,6 +114,18 @@ class ProductApp:
                                                  ptrs, ordinals.data_ptr() if ordinals is not None else None,
                                                  int(ordinal_base), hip_stream))
 
+    def snapshot(self):
+        """SiddhiAppRuntime.snapshot(): bytes"""
+        n = ctypes.c_size_t()
+        _call(lib().sm_app_snapshot(self.h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        _call(lib().sm_app_snapshot(self.h, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+    def restore(self, data):
+        """SiddhiAppRuntime.restore(byte[])"""
+        _call(lib().sm_app_restore(self.h, data, len(data)))
+
     def device_matches(self, query):
         p = ctypes.c_void_p()
         n = ctypes.c_size_t()
