@@ -14,6 +14,8 @@
  *   sm_app_process_device_batch     StreamJunction.sendData over a device-resident columnar batch (no Java
  *                                   counterpart: the bulk entry a JNI/Panama receiver would call)
  *   sm_app_snapshot / sm_app_restore  SiddhiAppRuntime.snapshot() / restore(byte[])  :548 / :560
+ *   sm_partition_by_owner           multi-GPU form of PartitionStreamReceiver.receive (partition/
+ *                                   PartitionStreamReceiver.java:156): route each event to its key's owner rank
  *   sm_app_process_device_events    a sequence of InputHandler.send calls over several streams of one
  *                                   schema (InputHandler.java:53 → StreamJunction.sendData :232), device-resident
  *
@@ -130,6 +132,13 @@ int sm_app_process_device_events(sm_app* app, size_t n, const int32_t* d_stream_
  * events are discarded. */
 int sm_app_snapshot(sm_app* app, uint8_t* buf, size_t cap, size_t* len);
 int sm_app_restore(sm_app* app, const uint8_t* buf, size_t len);
+/* Stable partition of a device batch by owner rank = key mod world (keys: 4- or 8-byte integers, world <= 64):
+ * column c (widths[c] bytes per element: 1, 2, 4 or 8) is copied from d_src[c] to d_dst[c] grouped by owner,
+ * arrival order kept within each owner; counts[o] = events for owner o (host array of world entries). The
+ * send side of the key exchange before the RCCL all-to-all-v. */
+int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t world, int ncols,
+                          const int32_t* widths, const void* const* d_src, void* const* d_dst, uint64_t* counts,
+                          void* hip_stream);
 /* Match tuples of the last device batch for a query: n pairs (e1, e2) of ordinals relative to the batch's
  * ordinal_base, uint32[2*n] in device memory, in reference output order (e2 ordinal, then e1 ordinal). */
 int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** d_pairs, size_t* n);

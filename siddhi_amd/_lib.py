@@ -19,7 +19,7 @@ EXPORTS = [
     "sm_input_send_columns", "sm_app_stream_schema", "sm_app_advance_time", "sm_app_advance_wallclock",
     "sm_app_add_stream_callback", "sm_app_add_query_callback", "sm_app_set_collect", "sm_app_dump_outputs",
     "sm_app_set_option", "sm_app_process_device_batch", "sm_app_process_device_events", "sm_app_device_matches",
-    "sm_app_snapshot", "sm_app_restore",
+    "sm_app_snapshot", "sm_app_restore", "sm_partition_by_owner",
     "sm_app_get_stat",
 ]
 
@@ -69,6 +69,9 @@ def lib():
         L.sm_app_set_option.argtypes = [vp, cp, i64]
         L.sm_app_process_device_batch.argtypes = [vp, cp, sz, vp, ctypes.POINTER(vp), vp, i64, vp]
         L.sm_app_process_device_events.argtypes = [vp, sz, vp, vp, ctypes.POINTER(vp), vp, i64, vp]
+        L.sm_partition_by_owner.argtypes = [vp, ctypes.c_int, sz, ctypes.c_uint32, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                            ctypes.POINTER(ctypes.c_uint64), vp]
         L.sm_app_snapshot.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.sm_app_restore.argtypes = [vp, ctypes.c_char_p, sz]
         L.sm_app_device_matches.argtypes = [vp, cp, ctypes.POINTER(vp), ctypes.POINTER(sz)]

@@ -1,0 +1,123 @@
+// Stable partition of a columnar batch by owning rank (key mod world) for the multi-GPU key exchange
+// (PartitionStreamReceiver.receive core/partition/PartitionStreamReceiver.java:156 routes each event to the
+// runtime of its key; across GPUs the key's owner rank plays that role). A counting sort with world <= 64 buckets:
+//   1. per 4096-event tile: events per owner                                  -> cnt[owner * tiles + tile]
+//   2. exclusive scan of cnt (owner-major)                                      -> first slot of (owner, tile)
+//   3. per tile, events in arrival order: rank within (tile, owner) from wave ballots, then every column is
+//      copied to its slot. Within an owner the output keeps arrival order, so rank r receives its rows in
+//      global arrival order once the ranks' slices are concatenated.
+// HBM traffic: key 4-8 B (pass 1) + every column read and written once (pass 3).
+#include "partition.h"
+
+namespace sm {
+namespace {
+
+constexpr int kPThreads = 256, kPItems = 16, kPTile = kPThreads * kPItems;
+
+template <typename K>
+__device__ __forceinline__ uint32_t owner_of(K k, uint32_t world) {
+  int64_t r = (int64_t)k % (int64_t)world;
+  return (uint32_t)(r < 0 ? r + world : r);
+}
+
+template <typename K>
+__global__ __launch_bounds__(kPThreads) void owner_count_kernel(const K* __restrict__ keys, int64_t n, uint32_t world,
+                                                                uint32_t ntiles, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t c[kMaxOwners];
+  if (threadIdx.x < kMaxOwners) c[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kPTile;
+  for (int k = 0; k < kPItems; ++k) {
+    const int64_t i = base + (int64_t)k * kPThreads + threadIdx.x;
+    if (i < n) atomicAdd(&c[owner_of(keys[i], world)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < world) cnt[(int64_t)threadIdx.x * ntiles + blockIdx.x] = c[threadIdx.x];
+}
+
+template <typename K>
+__global__ __launch_bounds__(kPThreads) void owner_scatter_kernel(const K* __restrict__ keys, int64_t n,
+                                                                  uint32_t world, uint32_t ntiles,
+                                                                  const uint32_t* __restrict__ start, PartCols cols) {
+  __shared__ uint32_t run[kMaxOwners];                   // next slot of each owner for this tile
+  __shared__ uint32_t wc[kPThreads / 64][kMaxOwners];    // per-wave counts of the current round
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x < world) run[threadIdx.x] = start[(int64_t)threadIdx.x * ntiles + blockIdx.x];
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int64_t base = (int64_t)blockIdx.x * kPTile;
+  for (int k = 0; k < kPItems; ++k) {
+    const int64_t i = base + (int64_t)k * kPThreads + threadIdx.x;
+    const bool in = i < n;
+    const uint32_t o = in ? owner_of(keys[i], world) : 0u;
+    // lanes of this wave with the same owner, via one ballot per owner bit
+    uint64_t peers = __ballot(in);
+    for (uint32_t b = 1; b < world; b <<= 1) {
+      const uint64_t bb = __ballot((o & b) != 0);
+      peers &= (o & b) ? bb : ~bb;
+    }
+    const uint32_t below = (uint32_t)__popcll(peers & lt);
+    __syncthreads();  // run[] of the previous round is final; wc may be reused
+    if (threadIdx.x < kPThreads / 64 * kMaxOwners) (&wc[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    if (in && below == 0) wc[w][o] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (in) {
+      uint32_t slot = run[o] + below;
+      for (int q = 0; q < w; ++q) slot += wc[q][o];
+      for (int c = 0; c < cols.n; ++c) {
+        switch (cols.width[c]) {
+          case 4: ((uint32_t*)cols.dst[c])[slot] = ((const uint32_t*)cols.src[c])[i]; break;
+          case 8: ((uint64_t*)cols.dst[c])[slot] = ((const uint64_t*)cols.src[c])[i]; break;
+          case 2: ((uint16_t*)cols.dst[c])[slot] = ((const uint16_t*)cols.src[c])[i]; break;
+          default: ((uint8_t*)cols.dst[c])[slot] = ((const uint8_t*)cols.src[c])[i]; break;
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < world) {
+      uint32_t t = 0;
+      for (int q = 0; q < kPThreads / 64; ++q) t += wc[q][threadIdx.x];
+      run[threadIdx.x] += t;
+    }
+  }
+}
+
+template <typename K>
+void partition_impl(const K* keys, int64_t n, uint32_t world, const PartCols& cols, uint64_t* counts_host,
+                    Scratch& sc, hipStream_t s) {
+  const uint32_t ntiles = (uint32_t)((n + kPTile - 1) / kPTile);
+  size_t mark = sc.used;
+  uint32_t* cnt = (uint32_t*)sc.take((size_t)world * ntiles * 4 + 4);
+  hipLaunchKernelGGL(owner_count_kernel<K>, dim3(ntiles), dim3(kPThreads), 0, s, keys, n, world, ntiles, cnt);
+  // per-owner totals before the scan turns the counts into slots
+  std::vector<uint32_t> h((size_t)world * ntiles);
+  SM_HIP(hipMemcpyAsync(h.data(), cnt, h.size() * 4, hipMemcpyDeviceToHost, s));
+  exclusive_scan_u32(cnt, (size_t)world * ntiles, sc, s);
+  hipLaunchKernelGGL(owner_scatter_kernel<K>, dim3(ntiles), dim3(kPThreads), 0, s, keys, n, world, ntiles,
+                     (const uint32_t*)cnt, cols);
+  SM_HIP(hipStreamSynchronize(s));
+  for (uint32_t o = 0; o < world; ++o) {
+    uint64_t t = 0;
+    for (uint32_t b = 0; b < ntiles; ++b) t += h[(size_t)o * ntiles + b];
+    counts_host[o] = t;
+  }
+  sc.used = mark;
+}
+
+}  // namespace
+
+void partition_by_owner(const void* keys, int key_width, int64_t n, uint32_t world, const PartCols& cols,
+                        uint64_t* counts_host, Scratch& sc, hipStream_t s) {
+  if (world == 0 || world > (uint32_t)kMaxOwners) throw std::invalid_argument("world size must be 1..64");
+  if (n >= (int64_t)UINT32_MAX) throw std::invalid_argument("partition batch too large (>= 2^32 events)");
+  if (cols.n > kMaxPartCols) throw std::invalid_argument("too many columns");
+  if (n == 0) {
+    for (uint32_t o = 0; o < world; ++o) counts_host[o] = 0;
+    return;
+  }
+  if (key_width == 4) partition_impl<int32_t>((const int32_t*)keys, n, world, cols, counts_host, sc, s);
+  else if (key_width == 8) partition_impl<int64_t>((const int64_t*)keys, n, world, cols, counts_host, sc, s);
+  else throw std::invalid_argument("partition keys must be 4- or 8-byte integers");
+}
+
+}  // namespace sm

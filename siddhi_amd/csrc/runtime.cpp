@@ -28,6 +28,7 @@
 #include "kernels/nfa.h"
 #include "kernels/primitives.h"
 #include "kernels/stream_ops.h"
+#include "kernels/partition.h"
 #include "siddhiql/ast.h"
 
 namespace sm {
@@ -1316,6 +1317,34 @@ int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
       }
     }
     if (r.o != len) throw std::runtime_error("CannotRestoreSiddhiAppStateException: trailing bytes");
+  });
+}
+
+// Multi-GPU key exchange helper (no app handle): stable partition of a device batch by owner rank.
+int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t world, int ncols,
+                          const int32_t* widths, const void* const* d_src, void* const* d_dst, uint64_t* counts,
+                          void* hip_stream) {
+  static std::mutex mu;
+  static sm::DBuf scratch;
+  static sm::Scratch sc;
+  std::lock_guard<std::mutex> g(mu);
+  return guarded([&] {
+    if (ncols < 0 || ncols > sm::kMaxPartCols) throw std::invalid_argument("ncols out of range");
+    sm::PartCols pc{};
+    pc.n = ncols;
+    for (int c = 0; c < ncols; ++c) {
+      if (widths[c] != 1 && widths[c] != 2 && widths[c] != 4 && widths[c] != 8)
+        throw std::invalid_argument("column width must be 1, 2, 4 or 8 bytes");
+      pc.width[c] = widths[c];
+      pc.src[c] = d_src[c];
+      pc.dst[c] = d_dst[c];
+    }
+    const size_t need = (size_t)world * ((n + 4095) / 4096 + 1) * 4 + (16 << 20);
+    if (scratch.cap < need) scratch.ensure(need);
+    sc.base = (char*)scratch.p;
+    sc.cap = scratch.cap;
+    sc.used = 0;
+    sm::partition_by_owner(d_keys, key_width, (int64_t)n, world, pc, counts, sc, (hipStream_t)hip_stream);
   });
 }
 

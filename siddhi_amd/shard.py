@@ -19,23 +19,46 @@ def owner_of(keys: torch.Tensor, world: int) -> torch.Tensor:
     return torch.remainder(keys.to(torch.int64), world)
 
 
+def partition_by_owner(keys: torch.Tensor, columns, world: int):
+    """Stable partition of `columns` by owner rank: (partitioned columns, per-owner counts). On the GPU this is
+    the HIP counting sort of the native library (sm_app partition kernel, one read of the key + one read and
+    write of each column); host tensors (the gloo CPU tests) take the equivalent torch form."""
+    if keys.is_cuda:
+        import ctypes
+        from siddhi_amd import _lib
+        n = keys.numel()
+        outs = [torch.empty_like(c) for c in columns]
+        k = len(columns)
+        widths = (ctypes.c_int32 * k)(*[c.element_size() for c in columns])
+        src = (ctypes.c_void_p * k)(*[c.data_ptr() for c in columns])
+        dst = (ctypes.c_void_p * k)(*[o.data_ptr() for o in outs])
+        counts = (ctypes.c_uint64 * world)()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(keys.device).cuda_stream)
+        rc = _lib.lib().sm_partition_by_owner(keys.data_ptr(), keys.element_size(), n, world, k, widths, src, dst,
+                                              counts, stream)
+        if rc != _lib.SM_OK:
+            raise RuntimeError(_lib.lib().sm_last_error().decode(errors="replace"))
+        return outs, [int(c) for c in counts]
+    owner = owner_of(keys, world)
+    order = torch.argsort(owner, stable=True)
+    return [c[order] for c in columns], torch.bincount(owner, minlength=world).tolist()
+
+
 def exchange_by_key(keys: torch.Tensor, columns, world: int, group=None):
     """All-to-all-v of `columns` (list of 1-D tensors aligned with `keys`) so that each rank receives the rows
     whose key it owns. Returns (received columns, received counts per source rank). Row order in the result:
     by source rank, then original order — i.e. global arrival order when rank r holds the r-th contiguous slice."""
     if world == 1:
         return list(columns), [keys.numel()]
-    owner = owner_of(keys, world)
-    order = torch.argsort(owner, stable=True)
-    send_counts = torch.bincount(owner, minlength=world)
+    parted, sc = partition_by_owner(keys, columns, world)
+    send_counts = torch.tensor(sc, dtype=torch.int64, device=keys.device)
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
-    nrecv = sum(rc)
+    rc = recv_counts.tolist()
     out = []
-    for col in columns:
-        buf = torch.empty(nrecv, dtype=col.dtype, device=col.device)
-        dist.all_to_all_single(buf, col[order].contiguous(), rc, sc, group=group)
+    for col in parted:
+        buf = torch.empty(sum(rc), dtype=col.dtype, device=col.device)
+        dist.all_to_all_single(buf, col, rc, sc, group=group)
         out.append(buf)
     return out, rc
 
