@@ -233,7 +233,7 @@ def main():
     import torch
     import torch.distributed as dist
     from siddhi_amd.testing import ProductApp
-    from siddhi_amd.shard import exchange_by_key
+    from siddhi_amd.shard import exchange_with_ordinals
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -269,8 +269,8 @@ def main():
             # a fresh runtime of the app per step (state dropped, device allocations kept), then the batch
             app.set_option("reset", 1)
             if world > 1:
-                (s_sym, s_price, s_ts, s_ord, s_sid), _ = exchange_by_key(symbol, [symbol, price, ts, ordinals, sidx],
-                                                                          world)
+                (s_sym, s_price, s_ts, s_sid), s_ord, _ = exchange_with_ordinals(symbol, [symbol, price, ts, sidx],
+                                                                                 world, lo)
                 s_sid, s_ts, (s_sym, s_price), s_ord = merge_ticks(s_sid, s_ts, [s_sym, s_price], s_ord, ticks)
             else:
                 s_sym, s_price, s_ts, s_ord, s_sid = symbol, price, ts, ordinals, sidx
@@ -280,7 +280,7 @@ def main():
                                       hip_stream=hip_stream)
             return int(app.get_stat("output_events:q"))
         if args.config == 4 and world > 1:
-            (s_sym, s_price, s_ts, s_ord), _ = exchange_by_key(symbol, [symbol, price, ts, ordinals], world)
+            (s_sym, s_price, s_ts), s_ord, _ = exchange_with_ordinals(symbol, [symbol, price, ts], world, lo)
         elif args.config == 4:
             s_sym, s_price, s_ts, s_ord = symbol, price, ts, None
         else:

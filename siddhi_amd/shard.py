@@ -63,6 +63,25 @@ def exchange_by_key(keys: torch.Tensor, columns, world: int, group=None):
     return out, rc
 
 
+def exchange_with_ordinals(keys: torch.Tensor, columns, world: int, lo: int, group=None):
+    """exchange_by_key plus the global arrival ordinal of every received row. The ordinal is not shipped as an
+    int64: each row carries its uint32 offset inside its source rank's contiguous slice, and the receiver adds
+    the source slice's first ordinal (all-gathered once), saving 4 of the bytes per event that cross xGMI.
+    Returns (received columns, received int64 ordinals, received counts per source rank)."""
+    n = keys.numel()
+    if world == 1:
+        return list(columns), torch.arange(lo, lo + n, dtype=torch.int64, device=keys.device), [n]
+    if n >= 2**31:
+        raise ValueError("exchange_with_ordinals: more than 2^31 events in one rank's slice")
+    off = torch.arange(n, dtype=torch.int32, device=keys.device)
+    out, rc = exchange_by_key(keys, list(columns) + [off], world, group=group)
+    los = torch.tensor([lo], dtype=torch.int64, device=keys.device)
+    all_lo = [torch.empty_like(los) for _ in range(world)]
+    dist.all_gather(all_lo, los, group=group)
+    base = torch.repeat_interleave(torch.cat(all_lo), torch.tensor(rc, device=keys.device))
+    return out[:-1], base + out[-1].to(torch.int64), rc
+
+
 def merge_matches(parts):
     """Merge per-rank match tuples (each an (n, 2) int array of global (e1, e2) ordinals in reference order for
     that rank's keys) into the reference's global order: by e2 ordinal; ties (same e2) come from one rank and

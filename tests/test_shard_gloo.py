@@ -52,6 +52,10 @@ def _worker(rank, world, port, outfile):
         assert sum(counts) == r_ord.numel()
         ords = r_ord.numpy()
         assert (np.diff(ords) > 0).all(), "received rows not in global arrival order"
+        from siddhi_amd.shard import exchange_with_ordinals
+        (w_sym, w_price), w_ord, w_counts = exchange_with_ordinals(t[0], [t[0], t[1]], world, lo)
+        assert w_counts == counts and torch.equal(w_ord, r_ord)
+        assert torch.equal(w_sym, r_sym) and torch.equal(w_price, r_price)
         assert (np.remainder(r_sym.numpy(), world) == rank).all()
         local = oracle_refs([r_sym.numpy(), r_price.numpy(), r_vol.numpy(), r_tsa.numpy()], r_ts.numpy())
         glob = ords[local] if len(local) else local
