@@ -68,6 +68,7 @@ constexpr int kWalkTile = kWalkBlock * kWalkItems;  // 1024 records per walk til
 constexpr int kWalkHalo = 256;                      // records staged past the tile for scans that leave it
 constexpr int kWalkLds = kWalkTile + kWalkHalo;
 constexpr int kWalkWaves = kWalkBlock / 64;
+constexpr int kUnkeyedBudget = 32;  // private (per-lane) scan steps of an unkeyed record before the wave helps
 constexpr uint32_t kNanCode = 0xffffffffu;  // value code of a NaN (FLOAT / DOUBLE): always compared exactly
 
 // value-code modes
@@ -1186,6 +1187,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
     int64_t tu = 0;
     uint32_t key = 0, cu = 0, ou = 0;
     bool live = false;
+    int vstart = 0;
     auto take = [&]() {
       live = todo != 0;
       k = live ? __ffs(todo) - 1 : 0;
@@ -1202,11 +1204,14 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
         vu = L.v[lu];
       }
       v = lu + 1;
+      vstart = v;
     };
     SM_STAMP(2);
     take();
     while (__any(live)) {
-      const bool inb = v < lend;
+      // unkeyed scans run until c2 holds or the window closes (up to window-many events: no key run bounds them),
+      // so a lane scans privately for kUnkeyedBudget records and leaves the rest to the wave-cooperative finish
+      const bool inb = v < lend && (KEYED || v - vstart < kUnkeyedBudget);
       const int vv = inb ? v : lend - 1;
       bool stop, hit;
       if constexpr (KEYED) {
@@ -1233,6 +1238,44 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       if (done) take();
     }
     SM_STAMP(3);
+    if constexpr (!KEYED) {
+      // wave-cooperative finish of the open scans: one scan at a time, 64 consecutive candidates per step (one
+      // ballot each), so a window of W events costs W / 64 steps instead of W steps on one lane
+      uint64_t pend = __ballot(openm != 0);
+#pragma unroll 1
+      while (pend) {
+        const int src = __ffsll((unsigned long long)pend) - 1;
+        const uint32_t om = __shfl(openm, src, 64);
+        const int kk = __ffs(om) - 1;
+        const int luu = w * 64 * kWalkItems + kk * 64 + src;
+        const int64_t t0 = L.t[luu];
+        const uint64_t v0 = L.v[luu];
+        int64_t found = -1;
+        for (int64_t p = base + sj[kk][w * 64 + src]; p < n; p += 64) {
+          const int64_t q = p + lane;
+          bool stp = q >= n, hit = false;
+          if (!stp) {
+            const int64_t d = a.ts[q] - t0;
+            stp = a.within >= 0 && (d < 0 ? -d : d) > a.within;
+            if (!stp) hit = c2(v0, canon(col_value(a.st, a.vattr, q), a.vtype));
+          }
+          const uint64_t hb = __ballot(hit), any = __ballot(stp) | hb;
+          if (any) {
+            const int f = __ffsll((unsigned long long)any) - 1;
+            if ((hb >> f) & 1ull) found = p + f;
+            break;
+          }
+        }
+        if (lane == src) {
+          if (found >= 0) {
+            hasm |= 1u << kk;
+            sj[kk][threadIdx.x] = (uint32_t)(found - base);
+          }
+          openm &= ~(1u << kk);
+        }
+        pend = __ballot(openm != 0);
+      }
+    }
     // scans that ran past the staged records
 #pragma unroll 1
     while (openm) {
