@@ -6,7 +6,7 @@
 # Stops at the first step that faults or times out.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out
+OUT=$ROOT/gpurun_out/${PROF_DIR:-.}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {  # step <name> <seconds> <cmd...>

@@ -7,7 +7,7 @@
 
 HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE come from separate rocprofv3 --pmc
 runs; FETCH_SIZE is doubled (gfx950 tallies 128-B requests of wide streaming reads at 64 B), WRITE_SIZE is taken as
-reported; both are KB (x 1024). Usage: python tools/summarize_profile.py <tag> [config]"""
+reported; both are KB (x 1024). Usage: [PROF_DIR=<sub>] python tools/summarize_profile.py <tag> [config]"""
 import csv
 import glob
 import json
@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import alg_bytes  # noqa: E402
 
-OUT = os.path.join(ROOT, "gpurun_out")
+OUT = os.path.join(ROOT, "gpurun_out", os.environ.get("PROF_DIR", "."))
 # kernel-name fragment -> bench label (first match wins)
 FAMILIES = [("walk_kernel<", "walk"), ("downsweep_wc_kernel<0", "key_pass0"), ("downsweep_kernel<0", "key_pass0"),
             ("downsweep_wc_kernel<1", "key_pass"), ("downsweep_kernel<1", "key_pass"),
