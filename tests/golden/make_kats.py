@@ -13,6 +13,8 @@ Thread-based sends, ...) are listed with a reason and skipped.
 import json
 import os
 import re
+
+import java_builder  # noqa: E402 (same directory)
 import struct
 import sys
 
@@ -160,6 +162,12 @@ def extract(path, name, ann, body, line):
         try:
             env[m.group(1)] = eval_concat(m.group(2), env)
         except ValueError as e:
+            kat["skip"] = str(e)
+            return kat
+    if "new SiddhiApp(" in body or "SiddhiApp.siddhiApp(" in body:
+        try:  # programmatic query API (FilterTestCase1/2): transcribe the builders into SiddhiQL text
+            env.update(java_builder.builder_apps(body))
+        except java_builder.Unsupported as e:
             kat["skip"] = str(e)
             return kat
     m = re.search(r"createSiddhiAppRuntime\(([^;]*)\);", body)
