@@ -191,6 +191,96 @@ def cpu_baseline(sample, K, ts_div, app_text, seed, out_stream, config=4):
     return sample / dt, dt, m
 
 
+def cpu_shards(config, sample, K, ts_div, seed, threads):
+    """The sample split for the multi-threaded CPU baseline (SURVEY.md §8(d) variant (b)): partitioned configs
+    (4, 5) by key, `symbol % threads` (keys are independent: PartitionRuntime.java:262-309), so each thread runs
+    the oracle app on its own key subset; config 2 by contiguous index range. Config 5 is @app:playback: the
+    event-time clock is global, so each thread also replays the other threads' clock-advance points as
+    heartbeats (stream -1), exactly as a rank of the multi-GPU path does. Returns a list of per-thread
+    (kind, args) ready for the oracle entry points."""
+    import numpy as np
+    if config == 5:
+        import synth
+        sid, cols, ts = synth.gen5(0, sample, K, ts_div, seed)
+        first = np.ones(sample, dtype=bool)
+        first[1:] = ts[1:] > ts[:-1]
+        out = []
+        for t in range(threads):
+            mine = (cols[0] % threads) == t
+            keep = mine | first
+            s = np.where(mine, sid, -1)[keep].astype(np.int32)
+            out.append(("interleaved", (s, ts[keep], [c[keep] for c in cols])))
+        return out
+    sym, price, vol, ts_attr, ts = gen_stock_numpy(0, sample, K, ts_div, seed)
+    cols = [sym, price, vol, ts_attr]
+    out = []
+    for t in range(threads):
+        if config == 2:
+            lo, hi = sample * t // threads, sample * (t + 1) // threads
+            sel = slice(lo, hi)
+        else:
+            sel = (sym % threads) == t
+        out.append(("columns", (ts[sel], [np.ascontiguousarray(c[sel]) for c in cols])))
+    return out
+
+
+def cpu_baseline_threads(sample, K, ts_div, app_text, seed, out_stream, config, threads):
+    """The CPU oracle on `threads` host threads, one app per shard (cpu_shards). The oracle's C entry points
+    run without the GIL (ctypes), so the shards run in parallel. Timed from the release of all threads to the
+    last one's return; the split itself is not timed (the generous baseline). Returns (events/s, s, matches)."""
+    import threading
+    import numpy as np
+    from oracle_lib import OracleApp, lib
+    shards = cpu_shards(config, sample, K, ts_div, seed, threads)
+    apps = []
+    for _ in shards:
+        a = OracleApp(app_text)
+        a.set_collect(False)
+        a.start()
+        apps.append(a)
+    errs = []
+    go = threading.Barrier(len(shards) + 1)
+
+    def work(app, kind, args):
+        go.wait()
+        try:
+            if kind == "interleaved":
+                app.send_interleaved(*args)
+            else:
+                ts, cols = args
+                ptrs = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+                err = ctypes.create_string_buffer(512)
+                ts = np.ascontiguousarray(ts)
+                rc = lib().cr_send_columns(app.h, app.stream_index("StockStream"), ts.size, ts.ctypes.data, ptrs,
+                                           err, 512)
+                if rc != 0:
+                    raise RuntimeError(err.value.decode())
+        except Exception as e:  # noqa: BLE001 — reported after join
+            errs.append(e)
+
+    ths = [threading.Thread(target=work, args=(a, k, x)) for a, (k, x) in zip(apps, shards)]
+    for th in ths:
+        th.start()
+    go.wait()
+    t0 = time.perf_counter()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    m = sum(a.output_count(out_stream) for a in apps)
+    for a in apps:
+        a.close()
+    return sample / dt, dt, m
+
+
+def host_threads():
+    """Host threads for the multi-threaded baseline: the box's CPU share (OMP_NUM_THREADS is set to it on the
+    GPU box; os.cpu_count() there shows the whole machine)."""
+    n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n)), 16))
+
+
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
@@ -339,6 +429,18 @@ def main():
         cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port",
                "sample": f"first {sample} events of the same stream through oracle/cpu_ref "
                          f"(C++ restatement of the reference engine, 1 thread): {sec:.2f} s, {mm} matches"}
+        nt = host_threads() if args.config != 3 else 1  # config 3 is one non-partitioned app: no split
+        if nt > 1:
+            # the generous baseline, the same sample split over host threads
+            log(f"cpu baseline on {sample} events, {nt} threads")
+            vt, sect, mt = cpu_baseline_threads(sample, K, ts_div, cfg["app"], seed, cfg["out"], args.config, nt)
+            if mt != mm:
+                raise RuntimeError(f"threaded CPU baseline found {mt} matches, 1 thread {mm}")
+            cpu = {"value": vt, "unit": "events/s", "cores": nt, "kind": "port",
+                   "sample": f"first {sample} events of the same stream through oracle/cpu_ref on {nt} host threads, "
+                             f"one app per {'key shard (symbol % threads)' if args.config in (4, 5) else 'index range'}"
+                             f"{' + global clock heartbeats' if args.config == 5 else ''}: {sect:.2f} s, {mt} matches",
+                   "single_thread": {"value": v, "cores": 1, "seconds": sec}}
     if rank == 0:
         alg = cfg["job_bytes"](N, total_matches) * (1 if cfg["shards"] else world)
         conf = {"workload": cfg["workload"], "config": args.config, "events": N,

@@ -1937,6 +1937,10 @@ int cr_send_interleaved(cr_app* app, size_t n, const int32_t* stream_idx, const 
   try {
     for (size_t i = 0; i < n; ++i) {
       int si = stream_idx[i];
+      if (si == -1) {  // playback heartbeat (the device batch's stream -1): clock only, no event
+        advance_clock(a, ts[i]);
+        continue;
+      }
       if (si < 0 || si >= (int)a->streams.size()) throw RuntimeError("bad stream index");
       send_row(a, si, ts[i], row_from_columns(a, a->streams[si].def, cols, i));
     }

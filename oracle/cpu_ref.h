@@ -38,7 +38,8 @@ int cr_send(cr_app* app, int stream_index, int64_t ts, const cr_value* row, char
  * attribute column (int32_t*, int64_t*, float*, double*; strings unsupported here). */
 int cr_send_columns(cr_app* app, int stream_index, size_t n, const int64_t* ts, const void* const* cols,
                     char* err, size_t errlen);
-/* interleaved batch over streams sharing one schema: event i -> stream stream_idx[i] */
+/* interleaved batch over streams sharing one schema: event i -> stream stream_idx[i];
+ * stream_idx[i] == -1 is a playback heartbeat at ts[i] (as cr_advance_time; its columns are not read) */
 int cr_send_interleaved(cr_app* app, size_t n, const int32_t* stream_idx, const int64_t* ts, const void* const* cols,
                         char* err, size_t errlen);
 /* Outputs collected since creation, as JSON text:
