@@ -6,7 +6,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsiddhi_amd.so")
+# SM_LIB_VARIANT=<dir> loads siddhi_amd/<dir>/libsiddhi_amd.so instead (A/B builds of the same sources)
+LIB_PATH = os.path.join(HERE, os.environ.get("SM_LIB_VARIANT", "lib"), "libsiddhi_amd.so")
 
 SM_OK, SM_E_PARSE, SM_E_VALIDATION, SM_E_UNSUPPORTED, SM_E_TYPE, SM_E_DEVICE, SM_E_RUNTIME, SM_E_ARG = range(8)
 TYPE_CODES = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3, "STRING": 4, "BOOL": 5}

@@ -528,6 +528,32 @@ CompiledQuery compile_query(const App& app, const Query& q, int order, int parti
     for (auto& r : recvs)
       if (r.multi) std::reverse(r.procs, r.procs + r.nproc);
     h.root_inner = root;
+    // resetAndUpdate visiting orders (NextInnerStateRuntime.java:58-68: next.reset() then current.reset(),
+    // current.update() then next.update(); LogicalInnerStateRuntime.java:62-70: inner2 only; Stream / Count /
+    // Every: the first pre processor), flattened so the device loops over a constant list per event
+    auto flatten = [&](bool reset, int32_t* out, int32_t& n) {
+      std::vector<int> st{root};
+      n = 0;
+      while (!st.empty()) {
+        const DInner& d = lw.inners[st.back()];
+        st.pop_back();
+        switch (d.kind) {
+          case IK_STREAM:
+          case IK_COUNT:
+          case IK_EVERY:
+            if (n >= 2 * kMaxSlots) throw UnsupportedError("inner runtime too large");
+            out[n++] = d.first;
+            break;
+          case IK_NEXT:
+            if (reset) { st.push_back(d.a); st.push_back(d.b); }
+            else { st.push_back(d.b); st.push_back(d.a); }
+            break;
+          default: st.push_back(d.b); break;
+        }
+      }
+    };
+    flatten(true, h.reset_seq, h.nreset);
+    flatten(false, h.update_seq, h.nupdate);
     // selector (SelectorParser :140-200): currentState UNKNOWN, default chain index 0
     Emitter em{dict, lw.code, lw.consts};
     em.metas = &lw.metas;

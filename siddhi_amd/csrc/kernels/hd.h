@@ -29,6 +29,10 @@ inline long long __double_as_longlong(double d) {
   memcpy(&x, &d, 8);
   return x;
 }
+struct longlong2 {
+  long long x, y;
+};
+inline longlong2 make_longlong2(long long x, long long y) { return {x, y}; }
 inline double __longlong_as_double(long long x) {
   double d;
   memcpy(&d, &x, 8);

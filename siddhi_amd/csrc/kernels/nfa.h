@@ -25,7 +25,11 @@ struct NfaStream {
 // image the NFA copies into a partial (word 0 unused, ts, ordinal, null mask, attribute words).
 struct LaneEv {
   enum : int { kPos = 0, kStream = 1, kClock = 2, kUpto = 3, kNode = 4 };
-  static __host__ __device__ constexpr int64_t words(int node_words) { return kNode + node_words; }
+  // padded to whole 64-byte halves / 128-byte lines: the lane-events pass scatters records to key order, and a
+  // record that fills its lines is written without a partial-line merge in HBM (96 -> 128 B for StockStream)
+  static __host__ __device__ constexpr int64_t words(int node_words) {
+    return kNode + node_words <= 8 ? 8 : (kNode + node_words + 15) / 16 * 16;
+  }
 };
 
 struct NfaBatch {

@@ -866,39 +866,6 @@ struct Lane {
     }
   }
 
-  // ------------------------------------------------------------ inner runtime reset/update (sequences)
-  __device__ void inner_reset(int in) {
-    // recursion depth bounded by the pattern size; explicit stack for the device
-    int st[32];
-    int sp = 0;
-    st[sp++] = in;
-    while (sp) {
-      const DInner& d = inner[st[--sp]];
-      switch (d.kind) {
-        case IK_STREAM:
-        case IK_COUNT:
-        case IK_EVERY: resetState(d.first); break;  // EveryInnerStateRuntime inherits Stream's reset
-        case IK_NEXT: st[sp++] = d.a; st[sp++] = d.b; break;  // next.reset() then current.reset()
-        default: st[sp++] = d.b; break;                         // Logical: inner2 only
-      }
-    }
-  }
-  __device__ void inner_update(int in) {
-    int st[32];
-    int sp = 0;
-    st[sp++] = in;
-    while (sp) {
-      const DInner& d = inner[st[--sp]];
-      switch (d.kind) {
-        case IK_STREAM:
-        case IK_COUNT:
-        case IK_EVERY: updateState(d.first); break;
-        case IK_NEXT: st[sp++] = d.b; st[sp++] = d.a; break;  // current.update() then next.update()
-        default: st[sp++] = d.b; break;
-      }
-    }
-  }
-
   // ------------------------------------------------------------ garbage collection (Cheney, safe points only)
   __device__ int32_t fwd(int32_t o, int64_t& top) {
     if (o < 0) return o;
@@ -962,8 +929,8 @@ struct Lane {
     int64_t now = r[LaneEv::kNode + 1];
     // stabilizeStates
     if (q->kind == 2) {
-      inner_reset(q->root_inner);
-      inner_update(q->root_inner);
+      for (int k = 0; k < q->nreset; ++k) resetState(q->reset_seq[k]);  // inner reset(), flattened (plan.h)
+      for (int k = 0; k < q->nupdate; ++k) updateState(q->update_seq[k]);
     } else if (R->multi) {
       for (int k = 0; k < R->nstate; ++k) updateState(R->stateProcs[k]);
     } else if (R->nstate > 0) {
@@ -1057,10 +1024,48 @@ __device__ int64_t gallop(const int64_t* __restrict__ v, int64_t from, int64_t n
 
 // Record k of the query's batch, in key order, as its LaneEv record (nfa.h): a lane then reads one contiguous
 // record per event instead of chasing key_pos -> stream / row / ts / clock / ordinal / columns.
+__device__ __forceinline__ int64_t lane_attr(const NfaStream& st, int a, int64_t row, int64_t& nulls) {
+  int64_t v = 0;
+  bool isnull = st.nulls[a] && st.nulls[a][row];
+  switch (st.types[a]) {
+    case T_INT: v = ((const int32_t*)st.cols[a])[row]; break;
+    case T_LONG: v = ((const int64_t*)st.cols[a])[row]; break;
+    case T_FLOAT: { double d = (double)((const float*)st.cols[a])[row]; v = __double_as_longlong(d); break; }
+    case T_DOUBLE: v = __double_as_longlong(((const double*)st.cols[a])[row]); break;
+    case T_STRING: v = ((const int32_t*)st.cols[a])[row]; isnull = isnull || v < 0; break;
+    default: v = ((const uint8_t*)st.cols[a])[row]; break;
+  }
+  if (isnull) nulls |= (1ll << a);
+  return v;
+}
+
 __device__ __forceinline__ void lane_event_record(const NfaBatch& b, int64_t p, int64_t k, int32_t node_words,
                                                   int64_t* __restrict__ out) {
-  int64_t* r = out + k * LaneEv::words(node_words);
+  const int64_t W = LaneEv::words(node_words);
+  int64_t* r = out + k * W;
   const int s = b.ev_stream[p];
+  const NfaStream* st = s >= 0 ? &b.streams[s] : nullptr;
+  const int na = st ? st->nattr : 0;
+  const int64_t row = st ? b.ev_row[p] : 0;
+  if (W == 16) {
+    // the common shape (<= 8 attributes): the record in registers, one full 128-byte line in 16-byte stores
+    int64_t v[16];
+    int64_t nulls = 0;
+    v[LaneEv::kPos] = p;
+    v[LaneEv::kStream] = s;
+    v[LaneEv::kClock] = b.ev_clock[p];
+    v[LaneEv::kUpto] = b.adv_upto ? b.adv_upto[p] : -1;
+    v[LaneEv::kNode] = 0;
+    v[LaneEv::kNode + 1] = b.ev_ts[p];
+    v[LaneEv::kNode + 2] = b.ev_ord[p];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) v[LaneEv::kNode + 4 + a] = (a < na) ? lane_attr(*st, a, row, nulls) : 0;
+    v[LaneEv::kNode + 3] = nulls;
+    longlong2* r2 = (longlong2*)r;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) r2[w] = make_longlong2(v[2 * w], v[2 * w + 1]);
+    return;
+  }
   r[LaneEv::kPos] = p;
   r[LaneEv::kStream] = s;
   r[LaneEv::kClock] = b.ev_clock[p];
@@ -1070,28 +1075,9 @@ __device__ __forceinline__ void lane_event_record(const NfaBatch& b, int64_t p, 
   node[1] = b.ev_ts[p];
   node[2] = b.ev_ord[p];
   int64_t nulls = 0;
-  int na = 0;
-  if (s >= 0) {
-    const NfaStream& st = b.streams[s];
-    const int64_t row = b.ev_row[p];
-    na = st.nattr;
-    for (int a = 0; a < na; ++a) {
-      int64_t v = 0;
-      bool isnull = st.nulls[a] && st.nulls[a][row];
-      switch (st.types[a]) {
-        case T_INT: v = ((const int32_t*)st.cols[a])[row]; break;
-        case T_LONG: v = ((const int64_t*)st.cols[a])[row]; break;
-        case T_FLOAT: { double d = (double)((const float*)st.cols[a])[row]; v = __double_as_longlong(d); break; }
-        case T_DOUBLE: v = __double_as_longlong(((const double*)st.cols[a])[row]); break;
-        case T_STRING: v = ((const int32_t*)st.cols[a])[row]; isnull = isnull || v < 0; break;
-        default: v = ((const uint8_t*)st.cols[a])[row]; break;
-      }
-      if (isnull) nulls |= (1ll << a);
-      node[4 + a] = v;
-    }
-  }
+  for (int a = 0; a < na; ++a) node[4 + a] = lane_attr(*st, a, row, nulls);
   node[3] = nulls;
-  for (int w = 4 + na; w < node_words; ++w) node[w] = 0;
+  for (int64_t w = LaneEv::kNode + 4 + na; w < W; ++w) r[w] = 0;  // padding too: whole lines are written
 }
 
 // First advance point after position x, at or after index `from`: O(1) through the per-position count of

@@ -106,6 +106,10 @@ struct DQuery {
   int32_t nslots;       // state slots (meta stream events)
   int32_t npre, npost, ninner, nrecv, nsched, nwithin;
   int32_t root_inner;
+  // StateStreamRuntime.resetAndUpdate (sequences, StateStreamRuntime.java:90-93) flattened at compile time:
+  // the pre processors inner reset() then update() visit, in the order the inner-runtime tree visits them
+  int32_t nreset, nupdate;
+  int32_t reset_seq[2 * kMaxSlots], update_seq[2 * kMaxSlots];
   int32_t nsel;         // output attributes
   int32_t nrefs;        // select variable references (parity tuples)
   int32_t nconst;
