@@ -35,7 +35,7 @@ int64_t select_records(const int32_t* ev_stream, int64_t n, uint64_t stream_mask
                        Scratch& sc, hipStream_t s);
 int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* ev_stream, const int64_t* ev_row,
                      const NfaStream* streams_dev, const KeyProg* progs_dev, int nprogs, int64_t** key_pos_out,
-                     int64_t** key_off_out, Scratch& sc, hipStream_t s);
+                     int64_t** key_off_out, Scratch& sc, hipStream_t s, bool pos_identity = false);
 
 // Per-event index arrays of a device-resident interleaved batch (the device restatement of stage_record);
 // returns the number of clock-advance points written to adv_*.

@@ -289,7 +289,7 @@ __global__ void assign_new_slots_kernel(const uint64_t* __restrict__ sk, const u
   uint32_t run = run_excl[i] + (start ? 1u : 0u) - 1u;  // inclusive count - 1
   int32_t slot = base + (int32_t)run;
   uint32_t m = sidx[i];  // index into the missing list
-  if (slot_out) slot_out[missing_map[m]] = slot;
+  if (slot_out) slot_out[missing_map ? missing_map[m] : m] = slot;
   if (start) {
     new_keys[run] = keys_of_missing[m];
     new_slots[run] = slot;
@@ -305,7 +305,9 @@ __global__ void all_new_csr_kernel(const uint64_t* __restrict__ sk, const uint32
                                    int64_t* __restrict__ key_pos, int64_t* __restrict__ key_off) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  key_pos[j] = pos[missing_map[sidx[j]]];
+  const uint32_t m = sidx[j];
+  const uint32_t x = missing_map ? missing_map[m] : m;  // no map: the missing list is the whole batch
+  key_pos[j] = pos ? pos[x] : x;                        // no pos: every batch record is the query's
   const bool start = (j == 0 || sk[j] != sk[j - 1]);
   if (start) key_off[base + run_excl[j]] = j;
   if (j == n - 1) key_off[base + run_excl[j] + (start ? 1 : 0)] = n;  // one past the last run
@@ -614,7 +616,7 @@ int64_t select_records(const int32_t* ev_stream, int64_t n, uint64_t stream_mask
 // all `*nslots` slots) are written into buffers from `sc` (valid until the caller releases the scratch).
 int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* ev_stream, const int64_t* ev_row,
                      const NfaStream* streams_dev, const KeyProg* progs_dev, int nprogs, int64_t** key_pos_out,
-                     int64_t** key_off_out, Scratch& sc, hipStream_t s) {
+                     int64_t** key_off_out, Scratch& sc, hipStream_t s, bool pos_identity) {
   int64_t* keys = (int64_t*)sc.take(std::max<int64_t>(n, 1) * 8);
   uint8_t* valid = (uint8_t*)sc.take(std::max<int64_t>(n, 1));
   int32_t* slot = (int32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
@@ -637,15 +639,21 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
     int64_t* fast_pos = all_new ? (int64_t*)sc.take((size_t)n * 8) : nullptr;
     int64_t* fast_off = all_new ? (int64_t*)sc.take(((size_t)base + hm + 2) * 8) : nullptr;
     size_t mark = sc.used;
-    uint8_t* f = (uint8_t*)sc.take(n);
-    uint32_t* ex = (uint32_t*)sc.take(n * 4);
-    hipLaunchKernelGGL(missing_flags_kernel, grid_for(n), dim3(256), 0, s, slot, n, f);
-    hipLaunchKernelGGL(u8_to_u32_kernel, grid_for(n), dim3(256), 0, s, f, n, ex);
-    exclusive_scan_u32(ex, n, sc, s);
-    uint32_t* miss = (uint32_t*)sc.take(hm * 4);
-    hipLaunchKernelGGL(compact_flag_kernel<uint32_t>, grid_for(n), dim3(256), 0, s, f, ex, n, miss);
-    int64_t* mkeys = (int64_t*)sc.take(hm * 8);
-    hipLaunchKernelGGL(gather_i64_kernel, grid_for(hm), dim3(256), 0, s, keys, miss, (int64_t)hm, mkeys);
+    // the missing list (records whose key is not in the table) and its keys; when every record misses, it is
+    // the whole batch in order (miss = identity: no compaction, no gathers)
+    uint32_t* miss = nullptr;
+    int64_t* mkeys = keys;
+    if (!all_new) {
+      uint8_t* f = (uint8_t*)sc.take(n);
+      uint32_t* ex = (uint32_t*)sc.take(n * 4);
+      hipLaunchKernelGGL(missing_flags_kernel, grid_for(n), dim3(256), 0, s, slot, n, f);
+      hipLaunchKernelGGL(u8_to_u32_kernel, grid_for(n), dim3(256), 0, s, f, n, ex);
+      exclusive_scan_u32(ex, n, sc, s);
+      miss = (uint32_t*)sc.take(hm * 4);
+      hipLaunchKernelGGL(compact_flag_kernel<uint32_t>, grid_for(n), dim3(256), 0, s, f, ex, n, miss);
+      mkeys = (int64_t*)sc.take(hm * 8);
+      hipLaunchKernelGGL(gather_i64_kernel, grid_for(hm), dim3(256), 0, s, keys, miss, (int64_t)hm, mkeys);
+    }
     unsigned long long* mm = (unsigned long long*)sc.take(16);
     unsigned long long init[2] = {~0ull, 0ull};
     SM_HIP(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, s));
@@ -684,7 +692,8 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
     T.nslots += hr;
     if (all_new) {
       SM_HIP(hipMemsetAsync(fast_off, 0, ((size_t)base + 1) * 8, s));
-      hipLaunchKernelGGL(all_new_csr_kernel, grid_for(hm), dim3(256), 0, s, sk, si, runs, miss, pos, (int64_t)hm, base,
+      hipLaunchKernelGGL(all_new_csr_kernel, grid_for(hm), dim3(256), 0, s, sk, si, runs, miss,
+                         pos_identity ? nullptr : pos, (int64_t)hm, base,
                          fast_pos, fast_off);
       sc.used = mark;
       *key_pos_out = fast_pos;

@@ -512,7 +512,7 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   if (partitioned) {
     int64_t nv = group_by_key(q.keys, pos, nq, ev.ev_stream, ev.ev_row,
                               ev.streams, (const KeyProg*)q.keyprogs.p, q.nkeyprogs, &key_pos,
-                              &key_off, a->sc, hs);
+                              &key_off, a->sc, hs, nq == N /* select_records kept every position: pos[i] = i */);
     nq = nv;
     nkeys = q.keys.nslots;
   } else {
