@@ -5,7 +5,14 @@
 namespace sm {
 namespace {
 
-__global__ void nfa_kernel(NfaBatch b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
+// SM_NFA_WAVES (A/B builds): minimum waves per SIMD the register allocator must leave room for
+#ifdef SM_NFA_WAVES
+#define SM_NFA_ATTR __attribute__((amdgpu_waves_per_eu(SM_NFA_WAVES)))
+#else
+#define SM_NFA_ATTR
+#endif
+
+__global__ SM_NFA_ATTR void nfa_kernel(NfaBatch b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
                            int32_t heap_half, int64_t lanes, int32_t nkeys, int32_t* err_out) {
   int key = blockIdx.x * blockDim.x + threadIdx.x;
   if (key >= nkeys) return;
