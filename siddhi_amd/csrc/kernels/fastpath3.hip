@@ -435,6 +435,29 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
     }
     if constexpr (MASK) {
       const Cond c1 = make_cond(c1code, c1len, consts);
+      if (c1.simple) {
+        // `x CMP y`: every operand load of the tile issued before the first compare (the interpreter loop below
+        // waits on one row's loads at a time)
+        StackVal l[kItems], r[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+          const int64_t p = base + w * 64 * kItems + k * 64 + lane;
+          if (p < hi0) {
+            const RowLoader ld{st, p};
+            l[k] = c1.a.op == OP_CONST ? c1.ka : ld.var(c1.a);
+            r[k] = c1.b.op == OP_CONST ? c1.kb : ld.var(c1.b);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+          const int64_t p = base + w * 64 * kItems + k * 64 + lane;
+          if (p - lane >= hi0) break;
+          const bool cv = p < hi0 && ((l[k].null || r[k].null) ? c1.op.sub == CMP_NE : do_compare(c1.op, l[k], r[k]));
+          const uint64_t bal = __ballot(cv);
+          if (lane == 0) c1mask[p >> 6] = bal;
+        }
+        continue;
+      }
 #pragma unroll 1
       for (int k = 0; k < kItems; ++k) {
         const int64_t p = base + w * 64 * kItems + k * 64 + lane;
