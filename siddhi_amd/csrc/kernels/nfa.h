@@ -52,6 +52,7 @@ struct NfaBatch {
   const int64_t* key_pos;
   const int64_t* lane_ev;    // LaneEv records, one per key_pos entry (filled by launch_lane_events)
   int32_t create_all;        // non-partitioned: the single lane exists from app creation
+  const uint32_t* lane_perm; // lane -> key slot (launch_lane_balance), nullptr = identity
   // output
   void* out;
   uint32_t* out_count;
@@ -63,6 +64,10 @@ struct NfaBatch {
 // words, inv_scratch at n int32
 void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_words, int32_t* inv_scratch,
                         hipStream_t s);
+// Lane order by descending event count of the batch (stable by slot), so that the 64 lanes of a wave walk about
+// as many events each: a wave runs as long as its longest lane. perm must hold nkeys uint32.
+struct Scratch;
+void launch_lane_balance(const int64_t* key_off, int32_t nkeys, uint32_t* perm, Scratch& sc, hipStream_t s);
 // ks is lane-interleaved: word w of key k at [w * lanes + k] (lanes = allocated key capacity); heap is key-major
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
                 int32_t nkeys, int32_t* err_dev, hipStream_t s);

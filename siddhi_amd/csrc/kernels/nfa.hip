@@ -14,8 +14,9 @@ namespace {
 
 __global__ SM_NFA_ATTR void nfa_kernel(NfaBatch b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
                            int32_t heap_half, int64_t lanes, int32_t nkeys, int32_t* err_out) {
-  int key = blockIdx.x * blockDim.x + threadIdx.x;
-  if (key >= nkeys) return;
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nkeys) return;
+  const int key = b.lane_perm ? (int)b.lane_perm[lane] : lane;
   nfa_lane(b, blob, ks_all, heap_all, heap_half, lanes, key, err_out);
 }
 
@@ -36,7 +37,30 @@ __global__ void lane_events_kernel(NfaBatch b, int64_t n, const int32_t* __restr
   if (k >= 0) lane_event_record(b, p, k, node_words, out);
 }
 
+// sort key of slot k: 65535 - min(events of k in this batch, 65535) (descending count)
+__global__ void lane_count_kernel(const int64_t* __restrict__ key_off, int32_t nkeys, uint32_t* __restrict__ ck,
+                                  uint32_t* __restrict__ slot) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nkeys) return;
+  const int64_t c = key_off[k + 1] - key_off[k];
+  ck[k] = 65535u - (uint32_t)(c < 65535 ? c : 65535);
+  slot[k] = (uint32_t)k;
+}
+
 }  // namespace
+
+void launch_lane_balance(const int64_t* key_off, int32_t nkeys, uint32_t* perm, Scratch& sc, hipStream_t s) {
+  if (nkeys <= 0) return;
+  size_t mark = sc.used;
+  uint32_t* ck = (uint32_t*)sc.take((size_t)nkeys * 4);
+  uint32_t* ck2 = (uint32_t*)sc.take((size_t)nkeys * 4);
+  uint32_t* v2 = (uint32_t*)sc.take((size_t)nkeys * 4);
+  hipLaunchKernelGGL(lane_count_kernel, dim3((unsigned)((nkeys + 255) / 256)), dim3(256), 0, s, key_off, nkeys, ck,
+                     perm);
+  if (radix_sort_pairs<uint32_t>(ck, ck2, perm, v2, (size_t)nkeys, 0, 16, sc, s))
+    SM_HIP(hipMemcpyAsync(perm, v2, (size_t)nkeys * 4, hipMemcpyDeviceToDevice, s));
+  sc.used = mark;
+}
 
 void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_words, int32_t* inv_scratch,
                         hipStream_t s) {

@@ -189,6 +189,9 @@ struct sm_app {
   bool shut = false;
   int64_t batch_events = 1 << 20;
   int32_t heap_half = 1024;
+  // NFA lanes in descending event-count order for batches with at least this many keys (0 = off;
+  // SM_NFA_BALANCE=<min keys> / option "lane_balance")
+  int64_t lane_balance = 0;
   int64_t out_records = 0;  // option "output_records" (0 = automatic)
   uint64_t text_hash = 0;   // FNV-1a of the SiddhiQL text (snapshots restore only into the same app)
   bool collect = false;
@@ -552,6 +555,11 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   SM_HIP(hipMemsetAsync(a->d_err.p, 0, 4, hs));
   launch_lane_events(b, N, nq, h.node_words, (int32_t*)a->sc.take((size_t)std::max<int64_t>(N, 1) * 4), hs);
   if (tm) tm->mark("nfa_setup", hs);
+  if (partitioned && a->lane_balance > 0 && nkeys >= a->lane_balance && a->sc.used + (size_t)nkeys * 24 + (4 << 20) < a->sc.cap) {
+    uint32_t* perm = (uint32_t*)a->sc.take((size_t)nkeys * 4);
+    launch_lane_balance(key_off, (int32_t)nkeys, perm, a->sc, hs);
+    b.lane_perm = perm;
+  }
   launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
              (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
   SM_HIP(hipGetLastError());
@@ -797,6 +805,7 @@ int sm_app_create(sm_manager* m, const char* siddhiql, sm_app** out) {
       throw std::runtime_error("HIP error: no MI355X device visible (the engine has no CPU fallback)");
     upload_app(a.get());
     if (const char* e = getenv("SIDDHI_AMD_HEAP_WORDS")) a->heap_half = std::max(256, atoi(e));
+    if (const char* e = getenv("SM_NFA_BALANCE")) a->lane_balance = atoll(e);
   });
   if (rc == SM_OK) *out = a.release();
   return rc;
@@ -976,6 +985,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
         a->fast_tm_ready = true;
       }
       a->fast_timing = value != 0;
+    } else if (k == "lane_balance") {
+      a->lane_balance = value;
     } else if (k == "reset") {
       // drop every partition instance, partial match, pending timer and the playback clock, keeping the device
       // allocations: the state of a freshly created runtime of the same app (bench / test helper)
