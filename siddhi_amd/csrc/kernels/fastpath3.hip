@@ -1438,6 +1438,16 @@ bool sort_wc() {
   return on;
 }
 
+// pair (j-order) passes with the write-combining down-sweep: SM_JPASS_WC=1 for the passes after the first,
+// 2 for all of them, 0 (default) none
+int jpass_wc() {
+  static const int v = [] {
+    const char* e = getenv("SM_JPASS_WC");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // c1 reads only the compared attribute (slot-0 variables / stream columns of vattr): evaluated in pass 0
 bool c1_inline(const FastHostInfo& hi, const FastArgs& a) {
   if (!hi.c1_host || hi.c1_len != a.c1_len) return false;
@@ -1698,8 +1708,12 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
       const uint32_t* seg = p == 0 ? mcount : nullptr;
       const int gg = p == 0 ? Gw : G;
       uint64_t* nq = last ? (uint64_t*)pairs_out : outs[p & 1];
-      hipLaunchKernelGGL((downsweep_kernel<2, PairSrc>), dim3(gg), dim3(kBlock), 0, s, PairSrc{cq}, nullptr, nq, nn,
-                         pp, seg, gg, p * kRB, cnt, dbase);
+      if (jpass_wc() > (p == 0 ? 1 : 0))
+        hipLaunchKernelGGL((downsweep_wc_kernel<2, PairSrc>), dim3(gg), dim3(kWcBlock), 0, s, PairSrc{cq}, nullptr, nq,
+                           nn, pp, seg, gg, p * kRB, cnt, dbase);
+      else
+        hipLaunchKernelGGL((downsweep_kernel<2, PairSrc>), dim3(gg), dim3(kBlock), 0, s, PairSrc{cq}, nullptr, nq, nn,
+                           pp, seg, gg, p * kRB, cnt, dbase);
       tmark(last ? "j_pass_last" : "j_pass");
       cq = nq;
     }
