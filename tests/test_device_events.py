@@ -69,6 +69,18 @@ def test_config5_variants_equal_oracle(name):
     assert got == exp
 
 
+@pytest.mark.parametrize("name", ["seq_count13_not1s", "pattern_count_and_within"])
+def test_config5_lane_balance_equals_oracle(name):
+    """Option lane_balance (NFA lanes ordered by descending event count, forced on for any key count): the lane
+    order must not change any output."""
+    sid, cols, ts = synth.gen5(0, 60_000, 2000, 1)
+    text = synth.app5(VARIANTS[name])
+    exp = oracle_out(text, sid, cols, ts)
+    got, _ = product_out(text, sid, cols, ts, lane_balance=1)
+    assert len(exp["streams"].get("Out", [])) > 50
+    assert got == exp
+
+
 @pytest.mark.parametrize("name", ["seq_count13_not1s", "pattern_count_not5s"])
 def test_config5_split_batches(name):
     # state (key table, per-key partials, pending timers, playback clock) carries across device batches,
