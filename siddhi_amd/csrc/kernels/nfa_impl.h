@@ -22,6 +22,37 @@ constexpr int K_REC = 1, K_NODE = 2, K_LNODE = 3, K_FWD = 0xFF;
 
 struct Lane;
 
+// Inlining of the interpreter's large member functions. Each non-inlined call saves the callee's registers to
+// per-lane scratch around the call, and at 4 waves per SIMD that scratch outgrows L2 and MALL. deliver and
+// pre_process are inlined (scratch 1216 -> 880 B per lane, config-5 NFA kernel 81.2 -> 75.8 ms); also inlining
+// fire_all (1040 B, 79.5 ms) or addState (1608 B, 335 VGPR spills) was worse. SM_NFA_CALL_DELIVER /
+// SM_NFA_CALL_PRE restore the calls, SM_NFA_INLINE_FIRE / SM_NFA_INLINE_ADD inline the others (A/B builds).
+#if defined(__HIPCC__) || defined(__HIP__)
+#define SM_NFA_ALWAYS_INLINE __attribute__((always_inline))
+#else
+#define SM_NFA_ALWAYS_INLINE
+#endif
+#ifndef SM_NFA_CALL_DELIVER
+#define SM_INL_DELIVER SM_NFA_ALWAYS_INLINE
+#else
+#define SM_INL_DELIVER
+#endif
+#ifndef SM_NFA_CALL_PRE
+#define SM_INL_PRE SM_NFA_ALWAYS_INLINE
+#else
+#define SM_INL_PRE
+#endif
+#ifdef SM_NFA_INLINE_ADD
+#define SM_INL_ADD SM_NFA_ALWAYS_INLINE
+#else
+#define SM_INL_ADD
+#endif
+#ifdef SM_NFA_INLINE_FIRE
+#define SM_INL_FIRE SM_NFA_ALWAYS_INLINE
+#else
+#define SM_INL_FIRE
+#endif
+
 struct StateLoader {  // OP_VAR loads for a run record
   const Lane* L;
   int rec;
@@ -352,7 +383,7 @@ struct Lane {
   // addState → (count min 0) processMinCountReached → next.addState / nextEvery.addEveryState is recursive
   // in the reference; here it runs over an explicit LIFO work list (same depth-first order) so the kernel has
   // a static stack.
-  __device__ void addState(int p0, int32_t r) {
+  SM_INL_ADD __device__ void addState(int p0, int32_t r) {
     enum { ACT_ADD = 0, ACT_MIN = 1, ACT_EVERY = 2 };
     uint16_t work[3 * kMaxSlots + 4];  // (processor index << 2) | action: a small per-lane (scratch) stack
     int sp = 0;
@@ -515,7 +546,7 @@ struct Lane {
   __device__ void count_startStateReset(int p) { setfl(p, F_START_RESET, true); }
 
   // StreamPreStateProcessor.process(StateEvent) :123-129 → FilterProcessor → post
-  __device__ void pre_process(int p, int32_t r) {
+  SM_INL_PRE __device__ void pre_process(int p, int32_t r) {
     setfl(p, F_STATE_CHANGED, false);
     if (!filter_pass(p, r)) return;
     post_process(pre[p].post, r);
@@ -914,7 +945,7 @@ struct Lane {
 
   // ------------------------------------------------------------ event delivery
   // MultiProcessStreamReceiver.receive / SingleProcessStreamReceiver.processAndClear + selector dispatch
-  __device__ void deliver(const int64_t* __restrict__ r) {
+  SM_INL_DELIVER __device__ void deliver(const int64_t* __restrict__ r) {
     const int64_t p = r[LaneEv::kPos];
     const int s = (int)r[LaneEv::kStream];
     const DReceiver* R = nullptr;
@@ -953,7 +984,7 @@ struct Lane {
   }
 
   // Playback listeners: every scheduler of this key drains its FIFO while head <= now (Scheduler.sendTimerEvents)
-  __device__ void fire_all(int64_t now, int64_t at_pos, int64_t step_time) {
+  SM_INL_FIRE __device__ void fire_all(int64_t now, int64_t at_pos, int64_t step_time) {
     clock = now;
     for (int p = 0; p < q->npre; ++p) {
       if (!is_absent(p)) continue;
