@@ -27,6 +27,7 @@ struct Lane;
 // pre_process are inlined (scratch 1216 -> 880 B per lane, config-5 NFA kernel 81.2 -> 75.8 ms); also inlining
 // fire_all (1040 B, 79.5 ms) or addState (1608 B, 335 VGPR spills) was worse. SM_NFA_CALL_DELIVER /
 // SM_NFA_CALL_PRE restore the calls, SM_NFA_INLINE_FIRE / SM_NFA_INLINE_ADD inline the others (A/B builds).
+// SM_NFA_INLINE_SMALL forces the small list / slot helpers inline: 992 B scratch, 293 VGPR spills, 76.2 -> 82.1 ms.
 #if defined(__HIPCC__) || defined(__HIP__)
 #define SM_NFA_ALWAYS_INLINE __attribute__((always_inline))
 #else
@@ -41,6 +42,11 @@ struct Lane;
 #define SM_INL_PRE SM_NFA_ALWAYS_INLINE
 #else
 #define SM_INL_PRE
+#endif
+#ifdef SM_NFA_INLINE_SMALL
+#define SM_INL_SMALL SM_NFA_ALWAYS_INLINE
+#else
+#define SM_INL_SMALL
 #endif
 #ifdef SM_NFA_INLINE_ADD
 #define SM_INL_ADD SM_NFA_ALWAYS_INLINE
@@ -120,7 +126,7 @@ struct Lane {
     int64_t w = heap[r + 2 + (s >> 1)];
     return (s & 1) ? (int32_t)(w >> 32) : (int32_t)w;
   }
-  __device__ void set_slot(int32_t r, int s, int32_t v) const {
+  SM_INL_SMALL __device__ void set_slot(int32_t r, int s, int32_t v) const {
     int64_t& w = heap[r + 2 + (s >> 1)];
     if (s & 1) w = (w & 0xFFFFFFFFll) | ((int64_t)(uint32_t)v << 32);
     else w = (w & ~0xFFFFFFFFll) | (int64_t)(uint32_t)v;
@@ -143,7 +149,7 @@ struct Lane {
   __device__ void set_nnext(int32_t n, int32_t v) const { set_hi(n, v); }
   __device__ int64_t nts(int32_t n) const { return heap[n + 1]; }
   __device__ int64_t nord(int32_t n) const { return heap[n + 2]; }
-  __device__ int32_t copy_node(int32_t src) {  // StreamEventCloner.copyStreamEvent: next = null
+  SM_INL_SMALL __device__ int32_t copy_node(int32_t src) {  // StreamEventCloner.copyStreamEvent: next = null
     int32_t n = alloc(q->node_words);
     for (int k = 1; k < q->node_words; ++k) heap[n + k] = heap[src + k];
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
@@ -167,14 +173,14 @@ struct Lane {
     return n;
   }
   // StateEvent.addEvent :212-222
-  __device__ void add_event(int32_t r, int s, int32_t n) {
+  SM_INL_SMALL __device__ void add_event(int32_t r, int s, int32_t n) {
     int32_t a = slot(r, s);
     if (a < 0) { set_slot(r, s, n); return; }
     while (nnext(a) >= 0) a = nnext(a);
     set_nnext(a, n);
   }
   // StateEvent.removeLastEvent :224-235
-  __device__ void remove_last_event(int32_t r, int s) {
+  SM_INL_SMALL __device__ void remove_last_event(int32_t r, int s) {
     int32_t a = slot(r, s);
     if (a >= 0) {
       while (nnext(a) >= 0) {
@@ -219,7 +225,7 @@ struct Lane {
   __device__ int32_t ln_next(int32_t ln) const { return (int32_t)heap[ln + 1]; }
   __device__ void ln_set_next(int32_t ln, int32_t v) const { heap[ln + 1] = v; }
   __device__ bool lempty(int p, int w) const { return lhead(p, w) < 0; }
-  __device__ void lappend(int p, int w, int32_t rec) {
+  SM_INL_SMALL __device__ void lappend(int p, int w, int32_t rec) {
     int32_t ln = alloc(2);
     heap[ln] = K_LNODE | ((int64_t)(uint32_t)rec << 32);
     heap[ln + 1] = -1;
@@ -248,7 +254,7 @@ struct Lane {
     lclear(p, src);
   }
   // iterator.remove(): unlink `cur` whose predecessor is `prev` (-1 = head); returns the successor
-  __device__ int32_t lerase(int p, int w, int32_t prev, int32_t cur) {
+  SM_INL_SMALL __device__ int32_t lerase(int p, int w, int32_t prev, int32_t cur) {
     int32_t nx = ln_next(cur);
     int32_t h = lhead(p, w), t = ltail(p, w);
     if (prev < 0) h = nx;
@@ -257,7 +263,7 @@ struct Lane {
     lset(p, w, h, t);
     return nx;
   }
-  __device__ void lremove_rec(int p, int w, int32_t rec) {  // LinkedList.remove(Object): first occurrence
+  SM_INL_SMALL __device__ void lremove_rec(int p, int w, int32_t rec) {  // LinkedList.remove(Object): first occurrence
     int32_t prev = -1;
     for (int32_t x = lhead(p, w); x >= 0; prev = x, x = ln_next(x))
       if (ln_rec(x) == rec) {
@@ -269,7 +275,7 @@ struct Lane {
   // ------------------------------------------------------------ flags
   __device__ int64_t& flags(int p) const { return lw(p, 2); }
   __device__ bool fl(int p, int64_t f) const { return (flags(p) & f) != 0; }
-  __device__ void setfl(int p, int64_t f, bool v) const {
+  SM_INL_SMALL __device__ void setfl(int p, int64_t f, bool v) const {
     if (v) flags(p) |= f;
     else flags(p) &= ~f;
   }
@@ -308,7 +314,7 @@ struct Lane {
   __device__ bool is_absent(int p) const { return pre[p].kind == PK_ABSENT_STREAM || pre[p].kind == PK_ABSENT_LOGICAL; }
 
   // StreamPreStateProcessor.isExpired :102-121
-  __device__ bool expired(int p, int32_t rec, int64_t now) {
+  SM_INL_SMALL __device__ bool expired(int p, int32_t rec, int64_t now) {
     const DPre& P = pre[p];
     for (int w = 0; w < P.withinCnt; ++w) {
       const DWithin& W = within[P.withinOff + w];
