@@ -1126,6 +1126,35 @@ __device__ __forceinline__ int64_t adv_after(const NfaBatch& b, int64_t from, in
   return upto > from ? upto : from;
 }
 
+// The rare part of a lane's timer loop: find the advance point where the earliest timer falls due and fire the
+// timers there. Out of line (SM_TIMER_INLINE undoes it, A/B), so that its registers stay off the per-event path.
+#ifdef SM_TIMER_INLINE
+#define SM_TIMER_ATTR
+#else
+#define SM_TIMER_ATTR __attribute__((noinline))
+#endif
+SM_TIMER_ATTR __device__ bool timer_fire(Lane& L, const NfaBatch& b, int64_t a1, int64_t t, int64_t next_pos,
+                                         int64_t& search_from) {
+  const int64_t a2 = gallop<false>(b.adv_clock, search_from, b.nadv, t);
+  const int64_t a = a1 < a2 ? a1 : a2;
+  if (a >= b.nadv || b.adv_pos[a] > next_pos) {
+    search_from = a;
+    return false;
+  }
+  if (b.adv_wall[a] >= 0) {
+    // wall-clock emulation: step through due timer times up to the tick target
+    int64_t target = b.adv_wall[a];
+    int64_t h;
+    while (L.min_head(h) && h <= target && h >= L.clock && !L.err) L.fire_all(h, b.adv_pos[a], h);
+    L.fire_all(target, b.adv_pos[a], target);
+  } else {
+    L.fire_all(b.adv_clock[a], b.adv_pos[a], b.adv_clock[a]);
+  }
+  search_from = a + 1;
+  L.safe_point();
+  return true;
+}
+
 __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
                          int32_t heap_half, int64_t lanes, int32_t key, int32_t* err_out) {
   const DQuery* q = (const DQuery*)blob;
@@ -1200,23 +1229,7 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
           search_from = a1;
           break;
         }
-        const int64_t a2 = gallop<false>(b.adv_clock, search_from, b.nadv, t);
-        const int64_t a = a1 < a2 ? a1 : a2;
-        if (a >= b.nadv || b.adv_pos[a] > next_pos) {
-          search_from = a;
-          break;
-        }
-        if (b.adv_wall[a] >= 0) {
-          // wall-clock emulation: step through due timer times up to the tick target
-          int64_t target = b.adv_wall[a];
-          int64_t h;
-          while (L.min_head(h) && h <= target && h >= L.clock && !L.err) L.fire_all(h, b.adv_pos[a], h);
-          L.fire_all(target, b.adv_pos[a], target);
-        } else {
-          L.fire_all(b.adv_clock[a], b.adv_pos[a], b.adv_clock[a]);
-        }
-        search_from = a + 1;
-        L.safe_point();
+        if (!timer_fire(L, b, a1, t, next_pos, search_from)) break;
       }
     }
     if (L.err || k >= eend) break;
