@@ -43,6 +43,11 @@ struct Lane;
 #else
 #define SM_INL_PRE
 #endif
+#ifdef SM_NFA_INLINE_PAR
+#define SM_INL_PAR SM_NFA_ALWAYS_INLINE
+#else
+#define SM_INL_PAR
+#endif
 #ifdef SM_NFA_INLINE_SMALL
 #define SM_INL_SMALL SM_NFA_ALWAYS_INLINE
 #else
@@ -560,7 +565,7 @@ struct Lane {
 
   // processAndReturn of every pre kind; returned records are appended to the temporary list `ret`
   // (list words kept in ks slots 4/5 of the pre: the selector runs after the loop, as in the receivers).
-  __device__ void processAndReturn(int p, int32_t evnode, int64_t now) {
+  SM_INL_PAR __device__ void processAndReturn(int p, int32_t evnode, int64_t now) {
     const DPre& P = pre[p];
     const int sid = P.stateId;
     lclear(p, 4 - 0);  // ret list lives in word 4 (head|tail); word 5 spare
