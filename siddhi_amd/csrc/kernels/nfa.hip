@@ -66,7 +66,8 @@ void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_w
                         hipStream_t s) {
   if (nq <= 0) return;
   if (nq >= INT32_MAX) throw std::runtime_error("query batch too large for the lane-event index (>= 2^31 records)");
-  SM_HIP(hipMemsetAsync(inv_scratch, 0xff, (size_t)n * 4, s));
+  // positions outside the query's records stay -1; when the query keeps every record, lane_index writes them all
+  if (nq < n) SM_HIP(hipMemsetAsync(inv_scratch, 0xff, (size_t)n * 4, s));
   hipLaunchKernelGGL(lane_index_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, b.key_pos, nq,
                      inv_scratch);
   hipLaunchKernelGGL(lane_events_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, n,
