@@ -281,6 +281,28 @@ def host_threads():
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n)), 16))
 
 
+def host_cpu():
+    """the host the CPU baseline ran on (lscpu model name, nproc)."""
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    if model is None:
+        try:
+            import subprocess
+            out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+            for ln in out.splitlines():
+                if ln.startswith("Model name"):
+                    model = ln.split(":", 1)[1].strip()
+        except Exception:  # noqa: BLE001
+            pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "threads_allowed": host_threads()}
+
+
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
@@ -317,6 +339,8 @@ def main():
     ap.add_argument("--ts-div", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stack", type=int, default=0, choices=(0, 1, 2),
+                    help="device-batch pipeline for configs 3/4: 0 automatic, 1 bucket stack, 2 sort / walk")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -349,7 +373,7 @@ def main():
     ticks = clock_ticks(ts, lo, world) if args.config == 5 and world > 1 else None
     torch.cuda.synchronize()
 
-    app = ProductApp(cfg["app"])
+    app = ProductApp(cfg["app"], fast_stack=args.stack)
     stream = torch.cuda.current_stream(dev)
     hip_stream = ctypes.c_void_p(stream.cuda_stream)
     n_local = [hi - lo]
@@ -369,6 +393,8 @@ def main():
             app.process_device_events(s_sid, s_ts, [s_sym, s_price, s_price, s_ord], ordinals=s_ord,
                                       hip_stream=hip_stream)
             return int(app.get_stat("output_events:q"))
+        # a fresh runtime of the app per step: the query's open partials (carried across device batches) dropped
+        app.set_option("reset", 0)
         if args.config == 4 and world > 1:
             (s_sym, s_price, s_ts), s_ord, _ = exchange_with_ordinals(symbol, [symbol, price, ts], world, lo)
         elif args.config == 4:
@@ -426,7 +452,7 @@ def main():
         sample = args.cpu_sample or cfg["cpu_sample"]
         log(f"cpu baseline on {sample} events")
         v, sec, mm = cpu_baseline(sample, K, ts_div, cfg["app"], seed, cfg["out"], args.config)
-        cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port",
+        cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port", **host_cpu(),
                "sample": f"first {sample} events of the same stream through oracle/cpu_ref "
                          f"(C++ restatement of the reference engine, 1 thread): {sec:.2f} s, {mm} matches"}
         nt = host_threads() if args.config != 3 else 1  # config 3 is one non-partitioned app: no split
@@ -440,7 +466,7 @@ def main():
                    "sample": f"first {sample} events of the same stream through oracle/cpu_ref on {nt} host threads, "
                              f"one app per {'key shard (symbol % threads)' if args.config in (4, 5) else 'index range'}"
                              f"{' + global clock heartbeats' if args.config == 5 else ''}: {sect:.2f} s, {mt} matches",
-                   "single_thread": {"value": v, "cores": 1, "seconds": sec}}
+                   "single_thread": {"value": v, "cores": 1, "seconds": sec}, **host_cpu()}
     if rank == 0:
         alg = cfg["job_bytes"](N, total_matches) * (1 if cfg["shards"] else world)
         conf = {"workload": cfg["workload"], "config": args.config, "events": N,
@@ -448,8 +474,9 @@ def main():
                 "parallelism": (f"key-sharded x{world}" if args.config in (4, 5) else
                                 f"index-range-sharded x{world}" if cfg["shards"] else f"replicas x{world}"),
                 "device_path": ("general NFA (interleaved device events)" if args.config == 5 else
-                                {1: "general closed form", 2: "onesweep closed form", 3: "filter interpreter",
-                                 4: "filter typed conjunction"}.get(int(path), str(path))),
+                                ({1: "general closed form", 2: "sort / walk closed form", 3: "bucket-stack closed form"}
+                                 if args.config in (3, 4) else {3: "filter interpreter", 4: "filter typed conjunction"})
+                                .get(int(path), str(path))),
                 "step_hbm_fraction": alg / (ms_per_step * 1e-3) / HBM_PEAK}
         if args.config in (4, 5):
             conf["keys"] = K
@@ -469,6 +496,7 @@ def main():
 # ALGORITHMIC bytes per launch for a batch of n events with m matches: what each launch must read
 # and write at minimum.
 KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last",
+           "stack_prep", "stack", "order", "carry_merge", "carry_out",
            "filter_count", "filter_scan", "filter_write",
            "event_index", "nfa_select", "nfa_group", "nfa_setup", "nfa"]
 
@@ -484,6 +512,11 @@ def alg_bytes(label, n, m, config):
             "key_pass": 16 * n + 16 * n,    # 16-B record in and out
             "walk": (16 * n + 8 * m) if keyed else (16 * n + n // 8 + 8 * m),  # records (unkeyed: price + ts +
                                                                                # c1 bits) in, (j, i) pairs out
+            "stack_prep": 0,                # staging bases (O(kBins))
+            "stack": 16 * n + 8 * m,        # bucket records in, staged (j, i) pairs out (bucket order)
+            "order": 8 * m + 8 * m,         # staged pairs in, output pairs out (reference order)
+            "carry_merge": 16 * m,
+            "carry_out": 0,                 # open partials at the end of the batch (O(keys))
             "j_up": 4 * m,
             "j_pass": 16 * m,               # (j, i) in and out
             "j_pass_last": 16 * m,
@@ -502,21 +535,53 @@ def alg_bytes(label, n, m, config):
 
 
 def roofline(ktot, n, m, steps, config):
-    """Dominant kernel (largest total time over the timed steps): algorithmic bytes per launch / average launch
-    duration, against HBM peak. Also the per-kernel breakdown."""
+    """Dominant kernel (largest total time over the timed steps). `achieved` follows SURVEY.md §8(d): the job's
+    algorithmic bytes per event / per match (config 4: 20 B per event + 8 B per match) x the events and matches
+    one launch of it processes (the dominant kernel handles the whole batch), / its average launch duration
+    (HIP events on the launch stream). The per-kernel breakdown keeps each kernel's own algorithmic bytes
+    (alg_bytes) as a diagnostic; traffic_step sums the committed PMC bytes of every kernel of one step."""
     if not ktot:
         return None
     dom = max(ktot, key=lambda k: ktot[k][0])
     tot_ms, calls = ktot[dom]
     avg_ms = tot_ms / calls
-    per_launch = alg_bytes(dom, n, m, config)
-    ach = per_launch / (avg_ms * 1e-3)
+    job = CONFIGS[config]["job_bytes"](n, m)
+    ach = job / (avg_ms * 1e-3)
+    own = alg_bytes(dom, n, m, config)
     brk = {k: {"avg_ms": v[0] / v[1], "calls_per_step": v[1] / steps,
                "gbps": alg_bytes(k, n, m, config) / (v[0] / v[1] * 1e-3) / 1e9} for k, v in ktot.items()}
     traffic, src = pmc_traffic(config, n, dom)
+    step_traffic = pmc_step_traffic(config, n, brk)
     return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
             "traffic": traffic, "traffic_unit": "HBM bytes per launch", "traffic_source": src,
-            "kernel": dom, "avg_launch_ms": avg_ms, "alg_bytes_per_launch": per_launch, "breakdown": brk}
+            "kernel": dom, "avg_launch_ms": avg_ms, "alg_bytes_per_launch": job,
+            "alg_bytes_basis": "SURVEY.md §8(d) job bytes of the batch the launch processes",
+            "kernel_own_alg_bytes": own, "kernel_own_frac": own / (avg_ms * 1e-3) / HBM_PEAK,
+            "traffic_step": step_traffic,
+            "traffic_step_ratio": (step_traffic / job) if step_traffic else None,
+            "breakdown": brk}
+
+
+def pmc_step_traffic(config, n, brk):
+    """HBM bytes of one step: the committed PMC bytes per launch of every kernel label x its launches per step
+    (None unless the summary covers every kernel of the step at this event count)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    try:
+        doc = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    labels = doc.get("labels", {})
+    if doc.get("events") != n:
+        return None
+    tot = 0.0
+    for lab, b in brk.items():
+        ent = labels.get(lab)
+        if ent is None:
+            if lab == "scan":
+                continue
+            return None
+        tot += ent.get("hbm_bytes", 0.0) * b["calls_per_step"]
+    return tot
 
 
 def pmc_traffic(config, n, label):

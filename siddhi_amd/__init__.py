@@ -8,7 +8,8 @@ Mirrors the reference's user-facing classes (modules/siddhi-core/src/main/java/o
   (QueryCallback.java:105), Event(timestamp, data) (core/event/Event.java)
 over the C ABI of libsiddhi_amd.so. Differences from the reference: events are processed on the GPU when the
 runtime flushes (flush(), shutdown(), or when the staging buffer fills), so callbacks fire at those points —
-in the reference's order — instead of inside send().
+in the reference's order, one call per output chunk (the events one trigger made one query emit) — instead of
+inside send(). Callbacks run with the runtime unlocked: they may send into the same runtime.
 """
 import ctypes
 import time
@@ -172,6 +173,10 @@ class SiddhiAppRuntime:
 
     def advance_time(self, ts):
         check(lib().sm_app_advance_time(self._h, int(ts)))
+
+    def advance_wallclock(self, ts):
+        """Wall-clock scheduler emulation: fire every due timer at its scheduled time up to ts."""
+        check(lib().sm_app_advance_wallclock(self._h, int(ts)))
 
     def __del__(self):
         try:

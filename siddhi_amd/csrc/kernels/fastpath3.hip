@@ -33,6 +33,7 @@
 
 #include "expr.h"
 #include "fastpath.h"
+#include "fastpath_dev.h"
 
 namespace sm {
 
@@ -48,13 +49,7 @@ constexpr int kBlock = SM_SB;
 constexpr int kWaves = kBlock / 64;
 constexpr int kItems = SM_SI;
 constexpr int kTile = kBlock * kItems;  // 4096 elements per down-sweep tile
-#ifndef SM_RB
-#define SM_RB 10
-#endif
-constexpr int kRB = SM_RB;  // radix bits per pass
-constexpr int kBins = 1 << kRB;
 constexpr int kBinsPerThread = kBins >= kBlock ? kBins / kBlock : 1;  // digits owned per thread
-constexpr uint32_t kKeyMask = 0x7fffffffu;
 constexpr int kUpUnroll = 8;  // independent loads in flight per thread in the up-sweeps
 #ifndef SM_WB
 #define SM_WB 512
@@ -69,10 +64,6 @@ constexpr int kWalkHalo = 256;                      // records staged past the t
 constexpr int kWalkLds = kWalkTile + kWalkHalo;
 constexpr int kWalkWaves = kWalkBlock / 64;
 constexpr int kUnkeyedBudget = 32;  // private (per-lane) scan steps of an unkeyed record before the wave helps
-constexpr uint32_t kNanCode = 0xffffffffu;  // value code of a NaN (FLOAT / DOUBLE): always compared exactly
-
-// value-code modes
-enum : int { VC_I32 = 0, VC_F32 = 1, VC_F64 = 2, VC_I64R = 3, VC_I64H = 4 };
 
 static_assert(kBins % kBlock == 0 || kBlock % kBins == 0, "bins per thread");
 static_assert(kTile % kWalkTile == 0, "walk tiles nest in sort tiles");
@@ -108,259 +99,6 @@ __device__ unsigned long long sm_stamps[16];
   } while (0)
 #endif
 
-struct Ctrl {
-  unsigned long long kmin, kmax;  // sign-biased key range
-  unsigned long long omax;        // max relative ordinal
-  unsigned long long vmin, vmax;  // sign-biased range of a LONG compared attribute
-  unsigned int bad_ts, bad_ord;   // ts decreasing / ordinals not increasing
-  long long ts0, ts_last;
-};
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global stores
-// (__syncthreads() may also drain vmcnt, which exposes every round of scattered stores). No kernel here exchanges
-// global data between the waves of a workgroup.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// Lanes of this wave whose kRB-bit digit equals this lane's (valid lanes only): one ballot per bit, and per
-// bit one v_bitop3 per half, peers &= bit ? ballot : ~ballot  ==  peers & ~(ballot ^ sext(bit)).
-__device__ __forceinline__ uint64_t peer_mask(uint32_t d, bool valid) {
-  const uint64_t v = __ballot(valid);
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#pragma unroll
-  for (int bb = 0; bb < kRB; ++bb) {
-    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)d, bb, 1);  // 0 or ~0
-    const uint64_t bal = __ballot(m != 0u);
-    lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)bal, m, 0x90);  // a & ~(b ^ c), a = 0xF0, b = 0xCC, c = 0xAA
-    hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(bal >> 32), m, 0x90);
-  }
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-
-__device__ __forceinline__ uint64_t lanemask_lt() {
-  const int lane = threadIdx.x & 63;
-  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
-}
-
-__device__ __forceinline__ StackVal col_value(const NfaStream* st, int a, int64_t row) {
-  StackVal v;
-  v.i = 0;
-  v.d = 0;
-  v.null = 0;
-  switch (st->types[a]) {
-    case T_INT: v.i = ((const int32_t*)st->cols[a])[row]; break;
-    case T_LONG: v.i = ((const int64_t*)st->cols[a])[row]; break;
-    case T_FLOAT: v.d = (double)((const float*)st->cols[a])[row]; break;
-    case T_DOUBLE: v.d = ((const double*)st->cols[a])[row]; break;
-    case T_STRING: v.i = ((const int32_t*)st->cols[a])[row]; v.null = v.i < 0; break;
-    default: v.i = ((const uint8_t*)st->cols[a])[row]; break;
-  }
-  return v;
-}
-
-// canonical 64-bit image of an attribute value (double bits for FLOAT/DOUBLE, integer otherwise)
-__device__ __forceinline__ uint64_t canon(const StackVal& v, int type) {
-  return (type == T_FLOAT || type == T_DOUBLE) ? (uint64_t)__double_as_longlong(v.d) : (uint64_t)v.i;
-}
-__device__ __forceinline__ StackVal uncanon(uint64_t bits, int type) {
-  StackVal v;
-  v.null = 0;
-  if (type == T_FLOAT || type == T_DOUBLE) v.d = __longlong_as_double((long long)bits);
-  else v.i = (int64_t)bits;
-  return v;
-}
-
-// monotone 32-bit value code (see the header)
-template <typename VT>
-__device__ __forceinline__ uint32_t vcode(VT v, int mode, int64_t vmin) {
-  if constexpr (std::is_same<VT, int32_t>::value) {
-    return (uint32_t)v ^ 0x80000000u;
-  } else if constexpr (std::is_same<VT, float>::value) {
-    if (v != v) return kNanCode;
-    const uint32_t b = v == 0.0f ? 0u : __float_as_uint(v);  // -0.0 == 0.0
-    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-  } else if constexpr (std::is_same<VT, double>::value) {
-    if (v != v) return kNanCode;
-    const uint64_t b = v == 0.0 ? 0ull : (uint64_t)__double_as_longlong(v);
-    const uint64_t m = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-    return (uint32_t)(m >> 32);
-  } else {  // int64
-    if (mode == VC_I64R) return (uint32_t)(v - vmin);
-    return (uint32_t)(((uint64_t)v ^ 0x8000000000000000ull) >> 32);
-  }
-}
-
-// A condition program decoded once per thread: its kernel-uniform instructions and constants stay in scalar
-// registers across loops instead of being re-read every iteration.
-struct Cond {
-  const Instr* code;
-  int len;
-  const DVal* consts;
-  bool simple;  // `x CMP y` with x, y variables or constants
-  Instr a, b, op;
-  StackVal ka, kb;
-};
-
-__device__ __forceinline__ StackVal const_val(const DVal* consts, int k) {
-  const DVal c = consts[k];
-  StackVal v;
-  v.i = c.i;
-  v.d = c.d;
-  v.null = c.null;
-  return v;
-}
-
-__device__ __forceinline__ Cond make_cond(const Instr* code, int len, const DVal* consts) {
-  Cond c;
-  c.code = code;
-  c.len = len;
-  c.consts = consts;
-  c.simple = len == 3 && code[2].op == OP_CMP && code[0].op != OP_CMP && code[1].op != OP_CMP &&
-             code[0].op != OP_MATH && code[1].op != OP_MATH && code[0].op != OP_NOT && code[1].op != OP_NOT;
-  if (c.simple) {
-    c.a = code[0];
-    c.b = code[1];
-    c.op = code[2];
-    if (c.a.op == OP_CONST) c.ka = const_val(consts, c.a.a);
-    if (c.b.op == OP_CONST) c.kb = const_val(consts, c.b.a);
-  }
-  return c;
-}
-
-template <typename Ld>
-__device__ __forceinline__ bool eval(const Cond& c, const Ld& ld) {
-  if (c.len == 0) return true;
-  if (c.simple) {
-    const StackVal l = c.a.op == OP_CONST ? c.ka : ld.var(c.a);
-    const StackVal r = c.b.op == OP_CONST ? c.kb : ld.var(c.b);
-    if (l.null || r.null) return c.op.sub == CMP_NE;
-    return do_compare(c.op, l, r);
-  }
-  return truthy(eval_prog(c.code, c.len, c.consts, ld));
-}
-
-// c.simple (or empty) conditions only: no interpreter stack in the caller
-template <typename Ld>
-__device__ __forceinline__ bool eval_simple(const Cond& c, const Ld& ld) {
-  if (c.len == 0) return true;
-  const StackVal l = c.a.op == OP_CONST ? c.ka : ld.var(c.a);
-  const StackVal r = c.b.op == OP_CONST ? c.kb : ld.var(c.b);
-  if (l.null || r.null) return c.op.sub == CMP_NE;
-  return do_compare(c.op, l, r);
-}
-
-template <int OP, typename T>
-__device__ __forceinline__ bool cmp_fixed(T x, T y) {
-  if constexpr (OP == CMP_EQ) return x == y;
-  else if constexpr (OP == CMP_NE) return x != y;
-  else if constexpr (OP == CMP_LT) return x < y;
-  else if constexpr (OP == CMP_LE) return x <= y;
-  else if constexpr (OP == CMP_GT) return x > y;
-  else return x >= y;
-}
-
-// e1-only program on an original row (c1)
-struct RowLoader {
-  const NfaStream* st;
-  int64_t row;
-  __device__ StackVal var(const Instr& in) const {
-    if (in.op == OP_COL) return col_value(st, in.a, row);
-    return col_value(st, in.c, row);
-  }
-};
-
-// c2 over the carried attribute: slot 0 = e1, slot 1 = e2 (host checked every variable reads `vattr`)
-struct PairLoader {
-  uint64_t v1, v2;
-  int type;
-  __device__ StackVal var(const Instr& in) const { return uncanon(in.a == 0 ? v1 : v2, type); }
-};
-
-// Unkeyed walk: c2 on canonical 64-bit values, as a fixed compare `e2.x OP e1.x` (OP >= 0; FP: compared as
-// double, else as int64) or the generic condition program (OP < 0).
-template <int OP, bool FP>
-struct C2 {
-  Cond c;
-  int vtype;
-  __device__ __forceinline__ bool operator()(uint64_t v1, uint64_t v2) const {
-    if constexpr (OP < 0) {
-      return eval(c, PairLoader{v1, v2, vtype});
-    } else {
-      if constexpr (FP) return cmp_fixed<OP>(__longlong_as_double((long long)v2), __longlong_as_double((long long)v1));
-      else return cmp_fixed<OP>((int64_t)v2, (int64_t)v1);
-    }
-  }
-};
-
-// Keyed walk: c2 = `e2.x OP e1.x` on value codes; equal inexact codes and NaN go to the exact column values.
-template <int OP, bool FP>
-struct C2Code {
-  bool exact_codes;  // the code mode is exact (INT, FLOAT, rebased LONG)
-  int vtype;
-  const void* vcol;
-  const int64_t* ord;  // ordinals of the batch rows (nullptr: row = relative ordinal)
-  int64_t obase, n;
-  __device__ int64_t row_of(uint32_t o) const {  // rows are in ordinal order
-    if (!ord) return o;
-    const int64_t want = (int64_t)o + obase;
-    int64_t lo = 0, hi = n - 1;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (ord[mid] < want) lo = mid + 1;
-      else hi = mid;
-    }
-    return lo;
-  }
-  __device__ bool exact(uint32_t o1, uint32_t o2) const {
-    const int64_t r1 = row_of(o1), r2 = row_of(o2);
-    if constexpr (FP) {
-      double x1, x2;
-      if (vtype == T_FLOAT) {
-        x1 = ((const float*)vcol)[r1];
-        x2 = ((const float*)vcol)[r2];
-      } else {
-        x1 = ((const double*)vcol)[r1];
-        x2 = ((const double*)vcol)[r2];
-      }
-      return cmp_fixed<OP>(x2, x1);
-    } else {
-      int64_t x1, x2;
-      if (vtype == T_INT) {
-        x1 = ((const int32_t*)vcol)[r1];
-        x2 = ((const int32_t*)vcol)[r2];
-      } else {
-        x1 = ((const int64_t*)vcol)[r1];
-        x2 = ((const int64_t*)vcol)[r2];
-      }
-      return cmp_fixed<OP>(x2, x1);
-    }
-  }
-  __device__ __forceinline__ bool operator()(uint32_t c1, uint32_t o1, uint32_t c2, uint32_t o2) const {
-    if (!needs_exact(c1, c2)) return cmp_fixed<OP>(c2, c1);
-    return exact(o1, o2);
-  }
-  // the codes alone do not decide the comparison (equal inexact codes, or a NaN)
-  __device__ __forceinline__ bool needs_exact(uint32_t c1, uint32_t c2) const {
-    const bool nan = FP & ((c1 == kNanCode) | (c2 == kNanCode));
-    return nan | (!exact_codes & (c1 == c2));
-  }
-};
-
-// Chunk g of a pass: [g * per, g * per + len_g); len_g = seg_len[g] when given, else the uniform split of n.
-__device__ __forceinline__ void chunk_range(int g, int64_t n, int64_t per, const uint32_t* seg_len, int64_t& lo,
-                                            int64_t& len) {
-  lo = (int64_t)g * per;
-  if (seg_len) {
-    len = seg_len[g];
-  } else {
-    len = n - lo;
-    if (len > per) len = per;
-    if (len < 0) len = 0;
-  }
-}
 
 // ---------------------------------------------------------------- prep
 
@@ -495,6 +233,7 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     c->ts0 = ts[0];
     c->ts_last = ts[n - 1];
+    c->o0 = ord ? ord[0] - obase : 0;
     if (!ord) c->omax = (unsigned long long)(n - 1);
   }
   __syncthreads();
@@ -1106,6 +845,12 @@ struct WalkArgs {
   int64_t n;
   bool exact_codes;
   const uint64_t* c1mask;  // unkeyed: c1 bits of the events
+  // carry out: partials still pending at the end (their key's events ran out before a match or expiry)
+  int64_t kmin, ts0;
+  int64_t* cand;
+  uint32_t* cand_n;
+  uint32_t cand_cap;
+  uint32_t* err;
 };
 
 template <bool KEYED>
@@ -1127,7 +872,7 @@ struct WalkLds<false> {
 // Matches are compacted in record order into the chunk's staging region [lo, lo + count); the chunk's match
 // count goes to mcount[g] and the digit-0 counts of j to jcnt[d * G + g] (the first j pass needs no up-sweep).
 template <bool KEYED, int OP, bool FP>
-__global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t per, int G,
+__global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu(6))) walk_kernel(WalkArgs a, int64_t per, int G,
                                                           uint64_t* __restrict__ stq, uint32_t* __restrict__ mcount,
                                                           uint32_t* __restrict__ jcnt) {
   __shared__ WalkLds<KEYED> L;
@@ -1203,7 +948,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
     }
     // lane-private queue over the items with c1. The loop body is written branch-light (selects, one
     // predicated take): every live lane advances its scan by one record per iteration.
-    uint32_t hasm = 0, openm = 0;
+    uint32_t hasm = 0, openm = 0, pendm = 0;  // matched / scan left the staged records / key's events ran out
     uint32_t todo = c1m;
     int k = 0, v = 0;
     uint64_t vu = 0;
@@ -1236,13 +981,14 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       // so a lane scans privately for kUnkeyedBudget records and leaves the rest to the wave-cooperative finish
       const bool inb = v < lend && (KEYED || v - vstart < kUnkeyedBudget);
       const int vv = inb ? v : lend - 1;
-      bool stop, hit;
+      bool stop, hit, kchg = false;
       if constexpr (KEYED) {
         // straight-line step: one ds_read_b128, conditions combined without short-circuit branches; the rare
         // exact comparisons run afterwards for the lanes that need them
         const uint4 r = L.r[vv];
         const bool expired = (a.within >= 0) & ((int64_t)(r.w - (uint32_t)tu) > a.within);
-        stop = (!inb) | (((r.x ^ key) & kKeyMask) != 0u) | expired;
+        kchg = inb & (((r.x ^ key) & kKeyMask) != 0u);
+        stop = (!inb) | kchg | expired;
         const bool ex = live & !stop & cc.needs_exact(cu, r.z);
         hit = live & !stop & !ex & cmp_fixed<OP>(r.z, cu);
         if (__any(ex))
@@ -1253,8 +999,10 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
         hit = live && !stop && c2(vu, L.v[vv]);
       }
       const bool open = live && !inb && base + v < n;  // leaves the staged records: finished from global below
+      const bool pend = live && (kchg || (!inb && base + v >= n));  // the key's events (or the batch) ran out
       hasm |= hit ? (1u << k) : 0u;
       openm |= open ? (1u << k) : 0u;
+      pendm |= pend ? (1u << k) : 0u;
       if (hit || open) sj[k][threadIdx.x] = (uint32_t)v;
       const bool done = live && (stop || hit);
       ++v;
@@ -1274,6 +1022,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
         const int64_t t0 = L.t[luu];
         const uint64_t v0 = L.v[luu];
         int64_t found = -1;
+        bool ran_out = true;  // no expiring event before the end of the batch
         for (int64_t p = base + sj[kk][w * 64 + src]; p < n; p += 64) {
           const int64_t q = p + lane;
           bool stp = q >= n, hit = false;
@@ -1286,6 +1035,7 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
           if (any) {
             const int f = __ffsll((unsigned long long)any) - 1;
             if ((hb >> f) & 1ull) found = p + f;
+            ran_out = found < 0 && p + f >= n;
             break;
           }
         }
@@ -1293,6 +1043,8 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
           if (found >= 0) {
             hasm |= 1u << kk;
             sj[kk][threadIdx.x] = (uint32_t)(found - base);
+          } else if (ran_out) {
+            pendm |= 1u << kk;
           }
           openm &= ~(1u << kk);
         }
@@ -1305,26 +1057,74 @@ __global__ void __launch_bounds__(kWalkBlock) walk_kernel(WalkArgs a, int64_t pe
       const int kk = __ffs(openm) - 1;
       openm &= openm - 1;
       const int luu = w * 64 * kWalkItems + kk * 64 + lane;
+      bool ran_out = true;
       for (int64_t p = base + sj[kk][threadIdx.x]; p < n; ++p) {
         bool hit;
         if constexpr (KEYED) {
           const uint4 r = a.rec[p];
           const uint4 ru = L.r[luu];
-          if ((r.x & kKeyMask) != (ru.x & kKeyMask) || (a.within >= 0 && (int64_t)(r.w - ru.w) > a.within)) break;
+          if ((r.x & kKeyMask) != (ru.x & kKeyMask)) break;  // the key's events ran out: pending
+          if (a.within >= 0 && (int64_t)(r.w - ru.w) > a.within) {
+            ran_out = false;
+            break;
+          }
           hit = cc(ru.z, ru.y, r.z, r.y);
         } else {
           const int64_t d = a.ts[p] - L.t[luu];
-          if (a.within >= 0 && (d < 0 ? -d : d) > a.within) break;
+          if (a.within >= 0 && (d < 0 ? -d : d) > a.within) {
+            ran_out = false;
+            break;
+          }
           hit = c2(L.v[luu], canon(col_value(a.st, a.vattr, p), a.vtype));
         }
         if (hit) {
           hasm |= 1u << kk;
           sj[kk][threadIdx.x] = (uint32_t)(p - base);
+          ran_out = false;
           break;
         }
       }
+      if (ran_out) pendm |= 1u << kk;
     }
     SM_STAMP(4);
+    // carry out: partials still pending at the end of the batch (wave-aggregated append)
+    if (__any(pendm != 0)) {
+      const uint32_t np = (uint32_t)__popc(pendm);
+      uint32_t inc = np;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+      }
+      uint32_t cb = 0;
+      if (lane == 63 && inc) cb = atomicAdd(a.cand_n, inc);
+      cb = __shfl(cb, 63, 64) + inc - np;
+      for (uint32_t pm = pendm; pm; pm &= pm - 1) {
+        const int q = __ffs(pm) - 1;
+        const int luq = w * 64 * kWalkItems + q * 64 + lane;
+        int64_t key = 0, ordg, tsg, row;
+        if constexpr (KEYED) {
+          const uint4 r = L.r[luq];
+          key = a.kmin + (int64_t)(r.x & kKeyMask);
+          ordg = (int64_t)r.y + a.obase;
+          tsg = (int64_t)r.w + a.ts0;
+          row = cc.row_of(r.y);
+        } else {
+          row = base + luq;
+          ordg = a.ord ? a.ord[row] : a.obase + row;
+          tsg = L.t[luq];
+        }
+        if (cb < a.cand_cap) {
+          int64_t* c = a.cand + 4 * (int64_t)cb;
+          c[0] = key;
+          c[1] = ordg;
+          c[2] = tsg;
+          c[3] = row;
+        } else {
+          atomicOr(a.err, 1u);
+        }
+        ++cb;
+      }
+    }
     uint32_t mine = 0;
 #pragma unroll 1
     for (int q = 0; q < kWalkItems; ++q) {
@@ -1494,22 +1294,205 @@ void launch_down0_k(const FastHostInfo& hi, const FastArgs& a, const void* kcol,
 
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// ---- carried partials on the walk pipeline
+
+struct ResolveArgs {
+  const int64_t* crow;  // carry rows [key, ordinal, ts, values...]
+  int64_t nc;
+  int w, vattr, vtype, vmode;
+  int64_t vmin;
+  bool exact_codes;
+  const uint4* rec;  // keyed: records sorted by key
+  const NfaStream* st;
+  const int64_t* ts;
+  const int64_t* ord;
+  int64_t obase, n, kmin, span, ts0, within;
+  uint64_t* cpair;  // per carried partial: (j << 32) | (e1 ordinal - base), or ~0
+  int64_t* cand;
+  uint32_t* cand_n;
+  uint32_t cand_cap;
+  uint32_t* err;
+};
+
+// One thread per carried partial: the first event of its key in this batch that matches it (reference:
+// processAndReturn over the pending list, StreamPreStateProcessor.java:274-327), finds it expired (dropped), or
+// none (still pending: carry-out candidate).
+template <bool KEYED, int OP, bool FP>
+__global__ void resolve_kernel(ResolveArgs r) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= r.nc) return;
+  const int64_t* row = r.crow + i * r.w;
+  const int64_t key = row[0], oc = row[1], tc = row[2];
+  const StackVal vc = uncanon((uint64_t)row[3 + r.vattr], r.vtype);
+  r.cpair[i] = ~0ull;
+  if (oc - r.obase < INT32_MIN) atomicOr(r.err, 2u);  // not expressible as a 32-bit relative ordinal
+  auto pending = [&]() {
+    const uint32_t q = atomicAdd(r.cand_n, 1u);
+    if (q < r.cand_cap) {
+      int64_t* c = r.cand + 4 * (int64_t)q;
+      c[0] = key;
+      c[1] = oc;
+      c[2] = tc;
+      c[3] = -i - 1;
+    } else {
+      atomicOr(r.err, 1u);
+    }
+  };
+  int64_t p = 0, kr = 0;
+  uint32_t code = 0;
+  if constexpr (KEYED) {
+    kr = key - r.kmin;
+    if (kr < 0 || kr > r.span) {  // no event of this key in the batch
+      pending();
+      return;
+    }
+    int64_t lo = 0, hi = r.n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)(r.rec[mid].x & kKeyMask) < kr) lo = mid + 1;
+      else hi = mid;
+    }
+    p = lo;
+    switch (r.vtype) {
+      case T_INT: code = vcode<int32_t>((int32_t)vc.i, r.vmode, r.vmin); break;
+      case T_LONG: code = vcode<int64_t>(vc.i, r.vmode, r.vmin); break;
+      case T_FLOAT: code = vcode<float>((float)vc.d, r.vmode, r.vmin); break;
+      default: code = vcode<double>(vc.d, r.vmode, r.vmin); break;
+    }
+  }
+  for (; p < r.n; ++p) {
+    int64_t tj, rowj = p;
+    uint32_t oj, cj = 0;
+    if constexpr (KEYED) {
+      const uint4 e = r.rec[p];
+      if ((int64_t)(e.x & kKeyMask) != kr) break;
+      tj = (int64_t)e.w + r.ts0;
+      oj = e.y;
+      cj = e.z;
+      rowj = -1;
+    } else {
+      tj = r.ts[p];
+      oj = r.ord ? (uint32_t)(r.ord[p] - r.obase) : (uint32_t)p;
+    }
+    const int64_t dt = tj - tc;
+    if (r.within >= 0 && (dt < 0 ? -dt : dt) > r.within) return;  // expired at this event: dropped
+    bool hit;
+    const bool nan = FP & ((code == kNanCode) | (cj == kNanCode));
+    if (KEYED && !nan && (r.exact_codes || code != cj)) {
+      hit = cmp_fixed<OP>(cj, code);
+    } else {
+      if (rowj < 0) {  // keyed: the row of ordinal oj
+        rowj = oj;
+        if (r.ord) {
+          const int64_t want = (int64_t)oj + r.obase;
+          int64_t lo = 0, hi = r.n - 1;
+          while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (r.ord[mid] < want) lo = mid + 1;
+            else hi = mid;
+          }
+          rowj = lo;
+        }
+      }
+      const StackVal vj = col_value(r.st, r.vattr, rowj);
+      if constexpr (FP) hit = cmp_fixed<OP>(vj.d, vc.d);
+      else hit = cmp_fixed<OP>(vj.i, vc.i);
+    }
+    if (hit) {
+      r.cpair[i] = ((uint64_t)oj << 32) | (uint32_t)(oc - r.obase);
+      return;
+    }
+  }
+  pending();
+}
+
+template <bool KEYED, int OP, bool FP>
+void launch_resolve_t(const ResolveArgs& r, hipStream_t s) {
+  hipLaunchKernelGGL((resolve_kernel<KEYED, OP, FP>), dim3((unsigned)((r.nc + 255) / 256)), dim3(256), 0, s, r);
+}
+
+void launch_resolve(bool keyed, int spec, const ResolveArgs& r, hipStream_t s) {
+#define SM_RES(OP, FP) (keyed ? launch_resolve_t<true, OP, FP>(r, s) : launch_resolve_t<false, OP, FP>(r, s))
+  switch (spec) {
+    case CMP_EQ * 2: SM_RES(CMP_EQ, false); break;
+    case CMP_EQ * 2 + 1: SM_RES(CMP_EQ, true); break;
+    case CMP_NE * 2: SM_RES(CMP_NE, false); break;
+    case CMP_NE * 2 + 1: SM_RES(CMP_NE, true); break;
+    case CMP_LT * 2: SM_RES(CMP_LT, false); break;
+    case CMP_LT * 2 + 1: SM_RES(CMP_LT, true); break;
+    case CMP_LE * 2: SM_RES(CMP_LE, false); break;
+    case CMP_LE * 2 + 1: SM_RES(CMP_LE, true); break;
+    case CMP_GT * 2: SM_RES(CMP_GT, false); break;
+    case CMP_GT * 2 + 1: SM_RES(CMP_GT, true); break;
+    case CMP_GE * 2: SM_RES(CMP_GE, false); break;
+    case CMP_GE * 2 + 1: SM_RES(CMP_GE, true); break;
+    default: throw std::logic_error("carried partials need a fixed compare");
+  }
+#undef SM_RES
+}
+
+__global__ void pair_flag_kernel(const uint64_t* __restrict__ cp, int64_t n, uint32_t* __restrict__ f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = cp[i] != ~0ull ? 1u : 0u;
+}
+
+// sign-flipped e1 word: (j, e1) sorts in signed e1 order (a carried e1 may lie before the ordinal base)
+__global__ void pair_compact_kernel(const uint64_t* __restrict__ cp, const uint32_t* __restrict__ pos, int64_t n,
+                                    uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && cp[i] != ~0ull) out[pos[i]] = cp[i] ^ 0x80000000ull;
+}
+
+// merge of the walk's (j, i)-ordered pairs with the carried partials' pairs (also (j, i)-ordered); for equal j the
+// carried ones (older e1) come first
+__global__ void merge_main_kernel(const uint64_t* __restrict__ mq, int64_t m, const uint64_t* __restrict__ cq,
+                                  int64_t mc, uint64_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  const uint64_t v = mq[k];
+  const uint32_t j = (uint32_t)(v >> 32);
+  int64_t lo = 0, hi = mc;  // carried pairs with j_c <= j
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((uint32_t)(cq[mid] >> 32) <= j) lo = mid + 1;
+    else hi = mid;
+  }
+  out[k + lo] = v;
+}
+
+__global__ void merge_carried_kernel(const uint64_t* __restrict__ cq, int64_t mc, const uint64_t* __restrict__ mq,
+                                     int64_t m, uint64_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= mc) return;
+  const uint64_t v = cq[k] ^ 0x80000000ull;
+  const uint32_t j = (uint32_t)(v >> 32);
+  int64_t lo = 0, hi = m;  // walk pairs with j_w < j
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((uint32_t)(mq[mid] >> 32) < j) lo = mid + 1;
+    else hi = mid;
+  }
+  out[k + lo] = v;
+}
+
 }  // namespace
 
 // Returns -1 when the batch is outside the v2 envelope (caller takes the general path).
-int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastState& fs, uint32_t* pairs_out,
-                             int64_t pairs_cap, Scratch& sc, hipStream_t s, FastTimings* tm) {
+int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastState& fs, FastCarry& carry,
+                             uint32_t* pairs_out, int64_t pairs_cap, Scratch& sc, hipStream_t s, FastTimings* tm,
+                             int stack_mode) {
   const int64_t n = a.n;
   if (n == 0) return 0;
-  if (n >= 0x7fffffffll || hi.vattr < 0) return -1;
+  if (n >= 0x7fffffffll || hi.vattr < 0) return FAST_OUTSIDE;
   const bool keyed = a.key != nullptr;
-  if (keyed && (hi.key_col < 0 || !(hi.key_type == T_INT || hi.key_type == T_LONG))) return -1;
+  if (keyed && (hi.key_col < 0 || !(hi.key_type == T_INT || hi.key_type == T_LONG))) return FAST_OUTSIDE;
   const int spec = c2_spec(hi);
-  if (keyed && spec < 0) return -1;  // keyed records carry value codes: fixed compares only
+  if (keyed && spec < 0) return FAST_OUTSIDE;  // keyed records carry value codes: fixed compares only
+  if (carry.n > 0 && spec < 0) return FAST_OUTSIDE;
   size_t mark = sc.used;
   auto bail = [&]() -> int64_t {
     sc.used = mark;
-    return -1;
+    return FAST_OUTSIDE;
   };
   Ctrl* c = (Ctrl*)sc.take(sizeof(Ctrl));
   {
@@ -1581,20 +1564,22 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   SM_HIP(hipMemcpyAsync(&hc, c, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));
   if (a.within >= 0) {
-    if (hc.bad_ts) {
+    // the closed form needs non-decreasing event time, inside the batch and after the carried state
+    if (hc.bad_ts || (carry.active && hc.ts0 < carry.ts_last)) {
       sc.used = mark;
-      throw std::runtime_error("fast path requires non-decreasing event timestamps within a device batch");
+      return FAST_NON_MONOTONE;
     }
     if ((unsigned long long)(hc.ts_last - hc.ts0) >= 0xffffffffull) return bail();
   }
   if (hc.omax >= 0x7fffffffull || hc.bad_ord) return bail();
   int kbits = 0;
   int64_t kmin = 0;
+  uint64_t kspan = 0;
   if (keyed) {
     kmin = (int64_t)(hc.kmin ^ 0x8000000000000000ull);
     kmin &= ~(int64_t)(kBins - 1);  // rebase on a digit boundary (prep counted digit 0 of the raw key)
-    const uint64_t span = (uint64_t)((int64_t)(hc.kmax ^ 0x8000000000000000ull) - kmin);
-    kbits = std::max(1, bits_for(span));
+    kspan = (uint64_t)((int64_t)(hc.kmax ^ 0x8000000000000000ull) - kmin);
+    kbits = std::max(1, bits_for(kspan));
     if (kbits > 30) return bail();
   }
   // value code of the compared attribute
@@ -1606,7 +1591,8 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     case T_FLOAT: vmode = VC_F32; break;
     case T_DOUBLE: vmode = VC_F64; exact_codes = false; break;
     default:
-      if (keyed && hc.vmax - hc.vmin <= 0xffffffffull) {
+      // rebased codes need every compared value (carried partials too) inside the batch's range
+      if (keyed && carry.n == 0 && hc.vmax - hc.vmin <= 0xffffffffull) {
         vmode = VC_I64R;
         vmin = (int64_t)(hc.vmin ^ 0x8000000000000000ull);
       } else {
@@ -1617,6 +1603,12 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   const int fpass = keyed ? (kbits + kRB - 1) / kRB : 0;
   const int jbits = std::max(1, bits_for(hc.omax));
   const int jpass = (jbits + kRB - 1) / kRB;
+  auto finish = [&](int64_t m) {
+    carry.ts_last = carry.active ? std::max<int64_t>(carry.ts_last, hc.ts_last) : (int64_t)hc.ts_last;
+    carry.active = true;
+    sc.used = mark;
+    return m;
+  };
 
   uint64_t* stq = nullptr;                // walk staging (chunk-local compaction), (j << 32) | i
   uint64_t *pq = nullptr, *qq = nullptr;  // j-sort ping-pong
@@ -1636,6 +1628,15 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   wa.n = n;
   wa.exact_codes = exact_codes;
   wa.c1mask = c1mask;
+  wa.kmin = kmin;
+  wa.ts0 = hc.ts0;
+  // carry-out candidates of the walk pipeline: pending partials of the batch + carried ones still pending
+  const int64_t nc = carry.n;
+  const int64_t cand_cap = std::min<int64_t>(n + nc, (int64_t)1 << 26) + 1024;
+  uint32_t* cflags = (uint32_t*)sc.take(16);  // [0] candidates, [1] overflow
+  SM_HIP(hipMemsetAsync(cflags, 0, 16, s));
+  int64_t* cand = nullptr;
+  uint4* cur = nullptr;
   if (keyed) {
     uint4* A = (uint4*)sc.take(n * 16);
     uint4* B = (uint4*)sc.take(n * 16);
@@ -1645,7 +1646,43 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
       launch_down0_k<int32_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
     else launch_down0_k<int64_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
     tmark("key_pass0");
-    uint4* cur = A;
+    // bucket-stack pipeline when the per-bucket keys fill a workgroup (stack.hip); it falls back here otherwise
+    const int H = (int)std::min<uint64_t>(kspan >> kRB, 1ull << 20) + 1;
+    const bool order_op = spec >= 0 && (spec >> 1) != CMP_EQ && (spec >> 1) != CMP_NE;
+    const bool ts_ok = a.within < 0 || (a.within < (1ll << 30) && hc.ts_last - hc.ts0 < (1ll << 30));
+    if (stack_mode != 2 && order_op && ts_ok && H <= kBins && (stack_mode == 1 || H >= kBins / 2)) {
+      StackPlan sp{};
+      sp.rec = A;
+      sp.dbase = dbase;
+      sp.n = n;
+      sp.omax = (int64_t)hc.omax;
+      sp.H = H;
+      sp.kmin = kmin;
+      sp.op = spec >> 1;
+      sp.fp = (spec & 1) != 0;
+      sp.exact_codes = exact_codes;
+      sp.vtype = hi.vtype;
+      sp.vattr = hi.vattr;
+      sp.vmode = vmode;
+      sp.vmin = vmin;
+      sp.vcol = hi.cols[hi.vattr];
+      sp.within = a.within;
+      sp.ts0 = hc.ts0;
+      sp.ts_last = hc.ts_last;
+      sp.o0 = (int32_t)hc.o0;
+      const int64_t m = stack_pipeline(sp, a, hi, fs, carry, pairs_out, pairs_cap, sc, s, tm);
+      if (m >= 0) {
+        fs.last_path = 3;
+        if (tm) {
+          SM_HIP(hipEventRecord(tm->ev[1], s));
+          SM_HIP(hipEventRecord(tm->ev[2], s));
+          SM_HIP(hipEventRecord(tm->ev[3], s));
+        }
+        return finish(m);
+      }
+    }
+    cand = (int64_t*)sc.take((size_t)cand_cap * 32);
+    cur = A;
     uint4* nxt = B;
     for (int p = 1; p < fpass; ++p) {
       hipLaunchKernelGGL((upsweep_kernel<RecDigits>), dim3(G), dim3(kBlock), 0, s, RecDigits{cur}, n, per, G,
@@ -1663,6 +1700,10 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     }
     if (tm) SM_HIP(hipEventRecord(tm->ev[1], s));
     wa.rec = cur;
+    wa.cand = cand;
+    wa.cand_n = cflags;
+    wa.cand_cap = (uint32_t)cand_cap;
+    wa.err = cflags + 1;
     // staging + one ping-pong buffer in the dead record buffer (2 x 8n of its 16n bytes); the other in `cur`
     // once the walk is done
     stq = (uint64_t*)nxt;
@@ -1671,26 +1712,88 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     launch_walk<true>(spec, Gw, s, wa, perw, stq, mcount, cnt);
   } else {
     if (tm) SM_HIP(hipEventRecord(tm->ev[1], s));
+    cand = (int64_t*)sc.take((size_t)cand_cap * 32);
+    wa.cand = cand;
+    wa.cand_n = cflags;
+    wa.cand_cap = (uint32_t)cand_cap;
+    wa.err = cflags + 1;
     stq = (uint64_t*)sc.take(n * 8);
     pq = (uint64_t*)sc.take(n * 8);
     qq = (uint64_t*)sc.take(n * 8);
     launch_walk<false>(spec, Gw, s, wa, perw, stq, mcount, cnt);
   }
+  fs.last_path = 2;
   tmark("walk");
   if (tm) SM_HIP(hipEventRecord(tm->ev[2], s));
+
+  // carried partials against this batch (before the walk's records are overwritten by the j passes)
+  uint64_t* cps = nullptr;
+  int64_t Mc = 0;
+  if (nc > 0) {
+    uint64_t* cpair = (uint64_t*)sc.take((size_t)nc * 8);
+    ResolveArgs ra{};
+    ra.crow = carry.rows;
+    ra.nc = nc;
+    ra.w = carry.width;
+    ra.vattr = hi.vattr;
+    ra.vtype = hi.vtype;
+    ra.vmode = vmode;
+    ra.vmin = vmin;
+    ra.exact_codes = exact_codes;
+    ra.rec = cur;
+    ra.st = a.st;
+    ra.ts = a.ts;
+    ra.ord = a.ordinals;
+    ra.obase = a.ordinal_base;
+    ra.n = n;
+    ra.kmin = kmin;
+    ra.span = (int64_t)kspan;
+    ra.ts0 = hc.ts0;
+    ra.within = a.within;
+    ra.cpair = cpair;
+    ra.cand = cand;
+    ra.cand_n = cflags;
+    ra.cand_cap = (uint32_t)cand_cap;
+    ra.err = cflags + 1;
+    launch_resolve(keyed, spec, ra, s);
+    uint32_t* fl = (uint32_t*)sc.take((size_t)nc * 4 + 4);
+    hipLaunchKernelGGL(pair_flag_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, cpair, nc, fl);
+    exclusive_scan_u32(fl, (size_t)nc, sc, s, fl + nc);
+    uint32_t hmc = 0;
+    SM_HIP(hipMemcpyAsync(&hmc, fl + nc, 4, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    Mc = hmc;
+    if (Mc > 0) {
+      cps = (uint64_t*)sc.take((size_t)Mc * 8);
+      uint64_t* cps2 = (uint64_t*)sc.take((size_t)Mc * 8);
+      hipLaunchKernelGGL(pair_compact_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, cpair, fl, nc, cps);
+      // (j, i) order
+      if (radix_sort_pairs<uint64_t>(cps, cps2, nullptr, nullptr, (size_t)Mc, 0, 64, sc, s)) cps = cps2;
+    }
+  }
 
   // order by j: LSD passes over the (j, i) pairs; the first reads the walk's chunk-local staging (its digit-0
   // counts came from the walk), the last writes the output
   std::vector<uint32_t> hm(Gw);
   SM_HIP(hipMemcpyAsync(hm.data(), mcount, sizeof(uint32_t) * Gw, hipMemcpyDeviceToHost, s));
   scan_counts(Gw);
+  uint32_t hcf[2];
+  SM_HIP(hipMemcpyAsync(hcf, cflags, 8, hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));
+  if (hcf[1]) {
+    sc.used = mark;
+    throw std::runtime_error((hcf[1] & 2) ? "a carried partial lies more than 2^31 events before the batch's ordinal "
+                                            "base (match tuples are 32-bit ordinals relative to it)"
+                                          : "fast path: more than 2^26 partial matches pending at the end of a device "
+                                            "batch");
+  }
   int64_t M = 0;
   for (int g = 0; g < Gw; ++g) M += hm[g];
-  if (M > pairs_cap) {
+  if (M + Mc > pairs_cap) {
     sc.used = mark;
     throw std::runtime_error("match buffer too small");
   }
+  uint64_t* mainq = (uint64_t*)pairs_out;
   if (M > 0) {
     const int64_t perM = round_up((M + G - 1) / G, kTile);
     const uint64_t* cq = stq;
@@ -1707,7 +1810,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
       const int64_t pp = p == 0 ? perw : perM;
       const uint32_t* seg = p == 0 ? mcount : nullptr;
       const int gg = p == 0 ? Gw : G;
-      uint64_t* nq = last ? (uint64_t*)pairs_out : outs[p & 1];
+      uint64_t* nq = (last && Mc == 0) ? (uint64_t*)pairs_out : outs[p & 1];
       if (jpass_wc() > (p == 0 ? 1 : 0))
         hipLaunchKernelGGL((downsweep_wc_kernel<2, PairSrc>), dim3(gg), dim3(kWcBlock), 0, s, PairSrc{cq}, nullptr, nq,
                            nn, pp, seg, gg, p * kRB, cnt, dbase);
@@ -1717,11 +1820,23 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
       tmark(last ? "j_pass_last" : "j_pass");
       cq = nq;
     }
+    mainq = (uint64_t*)cq;
+  }
+  if (Mc > 0) {  // merge the carried partials' matches in: for equal j they come first (older e1)
+    const int64_t tot = M + Mc;
+    (void)tot;
+    if (M > 0)
+      hipLaunchKernelGGL(merge_main_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, mainq, M, cps, Mc,
+                         (uint64_t*)pairs_out);
+    hipLaunchKernelGGL(merge_carried_kernel, dim3((unsigned)((Mc + 255) / 256)), dim3(256), 0, s, cps, Mc, mainq, M,
+                       (uint64_t*)pairs_out);
+    tmark("carry_merge");
   }
   if (tm) SM_HIP(hipEventRecord(tm->ev[3], s));
+  // carry out
+  build_carry(cand, hcf[0], a.st, hi.nattr, carry, sc, s);
   SM_HIP(hipStreamSynchronize(s));
-  sc.used = mark;
-  return M;
+  return finish(M + Mc);
 }
 
 }  // namespace sm

@@ -1,0 +1,1032 @@
+// Bucket-stack pipeline for `partition with (k of S) begin from every e1=S[c1] -> e2=S[c2] within T end` with
+// c2 = `e2.x OP e1.x`, OP one of > >= < <=.
+//
+// Why a stack. Per key, the reference keeps the e2 pre-processor's pending list in spawn order
+// (StreamPreStateProcessor.addState :208-221, updateState :268-271). An arriving event j walks that list
+// (processAndReturn :274-327): a partial whose e1 is more than T older than j is dropped (isExpired :102-121),
+// one that satisfies c2 emits and leaves (stateChanged), the rest stay; then j's own partial is appended
+// (e2 runs before e1: PatternMultiProcessStreamReceiver :39-45). Expired partials are a prefix of the list
+// (event time is non-decreasing) and, for an order compare, the partials c2 accepts are a suffix: after j the
+// list is monotone in the compared value (non-increasing for >, strictly decreasing for >=, mirrored for < <=),
+// so j accepts exactly the run of partials at the young end that it beats. The pending list is therefore a
+// monotone stack: pop while c2 holds (emitting in pop order, i.e. youngest e1 first), push j if c1. Expiry
+// is applied lazily: a popped candidate that has expired means every older one has too.
+//
+// Pipeline after key pass 0 (fastpath3.hip) has scattered the records into kBins buckets by the low key
+// digit (stable, so each bucket is in arrival order):
+//   stack_kernel  one workgroup per bucket (persistent), thread t owns in-bucket key h = t. The bucket is read
+//                 once, in slices of kS records: the slice is ranked by key in LDS (wave64 ballot peer masks),
+//                 every thread runs its key's events of the slice against its stack (top kC entries in
+//                 registers, older ones spilled to a per-thread HBM ring), the matches of the slice are put in
+//                 arrival order of j (count per j, block scan, placement) and written to the bucket's staging
+//                 run. Per (bucket, pass-0 chunk) the staging offset of the chunk's first j is recorded.
+//   order_kernel  per pass-0 chunk, tile by tile in arrival order: each thread owns one bucket and reads that
+//                 bucket's staged matches whose j falls in the tile (they are contiguous and in j order); a tile
+//                 count / scan / placement interleaves them by j. The output (i, j) pairs are written once,
+//                 in reference order (j, then i).
+// HBM traffic: records 16 B/event read, staged matches 8 B written + 8 B read, output 8 B per match. No sort by
+// j is needed: pass 0's bucket layout is inverted exactly, by ordinal ranges.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "fastpath_dev.h"
+
+namespace sm {
+
+namespace {
+
+constexpr int kSB = 512;       // threads per bucket workgroup: thread t owns in-bucket keys t and t + kSB (a 256-VGPR
+constexpr int kSW = kSB / 64;  // budget keeps both stacks and the slice machinery in registers)
+constexpr int kKeys = 1024;    // in-bucket keys
+constexpr int kSI = 8;         // records per thread per slice
+constexpr int kS = kSB * kSI;  // slice: 4096 records
+constexpr int kC = 6;          // stack entries held in registers
+constexpr int kQ = 32;         // spilled entries per thread (HBM ring)
+constexpr int kLog = 4096;     // match log of a slice: kLog / H entries per key thread ...
+constexpr int kOvf = 1024;     // ... and a shared overflow (more: the batch takes the sort / walk kernels)
+constexpr int kOB = 1024;      // order workgroup: thread d owns bucket d
+constexpr int kTB = 13;        // order tile: 2^kTB consecutive relative ordinals
+constexpr int kOT = 1 << kTB;
+constexpr int kOCap = 12288;   // matches of a tile staged in LDS before one coalesced write
+constexpr int kGT = 16;        // consecutive tiles per order workgroup
+
+static_assert(kBins == kKeys && kKeys == 2 * kSB && kBins == kOB, "two in-bucket keys per thread, one bucket per "
+              "order thread");
+
+enum : uint32_t { SE_OVERFLOW = 1, SE_LOG = 2, SE_NAN = 4, SE_CAND = 8, SE_ORD = 16 };
+
+struct StackArgs {
+  const uint4* rec;
+  const uint32_t* dbase;
+  int64_t ntiles;  // order tiles: relative ordinals [0, ntiles << kTB)
+  int64_t n;
+  int H;
+  int64_t kmin;
+  int64_t within;
+  int64_t ts0;
+  // exact comparison of equal inexact codes
+  bool exact_codes;
+  int vtype;
+  const void* vcol;
+  const int64_t* ord;
+  int64_t obase;
+  int32_t o0;  // relative ordinal of the batch's first event; carried partials lie before it
+  // carried partials (carry_in_kernel): cin[i] = {ordinal - base, code, ts - ts0}, rows [cstart, cend) of a key
+  const uint4* cin;
+  const uint32_t* cstart;
+  const uint32_t* cend;
+  const int64_t* crow;
+  int cwidth, vattr;
+  // outputs
+  const uint32_t* sbase;
+  uint64_t* stage;
+  uint32_t* mstart;
+  uint32_t* mtot;
+  uint4* spill;
+  int64_t* cand;
+  uint32_t* cand_n;
+  uint32_t cand_cap;
+  uint32_t* err;
+  unsigned long long* stamps;  // optional (SM_STACK_STAMPS=1): clock ticks per kernel phase, summed over waves
+  int dbg;                     // diagnostic mode (SM_STACK_DEBUG): 1 = skip the stacks (wrong results; timing only)
+  unsigned long long* counts;  // with stamps: events, pops, refills, spills, exact compares, log overflows
+};
+
+// Exact value of a compared attribute: a batch row's column, or a carried partial's stored value.
+struct ExactSrc {
+  bool exact_codes;
+  int vtype, vattr, cwidth;
+  const void* vcol;
+  const int64_t* ord;
+  int64_t obase, n;
+  const int64_t* crow;
+  int32_t o0;
+  uint32_t cs, ce;  // this key's carried rows
+  __device__ bool carried(uint32_t o) const { return (int32_t)o < o0; }
+  __device__ int64_t row_of(uint32_t o) const {
+    if (!ord) return o;
+    const int64_t want = (int64_t)o + obase;
+    int64_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ord[mid] < want) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  }
+  __device__ int64_t carry_row(uint32_t o) const {
+    const int64_t want = (int64_t)(int32_t)o + obase;
+    uint32_t lo = cs, hi = ce;
+    while (lo + 1 < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (crow[(int64_t)mid * cwidth + 1] <= want) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  }
+  __device__ double fval(uint32_t o) const {
+    if (carried(o)) return __longlong_as_double((long long)crow[carry_row(o) * cwidth + 3 + vattr]);
+    const int64_t r = row_of(o);
+    return vtype == T_FLOAT ? (double)((const float*)vcol)[r] : ((const double*)vcol)[r];
+  }
+  __device__ int64_t ival(uint32_t o) const {
+    if (carried(o)) return crow[carry_row(o) * cwidth + 3 + vattr];
+    const int64_t r = row_of(o);
+    return vtype == T_INT ? (int64_t)((const int32_t*)vcol)[r] : ((const int64_t*)vcol)[r];
+  }
+};
+
+// equal inexact codes (or NaN): the exact values decide. Out of line: rare, and its binary searches must not
+// hold registers in the event loop.
+template <int OP, bool FP>
+__device__ __noinline__ bool c2_exact(const ExactSrc& ex, uint32_t oi, uint32_t oj) {
+  if constexpr (FP) return cmp_fixed<OP>(ex.fval(oj), ex.fval(oi));
+  else return cmp_fixed<OP>(ex.ival(oj), ex.ival(oi));
+}
+
+// c2 = `e2.x OP e1.x` for partial i (code ci, ordinal oi) and event j
+template <int OP, bool FP>
+__device__ __forceinline__ bool c2_hit(const ExactSrc& ex, uint32_t ci, uint32_t oi, uint32_t cj, uint32_t oj) {
+  const bool nan = FP & ((ci == kNanCode) | (cj == kNanCode));
+  if (!nan & (ex.exact_codes | (ci != cj))) return cmp_fixed<OP>(cj, ci);
+  return c2_exact<OP, FP>(ex, oi, oj);
+}
+
+struct Stack {
+  uint32_t o[kC], c[kC];
+  int32_t t[kC];
+  int n;       // entries in registers
+  int hb, hn;  // spill ring: head, count
+};
+
+__device__ __forceinline__ void st_pop(Stack& s) {
+#pragma unroll
+  for (int k = 0; k + 1 < kC; ++k) {
+    s.o[k] = s.o[k + 1];
+    s.c[k] = s.c[k + 1];
+    s.t[k] = s.t[k + 1];
+  }
+  --s.n;
+}
+
+// the registers ran empty: bring back the youngest spilled entry (one at a time; spills are rare)
+__device__ __forceinline__ void st_refill(Stack& s, const uint4* sp) {
+  const uint4 e = sp[(s.hb + s.hn - 1) & (kQ - 1)];
+  s.o[0] = e.x;
+  s.c[0] = e.y;
+  s.t[0] = (int32_t)e.z;
+  s.hn -= 1;
+  s.n = 1;
+}
+
+// push (o, c, t) on top; `now` = event time of the pushing event (entries older than now - within are dead)
+__device__ __forceinline__ void st_push(Stack& s, uint4* sp, uint32_t o, uint32_t c, int32_t t, int32_t now,
+                                        int64_t within, uint32_t* err) {
+  if (s.n == kC) {
+    if (within >= 0 && now - s.t[kC - 1] > (int32_t)within) {  // the register bottom and all spilled are dead
+      s.hn = 0;
+      s.n = kC - 1;
+    } else {
+      if (s.hn == kQ) {  // free the ring's dead head first
+        while (s.hn > 0 && within >= 0 && now - (int32_t)sp[s.hb & (kQ - 1)].z > (int32_t)within) {
+          s.hb = (s.hb + 1) & (kQ - 1);
+          --s.hn;
+        }
+        if (s.hn == kQ) {  // more than kC + kQ live partials on one key: the walk pipeline takes the batch
+          atomicOr(err, SE_OVERFLOW);
+          s.hb = (s.hb + 1) & (kQ - 1);
+          --s.hn;
+        }
+      }
+      sp[(s.hb + s.hn) & (kQ - 1)] = make_uint4(s.o[kC - 1], s.c[kC - 1], (uint32_t)s.t[kC - 1], 0u);
+      ++s.hn;
+      s.n = kC - 1;
+    }
+  }
+#pragma unroll
+  for (int k = kC - 1; k > 0; --k) {
+    s.o[k] = s.o[k - 1];
+    s.c[k] = s.c[k - 1];
+    s.t[k] = s.t[k - 1];
+  }
+  s.o[0] = o;
+  s.c[0] = c;
+  s.t[0] = t;
+  ++s.n;
+}
+
+// block-wide exclusive scan of one value per thread (NT threads); returns the total through *tot
+template <int NT = kOB>
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* lw, uint32_t* tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) lw[w] = inc;
+  lds_barrier();
+  uint32_t r = inc - v, t = 0;
+  for (int q = 0; q < NT / 64; ++q) {
+    const uint32_t x = lw[q];
+    if (q < w) r += x;
+    t += x;
+  }
+  *tot = t;
+  return r;
+}
+
+template <int OP, bool FP>
+__global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
+  __shared__ uint4 rec[kS];         // the slice grouped by key (arrival order within a key); .x = slice position | c1
+  __shared__ uint32_t ordt[kS];     // ordinal of each slice position (arrival order)
+  __shared__ uint64_t area[kLog];   // ranking: per-wave key counts (u16 [kSW][kKeys]); then the match log
+  __shared__ uint64_t ovf[kOvf];    // log entries beyond a thread's slots
+  __shared__ uint16_t hst[kKeys], hcn[kKeys];
+  __shared__ uint16_t jcnt[kS], joff[kS];
+  __shared__ uint32_t lw[kSW];
+  __shared__ uint32_t s_ovf, s_slice_tot, s_lastj;
+
+  uint16_t(*wcnt)[kKeys] = (uint16_t(*)[kKeys])area;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // within < 2^30 and event times in [-2^30, 2^30) relative to the batch: differences fit 32 bits
+  const int32_t within32 = (int32_t)a.within;
+  // phase clock (diagnostic): 0 slice setup, 1 ranking, 2 placement, 3 stacks, 4 scan + tiles, 5 match writes,
+  // 6 bucket tail + carry out
+  unsigned long long st_acc[7] = {0, 0, 0, 0, 0, 0, 0}, st_last = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+#define SM_PHASE(i)                                               \
+  do {                                                            \
+    if (a.stamps) {                                               \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+      st_acc[i] += t_ - st_last;                                  \
+      st_last = t_;                                               \
+    }                                                             \
+  } while (0)
+  const uint64_t lt = lanemask_lt();
+  // the two keys of this thread: h = tid (A) and h = tid + kSB (B)
+  const bool hasA = tid < a.H, hasB = tid + kSB < a.H;
+  uint4* spA = a.spill + ((int64_t)blockIdx.x * kKeys + tid) * kQ;
+  uint4* spB = spA + (int64_t)kSB * kQ;
+  const uint32_t kSlots = kLog / (uint32_t)(a.H < kSB ? a.H : kSB);
+  unsigned long long cn[2] = {0, 0};
+
+  for (int d = blockIdx.x; d < kBins; d += gridDim.x) {
+    const int64_t b0 = a.dbase[d];
+    const int64_t b1 = d + 1 < kBins ? (int64_t)a.dbase[d + 1] : a.n;
+    const int64_t blen = b1 - b0;
+    const int64_t sb = a.sbase[d];
+    uint32_t* mst = a.mstart + (int64_t)d * (a.ntiles + 1);
+    Stack sA, sB;
+    sA.n = sA.hb = sA.hn = 0;
+    sB.n = sB.hb = sB.hn = 0;
+    ExactSrc exA{a.exact_codes, a.vtype, a.vattr, a.cwidth, a.vcol, a.ord, a.obase, a.n, a.crow, a.o0, 0u, 0u};
+    ExactSrc exB = exA;
+    const uint32_t krA = ((uint32_t)tid << kRB) | (uint32_t)d, krB = ((uint32_t)(tid + kSB) << kRB) | (uint32_t)d;
+    // carried partials first (oldest first)
+    auto carry_in = [&](Stack& s, ExactSrc& ex, uint4* sp, uint32_t kr) {
+      ex.cs = a.cstart[kr];
+      ex.ce = a.cend[kr];
+      for (uint32_t q = ex.cs; q < ex.ce; ++q) {
+        const uint4 e = a.cin[q];
+        st_push(s, sp, e.x, e.y, (int32_t)e.z, (int32_t)e.z, a.within, a.err);
+      }
+    };
+    if (a.cin) {
+      if (hasA) carry_in(sA, exA, spA, krA);
+      if (hasB) carry_in(sB, exB, spB, krB);
+    }
+    // event time of each key's last event in the batch: partials it did not find expired stay pending
+    int32_t tlA = 0, tlB = 0;
+    bool seenA = false, seenB = false;
+    if (tid == 0) s_lastj = 0xffffffffu;  // ordinal before the bucket's first record (none)
+    uint32_t mrun = 0;                    // matches of the bucket so far
+
+    uint4 pre[kSI];
+    auto prefetch = [&](int64_t q) {
+#pragma unroll
+      for (int k = 0; k < kSI; ++k) {
+        const int64_t p = q + w * 64 * kSI + k * 64 + lane;
+        if (p < blen) {
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 v = __builtin_nontemporal_load((const u32x4*)a.rec + b0 + p);
+          pre[k] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+      }
+    };
+    prefetch(0);
+
+    for (int64_t q = 0; q < blen; q += kS) {
+      const int sn = (int)(blen - q < kS ? blen - q : kS);
+      lds_barrier();  // previous slice's readers are done
+      for (int k = tid; k < kSW * kKeys / 4; k += kSB) area[k] = 0;
+      if (tid == 0) s_ovf = 0;
+      lds_barrier();
+      SM_PHASE(0);
+
+      // ---- rank by key, stable (arrival order) within a key; the slice lands in LDS grouped by key
+      uint32_t hk[kSI], lp[kSI];
+#pragma unroll
+      for (int k = 0; k < kSI; ++k) {
+        const int e = w * 64 * kSI + k * 64 + lane;
+        const bool valid = e < sn;
+        hk[k] = valid ? (pre[k].x & kKeyMask) >> kRB : 0u;
+        const uint64_t peers = peer_mask(hk[k], valid);
+        uint32_t old = 0;
+        if (valid) old = wcnt[w][hk[k]];
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        if (valid && below == 0) wcnt[w][hk[k]] = (uint16_t)(old + (uint32_t)__popcll(peers));
+        lp[k] = old + below;
+      }
+      lds_barrier();
+      {
+        // keys 2 * tid and 2 * tid + 1: exclusive over waves in place, totals, block scan over keys
+        uint32_t r2[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int h = 2 * tid + u;
+          uint32_t r = 0;
+          for (int qq = 0; qq < kSW; ++qq) {
+            const uint32_t c = wcnt[qq][h];
+            wcnt[qq][h] = (uint16_t)r;
+            r += c;
+          }
+          hcn[h] = (uint16_t)r;
+          r2[u] = r;
+        }
+        uint32_t tot;
+        const uint32_t st0 = block_excl<kSB>(r2[0] + r2[1], lw, &tot);
+        hst[2 * tid] = (uint16_t)st0;
+        hst[2 * tid + 1] = (uint16_t)(st0 + r2[0]);
+      }
+      lds_barrier();
+      SM_PHASE(1);
+#pragma unroll
+      for (int k = 0; k < kSI; ++k) {
+        const int e = w * 64 * kSI + k * 64 + lane;
+        if (e < sn) {
+          const uint4 r = pre[k];
+          rec[hst[hk[k]] + wcnt[w][hk[k]] + lp[k]] = make_uint4((uint32_t)e | (r.x & 0x80000000u), r.y, r.z, r.w);
+          ordt[e] = r.y;
+        }
+      }
+      lds_barrier();
+      SM_PHASE(2);
+
+      // ---- each key's events of the slice against its stack; matches go to the log (the thread's slots, then
+      // the shared overflow)
+      // One event j of a key against the key's stack. The register part is evaluated at once: entry k is popped
+      // iff entries 0..k all satisfy c2 and none has expired (the stack is monotone, so j accepts a prefix of it);
+      // the first entry that stops the run clears the whole stack when it has expired. Only a run through all the
+      // register entries with spilled ones behind them goes on entry by entry (rare).
+      auto log_put = [&](uint32_t& nlog, uint64_t ent) {
+        if (nlog < kSlots) {
+          area[tid * kSlots + nlog] = ent;
+        } else {
+          const uint32_t o = atomicAdd(&s_ovf, 1u);
+          if (o < kOvf) ovf[o] = ent;
+          else atomicOr(a.err, SE_LOG);
+        }
+        ++nlog;
+      };
+      auto step = [&](Stack& s, const ExactSrc& ex, uint4* sp, uint32_t& nlog, const uint4 r) {
+        const uint32_t e = r.x & 0xffffu;
+        const int32_t jt = (int32_t)r.w;
+        const uint32_t cj = r.z, oj = r.y;
+        if (FP && cj == kNanCode) atomicOr(a.err, SE_NAN);
+        uint32_t hit = 0, exp = 0, tie = 0;
+#pragma unroll
+        for (int k = 0; k < kC; ++k) {
+          const bool live = k < s.n;
+          const bool x = within32 >= 0 && jt - s.t[k] > within32;
+          const bool t = !a.exact_codes && s.c[k] == cj;
+          const bool nan = FP && ((s.c[k] == kNanCode) | (cj == kNanCode));
+          hit |= (live && cmp_fixed<OP>(cj, s.c[k])) ? (1u << k) : 0u;
+          exp |= (live && x) ? (1u << k) : 0u;
+          tie |= (live && (t || nan)) ? (1u << k) : 0u;
+        }
+        if (tie) {  // equal inexact codes: the exact values decide (out of line)
+#pragma unroll
+          for (int k = 0; k < kC; ++k)
+            if ((tie >> k) & 1u) {
+              const bool h = c2_exact<OP, FP>(ex, s.o[k], oj);
+              hit = h ? (hit | (1u << k)) : (hit & ~(1u << k));
+            }
+        }
+        const uint32_t ok = hit & ~exp;
+        uint32_t npop = (uint32_t)__builtin_ctz(~ok);  // leading entries popped
+        if (npop > (uint32_t)s.n) npop = s.n;
+#pragma unroll
+        for (int k = 0; k < kC; ++k)
+          if ((uint32_t)k < npop) log_put(nlog, (uint64_t)s.o[k] | ((uint64_t)(e | ((uint32_t)k << 16)) << 32));
+        const bool stop_expired = npop < (uint32_t)s.n && ((exp >> npop) & 1u);
+        // shift the register part down by npop (npop < 8)
+#pragma unroll
+        for (int b = 1; b < kC; b <<= 1)
+          if (npop & b) {
+#pragma unroll
+            for (int k = 0; k < kC; ++k)
+              if (k + b < kC) {
+                s.o[k] = s.o[k + b];
+                s.c[k] = s.c[k + b];
+                s.t[k] = s.t[k + b];
+              }
+          }
+        s.n -= (int)npop;
+        if (stop_expired) {  // the entry that stopped the run has expired: so has every older one
+          s.n = 0;
+          s.hn = 0;
+        } else if (s.n == 0 && s.hn > 0) {  // ran through the registers: continue into the spill
+          for (;;) {
+            st_refill(s, sp);
+            if (within32 >= 0 && jt - s.t[0] > within32) {
+              s.n = 0;
+              s.hn = 0;
+              break;
+            }
+            if (!c2_hit<OP, FP>(ex, s.c[0], s.o[0], cj, oj)) break;
+            log_put(nlog, (uint64_t)s.o[0] | ((uint64_t)(e | (npop << 16)) << 32));
+            ++npop;
+            st_pop(s);
+            if (s.hn == 0) break;
+          }
+        }
+        jcnt[e] = (uint16_t)npop;
+        if (r.x >> 31) st_push(s, sp, oj, cj, jt, jt, a.within, a.err);
+        if (a.counts) {
+          cn[0] += 1;
+          cn[1] += npop;
+        }
+      };
+      uint32_t nlog = 0;
+      if (a.dbg == 1)
+        for (int k = tid; k < sn; k += kSB) jcnt[k] = 0;
+      if (a.dbg != 1) {
+        const int cA = hasA ? hcn[tid] : 0, cB = hasB ? hcn[tid + kSB] : 0;
+        const int sA0 = hst[tid], sB0 = hst[tid + kSB];
+        const int cmax = cA > cB ? cA : cB;
+        if (cA) {
+          tlA = (int32_t)rec[sA0 + cA - 1].w;
+          seenA = true;
+        }
+        if (cB) {
+          tlB = (int32_t)rec[sB0 + cB - 1].w;
+          seenB = true;
+        }
+        // the two keys' events interleaved: two independent dependency chains per thread
+        for (int x = 0; x < cmax; ++x) {
+          if (x < cA) step(sA, exA, spA, nlog, rec[sA0 + x]);
+          if (x < cB) step(sB, exB, spB, nlog, rec[sB0 + x]);
+        }
+      }
+      SM_PHASE(3);
+      // ---- matches of the slice in arrival order of j: exclusive scan of the per-j counts
+      if (q + kS < blen) prefetch(q + kS);  // the next slice's loads overlap the scan and the match writes
+      lds_barrier();
+      {
+        uint32_t v[kSI], sum = 0;
+#pragma unroll
+        for (int k = 0; k < kSI; ++k) {
+          const int e = tid * kSI + k;
+          v[k] = e < sn ? jcnt[e] : 0u;
+          sum += v[k];
+        }
+        uint32_t tot;
+        uint32_t r = block_excl<kSB>(sum, lw, &tot);
+        const uint32_t jprev = tid == 0 ? s_lastj : 0u;
+#pragma unroll
+        for (int k = 0; k < kSI; ++k) {
+          const int e = tid * kSI + k;
+          if (e < sn) {
+            joff[e] = (uint16_t)r;
+            // ordinal tiles whose first ordinal falls in (previous record's ordinal, this record's]: their first
+            // match in this bucket is this record's first
+            const uint32_t j = ordt[e];
+            const uint32_t jp = e == 0 ? jprev : ordt[e - 1];
+            const uint32_t t0 = jp == 0xffffffffu ? 0u : (jp >> kTB) + 1u;
+            for (uint32_t t = t0; t <= (j >> kTB); ++t) mst[t] = mrun + r;
+          }
+          r += v[k];
+        }
+        if (tid == 0) s_slice_tot = tot;
+      }
+      lds_barrier();
+      SM_PHASE(4);
+      if (tid == 0) s_lastj = ordt[sn - 1];
+      const uint32_t stot = s_slice_tot;
+      const uint32_t no = s_ovf < kOvf ? s_ovf : kOvf;
+      auto emit = [&](uint64_t ent) {
+        const uint32_t io = (uint32_t)ent, pe = (uint32_t)(ent >> 32);
+        const uint32_t e = pe & 0xffffu, pop = pe >> 16;
+        const uint32_t pos = mrun + joff[e] + (jcnt[e] - 1u - pop);
+        a.stage[sb + pos] = ((uint64_t)ordt[e] << 32) | io;
+      };
+      for (uint32_t k = 0; k < nlog && k < kSlots; ++k) emit(area[tid * kSlots + k]);
+      for (uint32_t k = tid; k < no; k += kSB) emit(ovf[k]);
+      mrun += stot;
+      SM_PHASE(5);
+    }
+    // tiles after the bucket's last record start at its end
+    __syncthreads();
+    {
+      const uint32_t jl = s_lastj;
+      const uint32_t t0 = jl == 0xffffffffu ? 0u : (jl >> kTB) + 1u;
+      for (uint32_t t = t0 + tid; t <= (uint32_t)a.ntiles; t += kSB) mst[t] = mrun;
+      if (tid == 0) a.mtot[d] = mrun;
+    }
+
+    // ---- carry out: the partials still pending in the reference, i.e. those the key's last event found neither
+    // matched nor expired (a key without events in this batch keeps all of its carried partials)
+    auto keep_of = [&](const Stack& s, const uint4* sp, int32_t tl, bool seen) {
+      auto pending = [&](int32_t t) { return !seen || a.within < 0 || (int64_t)tl - t <= a.within; };
+      uint32_t keep = 0;
+#pragma unroll
+      for (int k = 0; k < kC; ++k)
+        if (k < s.n && pending(s.t[k])) ++keep;
+      for (int k = 0; k < s.hn; ++k)
+        if (pending((int32_t)sp[(s.hb + k) & (kQ - 1)].z)) ++keep;
+      return keep;
+    };
+    const uint32_t keepA = hasA ? keep_of(sA, spA, tlA, seenA) : 0u;
+    const uint32_t keepB = hasB ? keep_of(sB, spB, tlB, seenB) : 0u;
+    const uint32_t keep = keepA + keepB;
+    uint32_t inc = keep;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    uint32_t base = 0;
+    if (lane == 63 && inc) base = atomicAdd(a.cand_n, inc);
+    base = __shfl(base, 63, 64) + inc - keep;
+    auto put_all = [&](const Stack& s, const ExactSrc& ex, const uint4* sp, int32_t tl, bool seen, uint32_t kr) {
+      auto pending = [&](int32_t t) { return !seen || a.within < 0 || (int64_t)tl - t <= a.within; };
+      const int64_t key = a.kmin + (int64_t)kr;
+      auto put = [&](uint32_t o, int32_t t) {
+        if (!pending(t)) return;
+        if (base < a.cand_cap) {
+          int64_t* c = a.cand + 4 * (int64_t)base;
+          c[0] = key;
+          c[1] = (int64_t)(int32_t)o + a.obase;
+          c[2] = (int64_t)t + a.ts0;
+          c[3] = ex.carried(o) ? -(int64_t)ex.carry_row(o) - 1 : ex.row_of(o);
+        } else {
+          atomicOr(a.err, SE_CAND);
+        }
+        ++base;
+      };
+      // order does not matter: the carry is sorted
+      for (int k = 0; k < s.hn; ++k) {
+        const uint4 e = sp[(s.hb + k) & (kQ - 1)];
+        put(e.x, (int32_t)e.z);
+      }
+#pragma unroll
+      for (int k = kC - 1; k >= 0; --k)
+        if (k < s.n) put(s.o[k], s.t[k]);
+    };
+    if (keepA) put_all(sA, exA, spA, tlA, seenA, krA);
+    if (keepB) put_all(sB, exB, spB, tlB, seenB, krB);
+    __syncthreads();  // LDS of this bucket is free for the next one
+    SM_PHASE(6);
+  }
+  if (a.stamps && lane == 0)
+    for (int i = 0; i < 7; ++i) atomicAdd(&a.stamps[i], st_acc[i]);
+  if (a.counts) {
+    atomicAdd(&a.counts[0], cn[0]);
+    atomicAdd(&a.counts[1], cn[1]);
+  }
+#undef SM_PHASE
+}
+
+// mstart [d][t] (written bucket by bucket) → [t][d] (read tile by tile)
+__global__ void __launch_bounds__(256) transpose_kernel(const uint32_t* __restrict__ src, int64_t cols,
+                                                        uint32_t* __restrict__ dst) {
+  __shared__ uint32_t tile[32][33];
+  const int64_t c0 = (int64_t)blockIdx.x * 32, r0 = (int64_t)blockIdx.y * 32;  // src rows = buckets
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int64_t c = c0 + tx;
+    tile[k][tx] = c < cols ? src[(r0 + k) * cols + c] : 0u;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int64_t c = c0 + k;
+    if (c < cols) dst[c * kBins + r0 + tx] = tile[tx][k];
+  }
+}
+
+struct OrderArgs {
+  const uint64_t* stage;
+  const uint32_t* sbase;
+  const uint32_t* mt;  // [t][d]: matches of bucket d whose j precedes tile t
+  int64_t ntiles;
+  uint64_t* out;
+};
+
+// Tiles [blockIdx.x * kGT, +kGT) of kOT ordinals each, in order. Per tile, bucket d's staged matches with j in
+// the tile are one contiguous segment in (j, i) order (a j's matches are consecutive in it); 16 lanes read a
+// bucket's segment together (one 128-byte line per 16 matches). Pass A counts matches per ordinal (LDS atomics),
+// a block scan turns the counts into offsets, pass B re-reads the segments (cache-hot) and places each match at
+// offset of its j + its rank among the j's matches in an LDS image of the tile's output, which leaves as one
+// contiguous, coalesced run (its base = matches whose j precedes the tile, summed over buckets). A tile whose
+// output exceeds the LDS image writes its matches to their places directly.
+__global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
+  __shared__ uint32_t cnt[kOT];
+  __shared__ uint64_t obuf[kOCap];
+  __shared__ uint32_t sst[kBins], slen[kBins];
+  __shared__ uint32_t lw[kOB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const uint64_t gmask = 0xffffull << (g * 16);
+  const int64_t tb = (int64_t)blockIdx.x * kGT;
+  const int64_t te = tb + kGT < a.ntiles ? tb + kGT : a.ntiles;
+  uint32_t ms = a.mt[tb * kBins + tid];
+  uint32_t tot;
+  (void)block_excl(ms, lw, &tot);
+  int64_t out = tot;  // matches whose j precedes the tile
+  for (int64_t t = tb; t < te; ++t) {
+    const uint32_t me = a.mt[(t + 1) * kBins + tid];
+    const uint32_t j0 = (uint32_t)(t << kTB);
+    lds_barrier();  // previous tile's readers are done
+    sst[tid] = a.sbase[tid] + ms;
+    slen[tid] = me - ms;
+    for (int e = tid; e < kOT; e += kOB) cnt[e] = 0;
+    ms = me;
+    lds_barrier();
+    // pass A: matches per ordinal. The first 16 matches of each of the wave's 64 buckets are loaded at once (one
+    // load per round, all in flight) and kept for pass B; longer segments (rare) are walked chunk by chunk.
+    uint64_t v0[16];
+    uint32_t s0r[16], lenr[16];
+    bool more = false;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = w * 64 + r * 4 + g;
+      s0r[r] = sst[d];
+      lenr[r] = slen[d];
+      more |= lenr[r] > 16u;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v0[r] = (uint32_t)l16 < lenr[r] ? a.stage[s0r[r] + l16] : 0ull;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if ((uint32_t)l16 < lenr[r]) atomicAdd(&cnt[(uint32_t)(v0[r] >> 32) - j0], 1u);
+    if (__any(more))
+      for (int r = 0; r < 16; ++r)
+        for (uint32_t c = 16; __any(c < lenr[r]); c += 16)
+          if (c + l16 < lenr[r]) atomicAdd(&cnt[(uint32_t)(a.stage[s0r[r] + c + l16] >> 32) - j0], 1u);
+    lds_barrier();
+    {
+      constexpr int kPer = kOT / kOB;
+      uint32_t v[kPer], sum = 0;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        v[k] = cnt[tid * kPer + k];
+        sum += v[k];
+      }
+      uint32_t r = block_excl(sum, lw, &tot);
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        cnt[tid * kPer + k] = r;
+        r += v[k];
+      }
+    }
+    lds_barrier();
+    const bool staged = tot <= (uint32_t)kOCap;
+    // pass B: rank of each match among its j's matches = its segment position - the position where its j's run
+    // starts (runs may continue from the previous 16-match chunk of the segment)
+    auto place = [&](uint64_t v, bool valid, uint32_t c, uint32_t& cj, uint32_t& cstart) {
+      const uint32_t j = (uint32_t)(v >> 32);
+      uint32_t jp = __shfl_up(j, 1, 16);
+      if (l16 == 0) jp = cj;
+      const bool start = valid && j != jp;
+      const uint32_t sm = (uint32_t)((__ballot(start) & gmask) >> (g * 16));
+      const uint32_t upto = sm & ((2u << l16) - 1u);
+      const uint32_t rs = upto ? c + 31u - (uint32_t)__clz(upto) : cstart;
+      if (valid) {
+        const uint32_t pos = cnt[j - j0] + (c + l16 - rs);
+        if (staged) obuf[pos] = v;
+        else a.out[out + pos] = v;
+      }
+      const uint32_t vm = (uint32_t)((__ballot(valid) & gmask) >> (g * 16));
+      const int last = vm ? 31 - __clz(vm) : 0;
+      cj = __shfl(j, last, 16);
+      cstart = __shfl(rs, last, 16);
+    };
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      uint32_t cj = 0xffffffffu, cstart = 0;
+      place(v0[r], (uint32_t)l16 < lenr[r], 0, cj, cstart);
+      if (__any(lenr[r] > 16u))
+        for (uint32_t c = 16; __any(c < lenr[r]); c += 16) {
+          const bool valid = c + l16 < lenr[r];
+          place(valid ? a.stage[s0r[r] + c + l16] : 0ull, valid, c, cj, cstart);
+        }
+    }
+    lds_barrier();
+    if (staged)
+      for (uint32_t k = tid; k < tot; k += kOB) a.out[out + k] = obuf[k];
+    out += tot;
+  }
+}
+
+// Carried partials for this batch: codes of the compared value and each key's row range. Keys outside the
+// batch's key range see no event: their partials go straight to the carry-out candidates.
+template <typename VT>
+__global__ void carry_in_kernel(const int64_t* __restrict__ rows, int64_t n, int w, int vattr, int vtype, int vmode,
+                                int64_t vmin, int64_t kmin, int64_t span, int64_t obase, int64_t o0, int64_t ts0,
+                                uint4* __restrict__ cin, uint32_t* __restrict__ cstart, uint32_t* __restrict__ cend,
+                                uint32_t* __restrict__ ccnt, int64_t* __restrict__ cand, uint32_t* __restrict__ cand_n,
+                                uint32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t* r = rows + i * w;
+  const int64_t key = r[0];
+  const int64_t kr = key - kmin;
+  if (kr < 0 || kr > span) {
+    const uint32_t q = atomicAdd(cand_n, 1u);
+    int64_t* c = cand + 4 * (int64_t)q;
+    c[0] = key;
+    c[1] = r[1];
+    c[2] = r[2];
+    c[3] = -i - 1;
+    return;
+  }
+  const int64_t o = r[1] - obase;
+  if (o >= o0 || o < INT32_MIN) atomicOr(err, SE_ORD);
+  int64_t t = r[2] - ts0;  // older than 2^30 ms: dead for any event of this batch (within < 2^30)
+  if (t < -(1ll << 30)) t = -(1ll << 30);
+  const StackVal v = uncanon((uint64_t)r[3 + vattr], vtype);
+  uint32_t code;
+  if constexpr (std::is_same<VT, float>::value) code = vcode<float>((float)v.d, vmode, vmin);
+  else if constexpr (std::is_same<VT, double>::value) code = vcode<double>(v.d, vmode, vmin);
+  else if constexpr (std::is_same<VT, int32_t>::value) code = vcode<int32_t>((int32_t)v.i, vmode, vmin);
+  else code = vcode<int64_t>(v.i, vmode, vmin);
+  cin[i] = make_uint4((uint32_t)(int32_t)o, code, (uint32_t)(int32_t)t, 0u);
+  if (i == 0 || rows[(i - 1) * w] != key) cstart[kr] = (uint32_t)i;
+  if (i == n - 1 || rows[(i + 1) * w] != key) cend[kr] = (uint32_t)(i + 1);
+  atomicAdd(&ccnt[kr & (kBins - 1)], 1u);
+}
+
+// staging run of each bucket: its records plus its carried partials (a bucket's matches cannot exceed them)
+__global__ void __launch_bounds__(kOB) stage_base_kernel(const uint32_t* __restrict__ dbase,
+                                                         const uint32_t* __restrict__ ccnt, uint32_t* __restrict__ sbase,
+                                                         uint32_t* __restrict__ stot) {
+  __shared__ uint32_t lw[kOB / 64];
+  const int d = threadIdx.x;
+  const uint32_t c = ccnt ? ccnt[d] : 0u;
+  uint32_t tot;
+  const uint32_t r = block_excl(c, lw, &tot);
+  sbase[d] = dbase[d] + r;
+  if (d == 0) *stot = tot;
+}
+
+// ---- carry out
+__global__ void carry_rows_kernel(const int64_t* __restrict__ cand, int64_t n, const NfaStream* __restrict__ st,
+                                  int nattr, const int64_t* __restrict__ old, int w, int64_t* __restrict__ rows,
+                                  uint64_t* __restrict__ kord, uint64_t* __restrict__ kkey, uint32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t* c = cand + 4 * i;
+  int64_t* r = rows + i * w;
+  if (c[3] >= 0) {
+    r[0] = c[0];
+    r[1] = c[1];
+    r[2] = c[2];
+    for (int k = 0; k < nattr; ++k) r[3 + k] = (int64_t)canon(col_value(st, k, c[3]), st->types[k]);
+  } else {  // a carried partial that stays pending: its row unchanged
+    const int64_t* o = old + (-c[3] - 1) * w;
+    for (int k = 0; k < w; ++k) r[k] = o[k];
+  }
+  kord[i] = (uint64_t)c[1] ^ 0x8000000000000000ull;
+  kkey[i] = (uint64_t)c[0] ^ 0x8000000000000000ull;
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void gather_u64_kernel(const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx, int64_t n,
+                                  uint64_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+
+__global__ void gather_rows_kernel(const int64_t* __restrict__ src, const uint32_t* __restrict__ idx, int64_t n, int w,
+                                   int64_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t* s = src + (int64_t)idx[i] * w;
+  for (int k = 0; k < w; ++k) dst[i * w + k] = s[k];
+}
+
+inline dim3 grid_of(int64_t n, int t = 256) { return dim3((unsigned)std::max<int64_t>(1, (n + t - 1) / t)); }
+
+template <int OP, bool FP>
+void launch_stack_t(const StackArgs& sa, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((stack_kernel<OP, FP>), dim3(grid), dim3(kSB), 0, s, sa);
+}
+
+}  // namespace
+
+void FastCarry::reserve(int64_t rows_needed, int w) {
+  if (rows_needed <= cap && w == width) return;
+  int64_t* p = nullptr;
+  const int64_t c = std::max<int64_t>(rows_needed, std::max<int64_t>(cap * 2, 1024));
+  SM_HIP(hipMalloc(&p, (size_t)c * w * 8));
+  if (rows && n && w == width) SM_HIP(hipMemcpy(p, rows, (size_t)n * w * 8, hipMemcpyDeviceToDevice));
+  if (rows) SM_HIP(hipFree(rows));
+  rows = p;
+  cap = c;
+  width = w;
+}
+
+void FastCarry::release() {
+  if (rows) (void)hipFree(rows);
+  rows = nullptr;
+  cap = n = 0;
+}
+
+void build_carry(const int64_t* cand, int64_t ncand, const NfaStream* st, int nattr, FastCarry& carry, Scratch& sc,
+                 hipStream_t s) {
+  const int w = 3 + nattr;
+  if (ncand == 0) {
+    carry.n = 0;
+    carry.width = w;
+    return;
+  }
+  const size_t mark = sc.used;
+  int64_t* rows = (int64_t*)sc.take((size_t)ncand * w * 8);
+  uint64_t* kord = (uint64_t*)sc.take((size_t)ncand * 8);
+  uint64_t* kkey = (uint64_t*)sc.take((size_t)ncand * 8);
+  uint64_t* k2 = (uint64_t*)sc.take((size_t)ncand * 8);
+  uint32_t* idx = (uint32_t*)sc.take((size_t)ncand * 4);
+  uint32_t* idx2 = (uint32_t*)sc.take((size_t)ncand * 4);
+  hipLaunchKernelGGL(carry_rows_kernel, grid_of(ncand), dim3(256), 0, s, cand, ncand, st, nattr,
+                     (const int64_t*)carry.rows, w, rows, kord, kkey, idx);
+  // stable sort by ordinal, then by key
+  bool alt = radix_sort_pairs<uint64_t>(kord, k2, idx, idx2, (size_t)ncand, 0, 64, sc, s);
+  uint32_t* i1 = alt ? idx2 : idx;
+  uint32_t* i1b = alt ? idx : idx2;
+  hipLaunchKernelGGL(gather_u64_kernel, grid_of(ncand), dim3(256), 0, s, kkey, i1, ncand, k2);
+  alt = radix_sort_pairs<uint64_t>(k2, kkey, i1, i1b, (size_t)ncand, 0, 64, sc, s);
+  const uint32_t* fin = alt ? i1b : i1;
+  carry.reserve(ncand, w);
+  hipLaunchKernelGGL(gather_rows_kernel, grid_of(ncand), dim3(256), 0, s, rows, fin, ncand, w, carry.rows);
+  SM_HIP(hipStreamSynchronize(s));
+  carry.n = ncand;
+  sc.used = mark;
+}
+
+int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo& hi, FastState& fs, FastCarry& carry,
+                       uint32_t* pairs_out, int64_t pairs_cap, Scratch& sc, hipStream_t s, FastTimings* tm) {
+  const size_t mark = sc.used;
+  auto tmark = [&](const char* l) {
+    if (tm) tm->mark(l, s);
+  };
+  const int64_t n = p.n;
+  uint32_t* err = (uint32_t*)sc.take(16);
+  uint32_t* cand_n = err + 1;
+  uint32_t* stot = err + 2;
+  SM_HIP(hipMemsetAsync(err, 0, 16, s));
+  StackArgs sa{};
+  sa.rec = (const uint4*)p.rec;
+  sa.dbase = p.dbase;
+  sa.ntiles = (p.omax >> kTB) + 1;
+  sa.n = n;
+  sa.H = p.H;
+  sa.kmin = p.kmin;
+  sa.within = p.within;
+  sa.ts0 = p.ts0;
+  sa.exact_codes = p.exact_codes;
+  sa.vtype = p.vtype;
+  sa.vcol = p.vcol;
+  sa.ord = a.ordinals;
+  sa.obase = a.ordinal_base;
+  sa.o0 = p.o0;
+  sa.vattr = p.vattr;
+  sa.err = err;
+
+  // carry-out candidates: every partial still pending at the end (at most the batch's events + the carried ones)
+  int64_t nc = carry.n;
+  const int64_t cand_cap = std::min<int64_t>(n + nc, (int64_t)8 * p.H * kBins + nc) + 1024;
+  sa.cand = (int64_t*)sc.take((size_t)cand_cap * 32);
+  sa.cand_n = cand_n;
+  sa.cand_cap = (uint32_t)std::min<int64_t>(cand_cap, 0xffffffffll);
+  // carried partials of keys in this batch's key range
+  uint32_t* ccnt = nullptr;
+  if (nc > 0) {
+    const int64_t span = (int64_t)p.H << kRB;
+    uint4* cin = (uint4*)sc.take((size_t)nc * 16);
+    uint32_t* cst = (uint32_t*)sc.take((size_t)span * 4);
+    uint32_t* cen = (uint32_t*)sc.take((size_t)span * 4);
+    ccnt = (uint32_t*)sc.take(kBins * 4);
+    SM_HIP(hipMemsetAsync(cst, 0, (size_t)span * 4, s));
+    SM_HIP(hipMemsetAsync(cen, 0, (size_t)span * 4, s));
+    SM_HIP(hipMemsetAsync(ccnt, 0, kBins * 4, s));
+#define SM_CIN(VT)                                                                                                  \
+  hipLaunchKernelGGL((carry_in_kernel<VT>), grid_of(nc), dim3(256), 0, s, (const int64_t*)carry.rows, nc, carry.width, \
+                     p.vattr, p.vtype, p.vmode, p.vmin, p.kmin, span - 1, a.ordinal_base, p.o0, p.ts0, cin, cst, cen, ccnt,  \
+                     sa.cand, cand_n, err)
+    switch (p.vtype) {
+      case T_INT: SM_CIN(int32_t); break;
+      case T_LONG: SM_CIN(int64_t); break;
+      case T_FLOAT: SM_CIN(float); break;
+      default: SM_CIN(double); break;
+    }
+#undef SM_CIN
+    sa.cin = cin;
+    sa.cstart = cst;
+    sa.cend = cen;
+    sa.crow = (const int64_t*)carry.rows;
+    sa.cwidth = carry.width;
+  }
+  uint32_t* sbase = (uint32_t*)sc.take(kBins * 4);
+  hipLaunchKernelGGL(stage_base_kernel, dim3(1), dim3(kOB), 0, s, p.dbase, ccnt, sbase, stot);
+  uint32_t hs[3];
+  SM_HIP(hipMemcpyAsync(hs, err, 12, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  if (hs[0] & SE_ORD) {
+    sc.used = mark;
+    throw std::runtime_error("a carried partial lies more than 2^31 events before the batch's ordinal base (match "
+                             "tuples are 32-bit ordinals relative to it), or not before the batch");
+  }
+  const int64_t extra = hs[2];
+  sa.sbase = sbase;
+  sa.stage = (uint64_t*)sc.take((size_t)(n + extra) * 8);
+  sa.mstart = (uint32_t*)sc.take((size_t)kBins * (sa.ntiles + 1) * 4);
+  sa.mtot = (uint32_t*)sc.take(kBins * 4);
+  // resident workgroups (LDS bound: one per CU)
+  if (fs.cus == 0) {
+    int dev = 0;
+    SM_HIP(hipGetDevice(&dev));
+    SM_HIP(hipDeviceGetAttribute(&fs.cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int grid = std::min(kBins, fs.cus);
+  sa.spill = (uint4*)sc.take((size_t)grid * kKeys * kQ * 16);
+  static const bool want_stamps = getenv("SM_STACK_STAMPS") != nullptr;
+  static const int dbg = getenv("SM_STACK_DEBUG") ? atoi(getenv("SM_STACK_DEBUG")) : 0;
+  sa.dbg = dbg;
+  if (want_stamps) {
+    sa.stamps = (unsigned long long*)sc.take(128);
+    sa.counts = sa.stamps + 8;
+    SM_HIP(hipMemsetAsync(sa.stamps, 0, 128, s));
+  }
+  tmark("stack_prep");
+  switch (p.op * 2 + (p.fp ? 1 : 0)) {
+    case CMP_GT * 2: launch_stack_t<CMP_GT, false>(sa, grid, s); break;
+    case CMP_GT * 2 + 1: launch_stack_t<CMP_GT, true>(sa, grid, s); break;
+    case CMP_GE * 2: launch_stack_t<CMP_GE, false>(sa, grid, s); break;
+    case CMP_GE * 2 + 1: launch_stack_t<CMP_GE, true>(sa, grid, s); break;
+    case CMP_LT * 2: launch_stack_t<CMP_LT, false>(sa, grid, s); break;
+    case CMP_LT * 2 + 1: launch_stack_t<CMP_LT, true>(sa, grid, s); break;
+    case CMP_LE * 2: launch_stack_t<CMP_LE, false>(sa, grid, s); break;
+    case CMP_LE * 2 + 1: launch_stack_t<CMP_LE, true>(sa, grid, s); break;
+    default: sc.used = mark; return -1;
+  }
+  tmark("stack");
+  if (sa.stamps) {
+    unsigned long long hst[7], hcn[2];
+    SM_HIP(hipMemcpyAsync(hst, sa.stamps, sizeof(hst), hipMemcpyDeviceToHost, s));
+    SM_HIP(hipMemcpyAsync(hcn, sa.counts, sizeof(hcn), hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    double tot = 0;
+    for (double v : hst) tot += v;
+    fprintf(stderr, "[stack phases] setup %.3f rank %.3f place %.3f stacks %.3f scan %.3f writes %.3f tail %.3f\n",
+            hst[0] / tot, hst[1] / tot, hst[2] / tot, hst[3] / tot, hst[4] / tot, hst[5] / tot, hst[6] / tot);
+    fprintf(stderr, "[stack counts] events %llu pops %llu; wave-cycles %.3g\n", hcn[0], hcn[1], tot);
+  }
+  std::vector<uint32_t> mt(kBins);
+  SM_HIP(hipMemcpyAsync(mt.data(), sa.mtot, kBins * 4, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipMemcpyAsync(hs, err, 12, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  if (hs[0]) {
+    sc.used = mark;
+    return -1;
+  }
+  int64_t M = 0;
+  for (uint32_t v : mt) M += v;
+  if (M > pairs_cap) {
+    sc.used = mark;
+    throw std::runtime_error("match buffer too small");
+  }
+  OrderArgs oa{};
+  oa.stage = sa.stage;
+  oa.sbase = sbase;
+  oa.out = (uint64_t*)pairs_out;
+  if (M > 0) {
+    uint32_t* mt = (uint32_t*)sc.take((size_t)kBins * (sa.ntiles + 1) * 4);
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((sa.ntiles + 1 + 31) / 32), kBins / 32), dim3(256), 0, s,
+                       sa.mstart, sa.ntiles + 1, mt);
+    oa.mt = mt;
+    oa.ntiles = sa.ntiles;
+    hipLaunchKernelGGL(order_kernel, dim3((unsigned)((sa.ntiles + kGT - 1) / kGT)), dim3(kOB), 0, s, oa);
+  }
+  tmark("order");
+  // carry out (the stack kernel left each key's open partials as candidates)
+  const int64_t ncand = hs[1];
+  build_carry(sa.cand, ncand, a.st, hi.nattr, carry, sc, s);
+  tmark("carry_out");
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+  return M;
+}
+
+}  // namespace sm

@@ -13,6 +13,7 @@
 #include <charconv>
 #include <cmath>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -108,6 +109,19 @@ struct Callback {
   void* user = nullptr;
 };
 
+// One output chunk ready for the callbacks: the events one trigger (an input event or a scheduler firing) made
+// one query emit, delivered as one StreamCallback.receive(Event[]) (StreamCallback.java:65-76) and one
+// QueryCallback.receive(timestamp, in, removed) (QueryCallback.java:52-74). Prepared under the app lock with
+// owned copies of everything the events point at, so the callbacks can run after the lock is released.
+struct PreparedChunk {
+  int64_t ts = 0;
+  std::vector<Callback> cbs;      // stream callbacks of the output stream, then query callbacks of the query
+  size_t n_stream_cbs = 0;
+  std::vector<sm_event> evs;
+  std::vector<sm_value> vals;
+  std::deque<std::string> strs;   // stable addresses for STRING values
+};
+
 struct QueryRt {
   CompiledQuery cq;
   DBuf blob;
@@ -124,7 +138,10 @@ struct QueryRt {
   DBuf dev_pairs;
   int64_t dev_n = 0;
   FastState fast;            // v2 kernels' persistent look-back state
-  int fast_path_used = 0;    // 2 = onesweep form, 1 = general form (last device batch)
+  FastCarry carry;           // open partials carried across device batches (closed-form queries)
+  bool nfa_used = false;     // host-API batches ran through the NFA kernel (partials live in ks / heap)
+  int fast_path_used = 0;    // 3 = bucket stack, 2 = onesweep form, 1 = general form (last device batch)
+  ~QueryRt() { carry.release(); }
 };
 
 // v2 eligibility: c2 may read one attribute only (of e1 / e2 slots), c1 only e1, no timestamp reads.
@@ -167,6 +184,7 @@ struct sm_app {
   std::mutex mu;
   // device-batch fast path knobs (sm_app_set_option "fast_general" / "fast_timing") and the last timings
   bool force_general_fast = false;
+  int fast_stack = 0;  // option "fast_stack": 0 = automatic, 1 = always the bucket-stack kernels, 2 = never
   bool fast_timing = false;
   bool fast_tm_ready = false;
   sm::FastTimings fast_tm{};
@@ -177,6 +195,9 @@ struct sm_app {
   std::vector<sm::CompiledPartition> parts;
   std::vector<std::unique_ptr<sm_input>> inputs;
   std::map<std::string, std::vector<sm::Callback>> stream_cbs, query_cbs;
+  std::vector<sm::PreparedChunk> pending;  // outputs of the current call, delivered once the lock is released
+  bool failed = false;                      // a batch failed half-way: matching state is inconsistent
+  std::string failed_why;
   // batch staging
   std::vector<int32_t> ev_stream;
   std::vector<int64_t> ev_row, ev_ts, ev_clock, ev_ord;
@@ -228,6 +249,26 @@ int guarded(F&& f) {
     set_error(e.what());
     return status_of(e);
   }
+}
+
+void run_callbacks(std::vector<PreparedChunk>& chunks);
+
+// Entry points that can produce outputs: run f under the app lock, then the callbacks of what it produced
+// without it.
+template <typename F>
+int locked(sm_app* a, F&& f) {
+  std::vector<PreparedChunk> out;
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(a->mu);
+    rc = guarded([&] {
+      if (a->failed) throw std::runtime_error(a->failed_why);
+      f();
+    });
+    out.swap(a->pending);
+  }
+  run_callbacks(out);
+  return rc;
 }
 
 void ensure_scratch(sm_app* a, size_t bytes) {
@@ -366,62 +407,109 @@ void to_sm_values(const sm_app* a, const HostOut& h, const CompiledQuery& cq, st
   }
 }
 
+// Outputs in the reference's emission order (trigger position, timer phase, listener order, query order,
+// emission order), grouped into one chunk per (trigger, emitting query instance): the collect dump is appended
+// here, the callbacks run later (run_callbacks) outside the app lock.
 void deliver(sm_app* a, std::vector<HostOut>& outs) {
-  std::stable_sort(outs.begin(), outs.end(), [](const HostOut& x, const HostOut& y) {
-    if (x.r.pos != y.r.pos) return x.r.pos < y.r.pos;
-    if (x.r.phase != y.r.phase) return x.r.phase < y.r.phase;
-    if (x.r.phase == 0) {
-      if (x.r.time != y.r.time) return x.r.time < y.r.time;
-      int gx = x.r.create >= 0, gy = y.r.create >= 0;  // non-partitioned listeners registered first
+  auto key_less = [](const OutRec& x, const OutRec& y) {
+    if (x.pos != y.pos) return x.pos < y.pos;
+    if (x.phase != y.phase) return x.phase < y.phase;
+    if (x.phase == 0) {
+      if (x.time != y.time) return x.time < y.time;
+      int gx = x.create >= 0, gy = y.create >= 0;  // non-partitioned listeners registered first
       if (gx != gy) return gx < gy;
-      if (x.r.create != y.r.create) return x.r.create < y.r.create;
-      if (x.r.query != y.r.query) return x.r.query < y.r.query;
-      if (x.r.sched != y.r.sched) return x.r.sched < y.r.sched;
-      return x.r.seq < y.r.seq;
+      if (x.create != y.create) return x.create < y.create;
+      if (x.query != y.query) return x.query < y.query;
+      return x.sched < y.sched;
     }
-    if (x.r.query != y.r.query) return x.r.query < y.r.query;
+    return x.query < y.query;
+  };
+  std::stable_sort(outs.begin(), outs.end(), [&](const HostOut& x, const HostOut& y) {
+    if (key_less(x.r, y.r)) return true;
+    if (key_less(y.r, x.r)) return false;
     return x.r.seq < y.r.seq;
   });
-  std::vector<sm_value> vals;
-  for (auto& h : outs) {
-    const CompiledQuery& cq = a->queries[h.qidx]->cq;
-    to_sm_values(a, h, cq, vals);
-    sm_event ev{h.r.ts, vals.data(), (int32_t)vals.size()};
-    if (a->collect) {
-      std::ostringstream o;
-      o << "[" << h.r.ts << ",[";
-      for (size_t k = 0; k < h.vals.size(); ++k) {
-        if (k) o << ",";
-        json_val(o, a, h.vals[k], cq.sel_types[k]);
-      }
-      o << "],[";
-      for (size_t k = 0; k < h.refs.size(); ++k) {
-        if (k) o << ",";
-        o << h.refs[k];
-      }
-      o << "]]";
-      std::string ev_json = o.str();
-      a->collected_streams[cq.insert_into].push_back(ev_json);
-      if (cq.partition < 0) {
-        std::ostringstream q;
-        q << "[" << h.r.ts << ",[[";
-        for (size_t k = 0; k < h.vals.size(); ++k) {
-          if (k) q << ",";
-          json_val(q, a, h.vals[k], cq.sel_types[k]);
-        }
-        q << "]]]";
-        a->collected_queries[cq.name].push_back(q.str());
-      }
-    }
+  size_t i = 0;
+  while (i < outs.size()) {
+    size_t j = i + 1;  // the chunk: same trigger and emitting query instance
+    while (j < outs.size() && outs[j].qidx == outs[i].qidx && !key_less(outs[i].r, outs[j].r) &&
+           !key_less(outs[j].r, outs[i].r))
+      ++j;
+    const CompiledQuery& cq = a->queries[outs[i].qidx]->cq;
+    PreparedChunk ch;
+    ch.ts = outs[j - 1].r.ts;  // QueryCallback.receiveStreamEvent: the chunk's last event's timestamp
     auto it = a->stream_cbs.find(cq.insert_into);
     if (it != a->stream_cbs.end())
       for (auto& cb : it->second)
-        if (cb.scb) cb.scb(cb.user, &ev, 1);
+        if (cb.scb) ch.cbs.push_back(cb);
+    ch.n_stream_cbs = ch.cbs.size();
     if (cq.partition < 0) {  // partition clones do not inherit QueryCallbacks (PartitionRuntime)
       auto qt = a->query_cbs.find(cq.name);
       if (qt != a->query_cbs.end())
         for (auto& cb : qt->second)
-          if (cb.qcb) cb.qcb(cb.user, h.r.ts, &ev, 1, nullptr, 0);
+          if (cb.qcb) ch.cbs.push_back(cb);
+    }
+    const size_t nsel = cq.sel_types.size();
+    if (!ch.cbs.empty()) {
+      ch.vals.reserve((j - i) * nsel);
+      ch.evs.reserve(j - i);
+    }
+    for (size_t k = i; k < j; ++k) {
+      HostOut& h = outs[k];
+      if (a->collect) {
+        std::ostringstream o;
+        o << "[" << h.r.ts << ",[";
+        for (size_t q = 0; q < h.vals.size(); ++q) {
+          if (q) o << ",";
+          json_val(o, a, h.vals[q], cq.sel_types[q]);
+        }
+        o << "],[";
+        for (size_t q = 0; q < h.refs.size(); ++q) {
+          if (q) o << ",";
+          o << h.refs[q];
+        }
+        o << "]]";
+        a->collected_streams[cq.insert_into].push_back(o.str());
+        if (cq.partition < 0) {
+          std::ostringstream qo;
+          qo << "[" << h.r.ts << ",[[";
+          for (size_t q = 0; q < h.vals.size(); ++q) {
+            if (q) qo << ",";
+            json_val(qo, a, h.vals[q], cq.sel_types[q]);
+          }
+          qo << "]]]";
+          a->collected_queries[cq.name].push_back(qo.str());
+        }
+      }
+      if (ch.cbs.empty()) continue;
+      std::vector<sm_value> vals;
+      to_sm_values(a, h, cq, vals);
+      for (auto& v : vals)
+        if (v.type == T_STRING && !v.is_null) {
+          ch.strs.emplace_back(v.s);
+          v.s = ch.strs.back().c_str();
+        }
+      ch.vals.insert(ch.vals.end(), vals.begin(), vals.end());
+    }
+    if (!ch.cbs.empty()) {
+      for (size_t k = i; k < j; ++k)
+        ch.evs.push_back(sm_event{outs[k].r.ts, ch.vals.data() + (k - i) * nsel, (int32_t)nsel});
+      a->pending.push_back(std::move(ch));
+    }
+    i = j;
+  }
+}
+
+// Callbacks of the prepared chunks, on the calling thread, with the app lock released: a callback may send into
+// the same app (its outputs are delivered inside that send, as in the reference). Reference behaviour for a
+// callback that throws (caught and logged, StreamCallback.java:92-99) is the binding's business: C callbacks
+// cannot throw across the ABI.
+void run_callbacks(std::vector<PreparedChunk>& chunks) {
+  for (auto& ch : chunks) {
+    for (size_t c = 0; c < ch.cbs.size(); ++c) {
+      const Callback& cb = ch.cbs[c];
+      if (c < ch.n_stream_cbs) cb.scb(cb.user, ch.evs.data(), ch.evs.size());
+      else cb.qcb(cb.user, ch.ts, ch.evs.data(), ch.evs.size(), nullptr, 0);
     }
   }
 }
@@ -636,6 +724,28 @@ void flush(sm_app* a) {
                     (const int64_t*)a->d_ev_clock.p, (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p,
                     (const int64_t*)a->d_adv_pos.p, (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p,
                     (const int64_t*)a->d_adv_upto.p, (int64_t)a->adv_pos.size(), a->clock_batch_in};
+  // the batch is consumed whatever happens below: a query that fails half-way leaves the matching state
+  // inconsistent (earlier queries advanced, outputs lost), so the app refuses further events until it is restored
+  // or reset, instead of running the same events again
+  struct BatchDone {
+    sm_app* a;
+    int64_t N;
+    bool ok = false;
+    ~BatchDone() {
+      a->ordinal_base += N;
+      a->clock_batch_in = a->clock;
+      a->ev_stream.clear();
+      a->ev_row.clear();
+      a->ev_ts.clear();
+      a->ev_clock.clear();
+      a->ev_ord.clear();
+      a->adv_pos.clear();
+      a->adv_clock.clear();
+      a->adv_wall.clear();
+      for (auto& st : a->streams) st.clear();
+    }
+  } done{a, N};
+  try {
   for (size_t qi = 0; qi < a->queries.size(); ++qi) {
     QueryRt& q = *a->queries[qi];
     const DQuery& h = q.cq.hdr;
@@ -657,19 +767,15 @@ void flush(sm_app* a) {
       continue;
     }
     run_pattern_query(a, (int)qi, ev, N, outs, a->stream);
+    for (int s : q.cq.streams)
+      if (a->streams[s].rows > 0) q.nfa_used = true;
   }
-  // ---- batch done
-  a->ordinal_base += N;
-  a->clock_batch_in = a->clock;
-  a->ev_stream.clear();
-  a->ev_row.clear();
-  a->ev_ts.clear();
-  a->ev_clock.clear();
-  a->ev_ord.clear();
-  a->adv_pos.clear();
-  a->adv_clock.clear();
-  a->adv_wall.clear();
-  for (auto& st : a->streams) st.clear();
+  } catch (const std::exception& e) {
+    a->failed = true;
+    a->failed_why = std::string("a batch failed half-way (") + e.what() +
+                    "); the matching state is inconsistent: restore a snapshot or reset the app";
+    throw;
+  }
   deliver(a, outs);
 }
 
@@ -689,6 +795,16 @@ void stage_record(sm_app* a, int32_t stream, int64_t row, int64_t ts, int wall) 
     }
   }
   a->ev_clock.push_back(a->clock);
+}
+
+// Partials of a closed-form query fed by device batches live in its carried state, which the host-API (NFA)
+// path does not read: host events for a stream such a query reads are refused instead of silently losing the
+// matches that span the two paths.
+void check_host_stream(sm_app* a, int stream) {
+  for (auto& q : a->queries)
+    if (q->carry.active && std::find(q->cq.streams.begin(), q->cq.streams.end(), stream) != q->cq.streams.end())
+      throw sql::UnsupportedError("query '" + q->cq.name + "' holds partial matches from device batches; send its "
+                                  "stream's events through sm_app_process_device_batch (or reset the app)");
 }
 
 void maybe_autoflush(sm_app* a) {
@@ -819,8 +935,7 @@ void sm_app_destroy(sm_app* a) {
 }
 
 int sm_app_start(sm_app* a) {
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     if (a->started) return;
     a->started = true;
     // absent start-state processors of non-partitioned queries schedule their first timer at start()
@@ -829,13 +944,11 @@ int sm_app_start(sm_app* a) {
 }
 
 int sm_app_flush(sm_app* a) {
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] { flush(a); });
+  return locked(a, [&] { flush(a); });
 }
 
 int sm_app_shutdown(sm_app* a) {
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     if (a->shut) return;
     flush(a);
     a->shut = true;
@@ -857,11 +970,15 @@ int sm_app_input_handler(sm_app* a, const char* stream_id, sm_input** out) {
 
 int sm_input_send(sm_input* in, int64_t ts, const sm_value* row, size_t n) {
   sm_app* a = in->app;
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     StreamStage& st = a->streams[in->stream];
     if (n != st.def->attrs.size()) throw TypeError("row has " + std::to_string(n) + " values, stream '" + st.def->id +
                                                    "' has " + std::to_string(st.def->attrs.size()) + " attributes");
+    // the whole row is checked before any column grows (a rejected row leaves the staged columns aligned)
+    for (size_t k = 0; k < n; ++k)
+      if (!row[k].is_null && row[k].type != (int)st.def->attrs[k].type)
+        throw TypeError("value type does not match attribute '" + st.def->attrs[k].name + "'");
+    check_host_stream(a, in->stream);
     for (size_t k = 0; k < n; ++k) put_value(st, (int)k, row[k], a);
     st.row_pos.push_back((int64_t)a->ev_stream.size());
     stage_record(a, in->stream, st.rows, ts, 0);
@@ -873,10 +990,10 @@ int sm_input_send(sm_input* in, int64_t ts, const sm_value* row, size_t n) {
 int sm_input_send_columns(sm_input* in, size_t n, const int64_t* ts, const void* const* cols,
                           const uint8_t* const* null_flags) {
   sm_app* a = in->app;
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     StreamStage& st = a->streams[in->stream];
     size_t na = st.def->attrs.size();
+    check_host_stream(a, in->stream);
     for (size_t i = 0; i < n; ++i) {
       for (size_t k = 0; k < na; ++k) {
         sm_value v{};
@@ -913,16 +1030,14 @@ int sm_app_stream_schema(sm_app* a, const char* stream_id, int32_t* types, size_
 }
 
 int sm_app_advance_time(sm_app* a, int64_t ts) {
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     if (!a->ast.playback) return;
     stage_record(a, NFA_TICK, -1, ts, 0);
   });
 }
 
 int sm_app_advance_wallclock(sm_app* a, int64_t ts) {
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     if (!a->ast.playback) return;
     stage_record(a, NFA_WALL, -1, ts, 1);
   });
@@ -978,6 +1093,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       a->heap_half = (int32_t)std::max<int64_t>(256, value);
     } else if (k == "fast_general") {
       a->force_general_fast = value != 0;
+    } else if (k == "fast_stack") {
+      a->fast_stack = (int)std::min<int64_t>(std::max<int64_t>(value, 0), 2);
     } else if (k == "fast_timing") {
       if (value && !a->fast_tm_ready) {
         for (auto& e : a->fast_tm.ev) SM_HIP(hipEventCreate(&e));
@@ -1004,11 +1121,15 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
         q->keys.nslots = 0;
         if (q->state_slots) SM_HIP(hipMemsetAsync(q->ks.p, 0, (size_t)q->state_slots * q->cq.hdr.ks_words * 8, a->stream));
         q->dev_n = 0;
+        q->carry.reset();
       }
       SM_HIP(hipStreamSynchronize(a->stream));
       a->clock = a->clock_batch_in = 0;
       a->next_ordinal = a->ordinal_base = 0;
       a->started = false;
+      a->failed = false;
+      a->failed_why.clear();
+      for (auto& q : a->queries) q->nfa_used = false;
       if (value) {  // reset and start again
         a->started = true;
         stage_record(a, NFA_START, -1, a->clock, 0);
@@ -1026,10 +1147,15 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
 int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, const int64_t* d_ts,
                                 const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
                                 void* hip_stream) {
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     int s = stream_index(a->ast, stream_id ? stream_id : "");
     if (s < 0) throw sql::ValidationError("unknown stream");
+    flush(a);  // staged host events come first (arrival order)
+    for (auto& qp : a->queries)
+      if (qp->cq.hdr.kind != 0 && qp->nfa_used &&
+          std::find(qp->cq.streams.begin(), qp->cq.streams.end(), s) != qp->cq.streams.end())
+        throw sql::UnsupportedError("query '" + qp->cq.name + "' holds partial matches from host-API events; device "
+                                    "batches of its streams need a fresh (or reset) app");
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
     StreamStage& st = a->streams[s];
     NfaStream d;
@@ -1045,7 +1171,12 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
     for (auto& qp : a->queries) {
       const CompiledQuery& cq = qp->cq;
       if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
-      need = std::max(need, cq.hdr.kind == 0 ? n / 8 + n / 1024 + (64 << 20) : n * 64 + (64 << 20));
+      // patterns: records / staging / pairs (64 B per event), carry-out candidates (32 B each) and the carried
+      // partials' working arrays, plus the bucket-stack spill rings and bounded buffers
+      const size_t nc = (size_t)qp->carry.n, wc = (size_t)std::max(qp->carry.width, 4);
+      need = std::max(need, cq.hdr.kind == 0 ? n / 8 + n / 1024 + (64 << 20)
+                                             : n * 64 + std::min<size_t>(n + nc, (size_t)1 << 26) * 32 +
+                                                   nc * (160 + 8 * wc) + ((size_t)640 << 20));
     }
     ensure_scratch(a, need);
     for (auto& qp : a->queries) {
@@ -1088,7 +1219,7 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
       fa.within = cq.fast_within;
       fa.ordinals = d_ordinals;
       fa.ordinal_base = ordinal_base;
-      q.dev_pairs.ensure(std::max<size_t>(n * 8, 16));
+      q.dev_pairs.ensure(std::max<size_t>((n + (size_t)q.carry.n) * 8, 16));
       std::vector<int32_t> types(d.types, d.types + d.nattr);
       FastHostInfo hi;
       hi.cols = d_cols;
@@ -1099,6 +1230,7 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
       hi.c1_host = (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.fast_c1_off;
       hi.c1_len = cq.fast_c1_len;
       if (hi.vattr >= 0) hi.vtype = types[hi.vattr];
+      hi.nattr = d.nattr;
       if (fa.key) {
         const CompiledPartition& cp = *q.part;
         int idx = (int)(std::find(cp.streams.begin(), cp.streams.end(), s) - cp.streams.begin());
@@ -1108,11 +1240,17 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
           hi.key_type = types[hi.key_col];
         }
       }
-      int64_t m = -1;
-      if (!a->force_general_fast) m = fast_every_within_v2(fa, hi, q.fast, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs,
-                                                           a->fast_timing ? &a->fast_tm : nullptr);
-      q.fast_path_used = 2;
+      int64_t m = FAST_OUTSIDE;
+      if (!a->force_general_fast)
+        m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
+                                 a->fast_timing ? &a->fast_tm : nullptr, a->fast_stack);
+      q.fast_path_used = q.fast.last_path;
+      if (m == FAST_NON_MONOTONE)
+        throw std::runtime_error("query '" + cq.name + "': event time decreases in a device batch");
       if (m < 0) {
+        if (q.carry.n > 0)
+          throw sql::UnsupportedError("query '" + cq.name + "': partial matches carried from an earlier device batch "
+                                      "need the closed-form kernels");
         m = fast_every_within(fa, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs, a->fast_timing ? &a->fast_tm : nullptr);
         q.fast_path_used = 1;
       }
@@ -1128,8 +1266,7 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
 int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_idx, const int64_t* d_ts,
                                  const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
                                  void* hip_stream) {
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     flush(a);
     if (n == 0) return;
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
@@ -1211,8 +1348,7 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
 // are flushed first, so the snapshot is taken at a batch boundary.
 
 int sm_app_snapshot(sm_app* a, uint8_t* buf, size_t cap, size_t* len) {
-  std::lock_guard<std::mutex> g(a->mu);
-  return guarded([&] {
+  return locked(a, [&] {
     flush(a);
     SnapWriter w;
     w.raw(kSnapMagic, 8);
@@ -1278,6 +1414,9 @@ int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
     a->adv_clock.clear();
     a->adv_wall.clear();
     for (auto& st : a->streams) st.clear();
+    a->failed = false;
+    a->failed_why.clear();
+    for (auto& q : a->queries) q->carry.reset();
     a->clock = r.get<int64_t>();
     a->clock_batch_in = r.get<int64_t>();
     a->next_ordinal = r.get<int64_t>();
