@@ -16,6 +16,7 @@
  *   sm_app_snapshot / sm_app_restore  SiddhiAppRuntime.snapshot() / restore(byte[])  :548 / :560
  *   sm_partition_by_owner           multi-GPU form of PartitionStreamReceiver.receive (partition/
  *                                   PartitionStreamReceiver.java:156): route each event to its key's owner rank
+ *   sm_compile_dump                 SiddhiCompiler.parse (siddhi-query-compiler .../SiddhiCompiler.java:56)
  *   sm_app_process_device_events    a sequence of InputHandler.send calls over several streams of one
  *                                   schema (InputHandler.java:53 → StreamJunction.sendData :232), device-resident
  *
@@ -75,6 +76,9 @@ int sm_manager_create(sm_manager** out);
 void sm_manager_destroy(sm_manager* m);
 
 int sm_app_create(sm_manager* m, const char* siddhiql, sm_app** out);
+/* Parse only (no device needed): the app's query tree as canonical JSON (shapes in siddhiql/dump.cpp) into buf,
+ * NUL-terminated when it fits in cap; *len = its length. Errors as sm_app_create reports them for the same text. */
+int sm_compile_dump(const char* siddhiql, char* buf, size_t cap, size_t* len);
 void sm_app_destroy(sm_app* app);
 int sm_app_start(sm_app* app);
 int sm_app_flush(sm_app* app);

@@ -186,6 +186,16 @@ class SiddhiAppRuntime:
             pass
 
 
+def compile_dump(siddhi_app):
+    """SiddhiCompiler.parse: the app's query tree (dict), without a device. Raises the reference's exceptions."""
+    import json
+    n = ctypes.c_size_t()
+    check(lib().sm_compile_dump(siddhi_app.encode(), None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value + 1)
+    check(lib().sm_compile_dump(siddhi_app.encode(), buf, n.value + 1, ctypes.byref(n)))
+    return json.loads(buf.value.decode())
+
+
 class SiddhiManager:
     def __init__(self):
         h = ctypes.c_void_p()

@@ -927,6 +927,17 @@ int sm_app_create(sm_manager* m, const char* siddhiql, sm_app** out) {
   return rc;
 }
 
+int sm_compile_dump(const char* siddhiql, char* buf, size_t cap, size_t* len) {
+  return guarded([&] {
+    const std::string j = sql::dump_app_json(sql::parse_app(siddhiql ? siddhiql : ""));
+    *len = j.size();
+    if (buf && cap > j.size()) {
+      memcpy(buf, j.data(), j.size());
+      buf[j.size()] = 0;
+    }
+  });
+}
+
 void sm_app_destroy(sm_app* a) {
   if (!a) return;
   for (auto& q : a->queries) q->keys.release();

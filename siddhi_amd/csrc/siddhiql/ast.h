@@ -155,6 +155,9 @@ struct App {
 // Parses SiddhiQL text; throws ParseError / ValidationError / UnsupportedError.
 App parse_app(const std::string& text);
 
+// Canonical JSON of a parsed app (siddhiql/dump.cpp; shapes documented there).
+std::string dump_app_json(const App& a);
+
 // Utility: all stream ids referenced in a state tree in StateInputStream.collectStreamIds order
 // (StateInputStream.java:70-88; absent elements are StreamStateElements and are included).
 void collect_stream_ids(const StateElem* e, std::vector<std::string>& out);

@@ -569,9 +569,25 @@ struct Parser {
     maybe_within(*s);
     return s;
   }
+  // an element that is only `[every] not S for t` (chains of them included)
+  static bool all_absent(const StateElem* e) {
+    switch (e->kind) {
+      case StateKind::ABSENT: return true;
+      case StateKind::EVERY: return all_absent(e->a.get());
+      case StateKind::NEXT: return all_absent(e->a.get()) && all_absent(e->b.get());
+      default: return false;
+    }
+  }
   StateP pattern_chain() {
     StateP l = pattern_unit();
-    while (accept_sym("->")) l = mk_next(std::move(l), pattern_unit());
+    int n = 1;
+    while (accept_sym("->")) {
+      l = mk_next(std::move(l), pattern_unit());
+      ++n;
+    }
+    // left/right_absent_pattern_source (SiddhiQL.g4:224-238): a chain of absent elements needs a present one
+    // (compiler AbsentPatternTestCase.java:56-61, `not A for t -> not B for t` is a SiddhiParserException)
+    if (n > 1 && all_absent(l.get())) fail("an absent pattern chain needs at least one present (non-absent) element");
     return l;
   }
   // sequence_source_chain (SiddhiQL.g4:320-324)
@@ -659,6 +675,8 @@ struct Parser {
       q.state = pattern_chain();
     } else {
       q.state = sequence_top();
+      // left/right_absent_sequence_source (SiddhiQL.g4:312-326): absent elements need a present one
+      if (all_absent(q.state.get())) fail("an absent sequence needs at least one present (non-absent) element");
     }
     // query_section: select ... (group by / having / order by / limit are out of scope)
     if (accept_kw("select")) {

@@ -239,28 +239,39 @@ def extract(path, name, ann, body, line):
     for m in re.finditer(r"addCallback\(.*?\n\s*\}\);", body, re.S):
         main = main.replace(m.group(0), "")
     events, ts = [], BASE_TS
-    for m in re.finditer(r"(\w+)\.send\((.*?)\);\s*$|Thread\.sleep\((\d+)\)|siddhiAppRuntime\.start\(\)|"
+    # local event-time variables: `long t = System.currentTimeMillis();` then `t += 1000;` (explicit timestamps
+    # relative to the run's base time, e.g. EveryAbsentPatternTestCase.testQueryAbsent3's playback clock)
+    tvars = {}
+    for m in re.finditer(r"long\s+(\w+)\s*=\s*System\.currentTimeMillis\(\)\s*;|(\w+)\s*\+=\s*(\d+)L?\s*;|"
+                         r"(\w+)\.send\((.*?)\);\s*$|Thread\.sleep\((\d+)\)|siddhiAppRuntime\.start\(\)|"
                          r"waitForEvents\(\s*(\d+)\s*,\s*(\d+)\s*,\s*(\w+)\s*,\s*(\d+)\s*\)|"
                          r"assertEquals\((?:\"[^\"]*\",\s*)?(\d+),\s*(\w+)(\.get\(\)|\.getInEventCount\(\))?\)|"
                          r"siddhiAppRuntime\.shutdown\(\)",
                          main, re.S | re.M):
         if m.group(0).startswith("siddhiAppRuntime.shutdown"):
             break
-        if m.group(8):
-            name = m.group(9) + (".in" if m.group(10) == ".getInEventCount()" else "")
-            events.append(["__assert__", name, int(m.group(8))])
+        if m.group(1):
+            tvars[m.group(1)] = BASE_TS
             continue
-        if m.group(3):
-            ts += int(m.group(3))
-            events.append(["__sleep__", int(m.group(3))])
+        if m.group(2):
+            if m.group(2) in tvars:
+                tvars[m.group(2)] += int(m.group(3))
             continue
-        if m.group(4):
-            events.append(["__wait__", int(m.group(4)), int(m.group(5)), m.group(6), int(m.group(7))])
+        if m.group(11):
+            name = m.group(12) + (".in" if m.group(13) == ".getInEventCount()" else "")
+            events.append(["__assert__", name, int(m.group(11))])
+            continue
+        if m.group(6):
+            ts += int(m.group(6))
+            events.append(["__sleep__", int(m.group(6))])
+            continue
+        if m.group(7):
+            events.append(["__wait__", int(m.group(7)), int(m.group(8)), m.group(9), int(m.group(10))])
             continue
         if m.group(0).startswith("siddhiAppRuntime.start"):
             events.append(["__start__"])
             continue
-        h, args = m.group(1), m.group(2).strip()
+        h, args = m.group(4), m.group(5).strip()
         if h not in handlers:
             kat["skip"] = "send on unknown handler " + h
             return kat
@@ -272,6 +283,10 @@ def extract(path, name, ann, body, line):
             am = re.fullmatch(r"(\d+)L?\s*,\s*new\s+Object\[\]\s*\{(.*)\}", args, re.S)
             if am:
                 events.append([handlers[h], int(am.group(1)), [parse_value(x) for x in split_args(am.group(2))]])
+                continue
+            am = re.fullmatch(r"(\w+)\s*,\s*new\s+Object\[\]\s*\{(.*)\}", args, re.S)
+            if am and am.group(1) in tvars:
+                events.append([handlers[h], tvars[am.group(1)], [parse_value(x) for x in split_args(am.group(2))]])
                 continue
             am = re.fullmatch(r"new Event\((\d+)L?\s*,\s*new\s+Object\[\]\s*\{(.*)\}\)", args, re.S)
             if am:
