@@ -347,7 +347,7 @@ def main():
     import torch
     import torch.distributed as dist
     from siddhi_amd.testing import ProductApp
-    from siddhi_amd.shard import exchange_with_ordinals
+    from siddhi_amd.shard import concat_ordered, exchange_with_ordinals, return_matches, slice_starts
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -371,6 +371,12 @@ def main():
     ordinals = torch.arange(lo, hi, dtype=torch.int64, device=dev) if args.config in (4, 5) else None
     sidx = gen_stream_idx(lo, hi, dev, seed) if args.config == 5 else None
     ticks = clock_ticks(ts, lo, world) if args.config == 5 and world > 1 else None
+    # multi-GPU constants of the exchange, made once: every slice's first ordinal, the in-slice offsets shipped in
+    # the packed records, and the device buffer the per-rank match tuples are copied into for the return exchange
+    starts = slice_starts(lo, world, dev) if world > 1 and cfg["shards"] else None
+    offsets = torch.arange(hi - lo, dtype=torch.int32, device=dev) if world > 1 and cfg["shards"] else None
+    mbuf = [None]
+    out_local = [0]
     torch.cuda.synchronize()
 
     app = ProductApp(cfg["app"], fast_stack=args.stack)
@@ -383,8 +389,8 @@ def main():
             # a fresh runtime of the app per step (state dropped, device allocations kept), then the batch
             app.set_option("reset", 1)
             if world > 1:
-                (s_sym, s_price, s_ts, s_sid), s_ord, _ = exchange_with_ordinals(symbol, [symbol, price, ts, sidx],
-                                                                                 world, lo)
+                (s_sym, s_price, s_ts, s_sid), s_ord, _ = exchange_with_ordinals(
+                    symbol, [symbol, price, ts, sidx], world, lo, starts=starts, offsets=offsets)
                 s_sid, s_ts, (s_sym, s_price), s_ord = merge_ticks(s_sid, s_ts, [s_sym, s_price], s_ord, ticks)
             else:
                 s_sym, s_price, s_ts, s_ord, s_sid = symbol, price, ts, ordinals, sidx
@@ -396,7 +402,8 @@ def main():
         # a fresh runtime of the app per step: the query's open partials (carried across device batches) dropped
         app.set_option("reset", 0)
         if args.config == 4 and world > 1:
-            (s_sym, s_price, s_ts), s_ord, _ = exchange_with_ordinals(symbol, [symbol, price, ts], world, lo)
+            (s_sym, s_price, s_ts), s_ord, _ = exchange_with_ordinals(symbol, [symbol, price, ts], world, lo,
+                                                                      starts=starts, offsets=offsets)
         elif args.config == 4:
             s_sym, s_price, s_ts, s_ord = symbol, price, ts, None
         else:
@@ -406,7 +413,20 @@ def main():
         cols = [s_sym, s_price, volume if args.config == 2 else s_price, tsattr if args.config == 2 else s_price]
         app.process_device_batch("StockStream", s_ts, cols, ordinals=s_ord, ordinal_base=lo if args.config == 2 else 0,
                                  hip_stream=hip_stream)
-        return app.device_matches("q")[1]
+        m = app.device_matches("q")[1]
+        if world > 1 and cfg["shards"]:
+            # the reference's single output order across ranks (shard.py): config 4 returns every tuple to the
+            # rank that ingested its e2 and orders it there; config 2's index-range outputs are concatenated
+            elem = torch.int32 if args.config == 2 else torch.int64
+            if mbuf[0] is None or mbuf[0].numel() < m:
+                mbuf[0] = torch.empty(max(m, 1) + (m >> 3), dtype=elem, device=dev)
+            app.copy_device_matches("q", mbuf[0])
+            mine = mbuf[0][:m]
+            if args.config == 2:
+                out_local[0] = concat_ordered(mine.to(torch.int64) + lo, world).numel()
+            else:
+                out_local[0] = return_matches(mine, starts, N, world).numel()
+        return m
 
     log(f"rank {rank}: config {args.config}, {hi - lo} events resident; warmup {args.warmup}")
     for _ in range(args.warmup):

@@ -16,6 +16,10 @@
  *   sm_app_snapshot / sm_app_restore  SiddhiAppRuntime.snapshot() / restore(byte[])  :548 / :560
  *   sm_partition_by_owner           multi-GPU form of PartitionStreamReceiver.receive (partition/
  *                                   PartitionStreamReceiver.java:156): route each event to its key's owner rank
+ *   sm_order_matches                multi-GPU merge of the per-rank outputs back into the single output order a
+ *                                   query callback sees (QueryCallback.receive, query/output/callback/
+ *                                   QueryCallback.java:51): no Java counterpart, one JVM has one output queue
+ *   sm_app_copy_device_matches      the device tuples of the last batch into a caller buffer (for collectives)
  *   sm_compile_dump                 SiddhiCompiler.parse (siddhi-query-compiler .../SiddhiCompiler.java:56)
  *   sm_app_process_device_events    a sequence of InputHandler.send calls over several streams of one
  *                                   schema (InputHandler.java:53 → StreamJunction.sendData :232), device-resident
@@ -138,16 +142,29 @@ int sm_app_process_device_events(sm_app* app, size_t n, const int32_t* d_stream_
  * events are discarded. */
 int sm_app_snapshot(sm_app* app, uint8_t* buf, size_t cap, size_t* len);
 int sm_app_restore(sm_app* app, const uint8_t* buf, size_t len);
-/* Stable partition of a device batch by owner rank = key mod world (keys: 4- or 8-byte integers, world <= 64):
- * column c (widths[c] bytes per element: 1, 2, 4 or 8) is copied from d_src[c] to d_dst[c] grouped by owner,
- * arrival order kept within each owner; counts[o] = events for owner o (host array of world entries). The
- * send side of the key exchange before the RCCL all-to-all-v. */
+/* Stable partition of a device batch by owner rank (keys: 1/2/4/8-byte integers, world <= 64). The owner of key
+ * k is (hi32(splitmix64_finalizer((uint64_t)(int64_t)k))) mod world, hash-by-key so that structured keys spread.
+ * Column c (widths[c] bytes per element: 1, 2, 4 or 8) is copied from d_src[c] to d_dst[c] grouped by owner,
+ * arrival order kept within each owner; element i of the output lands at d_dst[c] + i * strides[c] (strides
+ * NULL = widths: plain columns; a record size: several columns packed into one record buffer, each field aligned
+ * to its width); counts[o] = events for owner o (host array of world entries). The send side of the key
+ * exchange before the RCCL all-to-all-v (one packed record per event, siddhi_amd/shard.py). */
 int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t world, int ncols,
-                          const int32_t* widths, const void* const* d_src, void* const* d_dst, uint64_t* counts,
-                          void* hip_stream);
+                          const int32_t* widths, const int32_t* strides, const void* const* d_src,
+                          void* const* d_dst, uint64_t* counts, void* hip_stream);
+/* Receive side of the multi-GPU match return: n match pairs (e2 << 32) | uint32(e1) of global ordinals, every e2
+ * in [lo, hi) (this rank's ingest slice), given as the concatenation of per-source runs each in reference order
+ * (e2, then e1; one e2's matches all in one run) → d_out (n entries, not aliasing d_pairs) in the reference's
+ * global output order for that slice. Concatenating the ranks' outputs in rank order gives the single-process
+ * output order. */
+int sm_order_matches(const uint64_t* d_pairs, size_t n, int64_t lo, int64_t hi, uint64_t* d_out, void* hip_stream);
 /* Match tuples of the last device batch for a query: n pairs (e1, e2) of ordinals relative to the batch's
  * ordinal_base, uint32[2*n] in device memory, in reference output order (e2 ordinal, then e1 ordinal). */
 int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** d_pairs, size_t* n);
+/* The same tuples (or a filter query's kept rows, uint32 each) copied into a caller-owned device buffer of
+ * cap_bytes on hip_stream (asynchronous); *n = tuples. Lets a caller hand them to its own collectives. */
+int sm_app_copy_device_matches(sm_app* app, const char* query_name, void* d_dst, size_t cap_bytes, size_t* n,
+                               void* hip_stream);
 /* Diagnostics of the last device batch: "fast_path:<query>" (2 = onesweep kernels, 1 = general kernels),
  * "fast_ms:group" / "fast_ms:walk" / "fast_ms:order" (phase times in ms; needs the "fast_timing" option). */
 int sm_app_get_stat(sm_app* app, const char* key, double* out);

@@ -20,7 +20,7 @@ EXPORTS = [
     "sm_input_send_columns", "sm_app_stream_schema", "sm_app_advance_time", "sm_app_advance_wallclock",
     "sm_app_add_stream_callback", "sm_app_add_query_callback", "sm_app_set_collect", "sm_app_dump_outputs",
     "sm_app_set_option", "sm_app_process_device_batch", "sm_app_process_device_events", "sm_app_device_matches",
-    "sm_app_snapshot", "sm_app_restore", "sm_partition_by_owner",
+    "sm_app_snapshot", "sm_app_restore", "sm_partition_by_owner", "sm_order_matches", "sm_app_copy_device_matches",
     "sm_app_get_stat", "sm_compile_dump",
 ]
 
@@ -71,8 +71,10 @@ def lib():
         L.sm_app_process_device_batch.argtypes = [vp, cp, sz, vp, ctypes.POINTER(vp), vp, i64, vp]
         L.sm_app_process_device_events.argtypes = [vp, sz, vp, vp, ctypes.POINTER(vp), vp, i64, vp]
         L.sm_partition_by_owner.argtypes = [vp, ctypes.c_int, sz, ctypes.c_uint32, ctypes.c_int,
-                                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(vp), ctypes.POINTER(vp),
-                                            ctypes.POINTER(ctypes.c_uint64), vp]
+                                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                            ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64), vp]
+        L.sm_order_matches.argtypes = [vp, sz, i64, i64, vp, vp]
+        L.sm_app_copy_device_matches.argtypes = [vp, cp, vp, sz, ctypes.POINTER(sz), vp]
         L.sm_app_snapshot.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.sm_app_restore.argtypes = [vp, ctypes.c_char_p, sz]
         L.sm_app_device_matches.argtypes = [vp, cp, ctypes.POINTER(vp), ctypes.POINTER(sz)]

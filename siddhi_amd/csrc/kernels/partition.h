@@ -11,10 +11,29 @@ constexpr int kMaxPartCols = 16;
 
 struct PartCols {
   int32_t n;
-  int32_t width[kMaxPartCols];  // bytes per element: 1, 2, 4 or 8
+  int32_t width[kMaxPartCols];   // bytes per element: 1, 2, 4 or 8
+  int32_t stride[kMaxPartCols];  // bytes between consecutive destination elements (= width for a column;
+                                 // the record size when several columns are packed into one record buffer)
   const void* src[kMaxPartCols];
   void* dst[kMaxPartCols];
 };
+
+// Owner rank of a partition key: the high half of the splitmix64 finalizer of the key's 64-bit two's complement
+// image, modulo world (hash-by-key, so keys with structure in their low residues still spread over the ranks).
+// siddhi_amd/shard.py owner_of computes the same function with torch.
+__host__ __device__ inline uint32_t key_owner(int64_t key, uint32_t world) {
+  uint64_t z = (uint64_t)key;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32) % world;
+}
+
+// Matches received from the key-owning ranks, ordered back into the reference's global order for the ordinal
+// slice [lo, hi) this rank ingested: pairs are (e2 << 32) | e1 (e1 as 32-bit two's complement), the input is the
+// concatenation of per-source runs each ordered by (e2, e1), and every e2 appears in one run only.
+void order_matches(const uint64_t* pairs, int64_t n, int64_t lo, int64_t hi, uint64_t* out, Scratch& sc,
+                   hipStream_t s);
 
 void partition_by_owner(const void* keys, int key_width, int64_t n, uint32_t world, const PartCols& cols,
                         uint64_t* counts_host, Scratch& sc, hipStream_t s);

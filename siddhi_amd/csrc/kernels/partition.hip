@@ -1,4 +1,4 @@
-// Stable partition of a columnar batch by owning rank (key mod world) for the multi-GPU key exchange
+// Stable partition of a columnar batch by owning rank (key_owner: hash of the key) for the multi-GPU key exchange
 // (PartitionStreamReceiver.receive core/partition/PartitionStreamReceiver.java:156 routes each event to the
 // runtime of its key; across GPUs the key's owner rank plays that role). A counting sort with world <= 64 buckets:
 //   1. per 4096-event tile: events per owner                                  -> cnt[owner * tiles + tile]
@@ -16,8 +16,7 @@ constexpr int kPThreads = 256, kPItems = 16, kPTile = kPThreads * kPItems;
 
 template <typename K>
 __device__ __forceinline__ uint32_t owner_of(K k, uint32_t world) {
-  int64_t r = (int64_t)k % (int64_t)world;
-  return (uint32_t)(r < 0 ? r + world : r);
+  return key_owner((int64_t)k, world);
 }
 
 template <typename K>
@@ -65,11 +64,12 @@ __global__ __launch_bounds__(kPThreads) void owner_scatter_kernel(const K* __res
       uint32_t slot = run[o] + below;
       for (int q = 0; q < w; ++q) slot += wc[q][o];
       for (int c = 0; c < cols.n; ++c) {
+        char* d = (char*)cols.dst[c] + (size_t)slot * cols.stride[c];
         switch (cols.width[c]) {
-          case 4: ((uint32_t*)cols.dst[c])[slot] = ((const uint32_t*)cols.src[c])[i]; break;
-          case 8: ((uint64_t*)cols.dst[c])[slot] = ((const uint64_t*)cols.src[c])[i]; break;
-          case 2: ((uint16_t*)cols.dst[c])[slot] = ((const uint16_t*)cols.src[c])[i]; break;
-          default: ((uint8_t*)cols.dst[c])[slot] = ((const uint8_t*)cols.src[c])[i]; break;
+          case 4: *(uint32_t*)d = ((const uint32_t*)cols.src[c])[i]; break;
+          case 8: *(uint64_t*)d = ((const uint64_t*)cols.src[c])[i]; break;
+          case 2: *(uint16_t*)d = ((const uint16_t*)cols.src[c])[i]; break;
+          default: *(uint8_t*)d = ((const uint8_t*)cols.src[c])[i]; break;
         }
       }
     }
@@ -104,7 +104,41 @@ void partition_impl(const K* keys, int64_t n, uint32_t world, const PartCols& co
   sc.used = mark;
 }
 
+// per pair: one more match of its e2
+__global__ void e2_count_kernel(const uint64_t* __restrict__ p, int64_t n, int64_t lo, uint32_t* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&cnt[(int64_t)(p[i] >> 32) - lo], 1u);
+}
+
+// per pair: its place = matches of earlier e2 (scanned counts) + its rank among its e2's matches, which sit
+// consecutively (one source run, e1 order) just before it
+__global__ void e2_place_kernel(const uint64_t* __restrict__ p, int64_t n, int64_t lo, const uint32_t* __restrict__ off,
+                                uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t v = p[i];
+  const uint32_t j = (uint32_t)(v >> 32);
+  int64_t r = 0;
+  while (i - r - 1 >= 0 && (uint32_t)(p[i - r - 1] >> 32) == j) ++r;
+  out[off[(int64_t)j - lo] + r] = v;
+}
+
 }  // namespace
+
+void order_matches(const uint64_t* pairs, int64_t n, int64_t lo, int64_t hi, uint64_t* out, Scratch& sc,
+                   hipStream_t s) {
+  if (n == 0) return;
+  if (hi <= lo || hi - lo >= (int64_t)UINT32_MAX) throw std::invalid_argument("ordinal slice out of range");
+  const size_t mark = sc.used;
+  uint32_t* cnt = (uint32_t*)sc.take((size_t)(hi - lo) * 4 + 4);
+  SM_HIP(hipMemsetAsync(cnt, 0, (size_t)(hi - lo) * 4, s));
+  const dim3 g((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(e2_count_kernel, g, dim3(256), 0, s, pairs, n, lo, cnt);
+  exclusive_scan_u32(cnt, (size_t)(hi - lo), sc, s);
+  hipLaunchKernelGGL(e2_place_kernel, g, dim3(256), 0, s, pairs, n, lo, (const uint32_t*)cnt, out);
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+}
 
 void partition_by_owner(const void* keys, int key_width, int64_t n, uint32_t world, const PartCols& cols,
                         uint64_t* counts_host, Scratch& sc, hipStream_t s) {

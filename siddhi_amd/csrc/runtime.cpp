@@ -1481,31 +1481,75 @@ int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
   });
 }
 
+// Scratch of the app-less multi-GPU helpers, one per device (a process may drive several devices).
+namespace {
+struct HelperScratch {
+  std::mutex mu;
+  sm::DBuf buf;
+  sm::Scratch sc;
+};
+
+HelperScratch& helper_scratch(size_t need) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<HelperScratch>> per_dev;
+  int dev = 0;
+  SM_HIP(hipGetDevice(&dev));
+  HelperScratch* h;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto& p = per_dev[dev];
+    if (!p) p = std::make_unique<HelperScratch>();
+    h = p.get();
+  }
+  h->mu.lock();  // released by the caller (HelperLock)
+  if (h->buf.cap < need) h->buf.ensure(need);
+  h->sc.base = (char*)h->buf.p;
+  h->sc.cap = h->buf.cap;
+  h->sc.used = 0;
+  return *h;
+}
+
+struct HelperLock {
+  HelperScratch& h;
+  ~HelperLock() { h.mu.unlock(); }
+};
+}  // namespace
+
 // Multi-GPU key exchange helper (no app handle): stable partition of a device batch by owner rank.
 int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t world, int ncols,
-                          const int32_t* widths, const void* const* d_src, void* const* d_dst, uint64_t* counts,
-                          void* hip_stream) {
-  static std::mutex mu;
-  static sm::DBuf scratch;
-  static sm::Scratch sc;
-  std::lock_guard<std::mutex> g(mu);
+                          const int32_t* widths, const int32_t* strides, const void* const* d_src,
+                          void* const* d_dst, uint64_t* counts, void* hip_stream) {
   return guarded([&] {
     if (ncols < 0 || ncols > sm::kMaxPartCols) throw std::invalid_argument("ncols out of range");
+    if (key_width != 1 && key_width != 2 && key_width != 4 && key_width != 8)
+      throw std::invalid_argument("key width must be 1, 2, 4 or 8 bytes");
     sm::PartCols pc{};
     pc.n = ncols;
     for (int c = 0; c < ncols; ++c) {
       if (widths[c] != 1 && widths[c] != 2 && widths[c] != 4 && widths[c] != 8)
         throw std::invalid_argument("column width must be 1, 2, 4 or 8 bytes");
+      const int32_t st = strides ? strides[c] : widths[c];
+      if (st < widths[c]) throw std::invalid_argument("column stride smaller than its width");
+      if (((uintptr_t)d_dst[c] | (uintptr_t)st) % widths[c])
+        throw std::invalid_argument("packed field not aligned to its width");
       pc.width[c] = widths[c];
+      pc.stride[c] = st;
       pc.src[c] = d_src[c];
       pc.dst[c] = d_dst[c];
     }
-    const size_t need = (size_t)world * ((n + 4095) / 4096 + 1) * 4 + (16 << 20);
-    if (scratch.cap < need) scratch.ensure(need);
-    sc.base = (char*)scratch.p;
-    sc.cap = scratch.cap;
-    sc.used = 0;
-    sm::partition_by_owner(d_keys, key_width, (int64_t)n, world, pc, counts, sc, (hipStream_t)hip_stream);
+    HelperScratch& h = helper_scratch((size_t)world * ((n + 4095) / 4096 + 1) * 4 + (16 << 20));
+    HelperLock lk{h};
+    sm::partition_by_owner(d_keys, key_width, (int64_t)n, world, pc, counts, h.sc, (hipStream_t)hip_stream);
+  });
+}
+
+int sm_order_matches(const uint64_t* d_pairs, size_t n, int64_t lo, int64_t hi, uint64_t* d_out, void* hip_stream) {
+  return guarded([&] {
+    if (n == 0) return;
+    if (d_pairs == d_out) throw std::invalid_argument("order_matches: output must not alias the input");
+    HelperScratch& h = helper_scratch((size_t)std::max<int64_t>(hi - lo, 0) * 4 + (16 << 20));
+    HelperLock lk{h};
+    sm::order_matches(d_pairs, (int64_t)n, lo, hi, d_out, h.sc, (hipStream_t)hip_stream);
   });
 }
 
@@ -1555,6 +1599,22 @@ int sm_app_get_stat(sm_app* a, const char* key, double* out) {
       return;
     }
     throw std::invalid_argument("unknown stat " + k);
+  });
+}
+
+int sm_app_copy_device_matches(sm_app* a, const char* query_name, void* d_dst, size_t cap_bytes, size_t* n,
+                               void* hip_stream) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    for (auto& q : a->queries)
+      if (q->cq.name == query_name) {
+        const size_t bytes = (size_t)q->dev_n * (q->cq.hdr.kind == 0 ? 4 : 8);
+        if (bytes > cap_bytes) throw std::invalid_argument("copy_device_matches: destination too small");
+        if (bytes) SM_HIP(hipMemcpyAsync(d_dst, q->dev_pairs.p, bytes, hipMemcpyDeviceToDevice, (hipStream_t)hip_stream));
+        *n = (size_t)q->dev_n;
+        return;
+      }
+    throw sql::ValidationError(std::string("No query with name ") + query_name);
   });
 }
 

@@ -3,89 +3,261 @@
 The reference runs every partition key in one JVM (PartitionStreamReceiver.receive
 core/partition/PartitionStreamReceiver.java:156 → PartitionRuntime.cloneIfNotExist core/partition/PartitionRuntime.java:256):
 keys are independent, and for one input event only the runtime of that event's key runs. So a partitioned app
-shards by key with ONE exchange step: every rank ingests a contiguous slice of the arrival order, computes
-`owner = key mod world`, and the ranks swap events with one all-to-all-v. Each rank then holds the complete
-event sequence of the keys it owns, in global arrival order (stable local order + contiguous rank slices), with
-the events' global ordinals, so the per-rank device pipeline returns exactly the reference's match tuples of
-those keys. Every event belongs to one key, hence the matches triggered by one event come from one rank and a
-merge by trigger ordinal (`merge_matches`) reproduces the reference's global output order.
+shards by key with ONE exchange step: every rank ingests a contiguous slice of the arrival order, computes the
+owner rank of each event's key (`owner_of`: a splitmix64 hash of the key, so structured keys still spread), and
+the ranks swap events with one all-to-all-v of packed records (`exchange_with_ordinals`: every event's fields in
+one record, so one collective per step whatever the number of columns). Each rank then holds the complete event
+sequence of the keys it owns, in global arrival order (stable local order + contiguous rank slices), with the
+events' global ordinals, so the per-rank device pipeline returns exactly the reference's match tuples of those
+keys.
+
+Output order: every event belongs to one key, hence the matches triggered by one event (one e2) come from one
+rank. `return_matches` sends each match tuple back to the rank whose ingest slice holds its e2 (one all-to-all-v;
+the per-rank tuples are e2-ordered, so the split points are a binary search) and `order_matches` (HIP) puts the
+received runs into the reference's order for that slice: the ranks' outputs concatenated in rank order are the
+single-process output. `concat_ordered` is the same idea for index-range shards (the filter of config 2).
 """
 import torch
 import torch.distributed as dist
 
+_INT_DTYPES = (torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64)
+_BY_WIDTH = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
+
+
+def _i64(v):
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def _check_keys(keys: torch.Tensor):
+    if keys.dtype not in _INT_DTYPES:
+        raise TypeError(f"partition keys must be an integer tensor, got {keys.dtype} (hash a non-integer key to an "
+                        "integer first)")
+    if keys.dim() != 1:
+        raise ValueError("partition keys must be a 1-D tensor")
+
 
 def owner_of(keys: torch.Tensor, world: int) -> torch.Tensor:
-    """Owning rank of each key (non-negative modulo, also for negative keys)."""
-    return torch.remainder(keys.to(torch.int64), world)
+    """Owning rank of each key: hi32(splitmix64 finaliser of the key's 64-bit two's complement) mod world — the
+    function kernels/partition.h key_owner computes on the GPU (wrap-around int64 arithmetic, logical shifts)."""
+    _check_keys(keys)
+    z = keys.to(torch.int64)
+    z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * _i64(0xBF58476D1CE4E5B9)
+    z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * _i64(0x94D049BB133111EB)
+    z = z ^ ((z >> 31) & ((1 << 33) - 1))
+    return ((z >> 32) & 0xFFFFFFFF) % world
+
+
+def _launch_partition(keys, world, srcs, dsts, widths, strides):
+    import ctypes
+    from siddhi_amd import _lib
+    k = len(srcs)
+    cw = (ctypes.c_int32 * k)(*widths)
+    cs = (ctypes.c_int32 * k)(*strides)
+    src = (ctypes.c_void_p * k)(*srcs)
+    dst = (ctypes.c_void_p * k)(*dsts)
+    counts = (ctypes.c_uint64 * world)()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(keys.device).cuda_stream)
+    rc = _lib.lib().sm_partition_by_owner(keys.data_ptr(), keys.element_size(), keys.numel(), world, k, cw, cs, src,
+                                          dst, counts, stream)
+    if rc != _lib.SM_OK:
+        raise RuntimeError(_lib.lib().sm_last_error().decode(errors="replace"))
+    return [int(c) for c in counts]
+
+
+def _check_columns(keys, columns):
+    for c in columns:
+        if c.dim() != 1 or c.numel() != keys.numel() or c.device != keys.device or not c.is_contiguous():
+            raise ValueError("columns must be contiguous 1-D tensors aligned with the keys, on the keys' device")
+        if c.element_size() not in _BY_WIDTH:
+            raise ValueError(f"column element size {c.element_size()} not supported")
 
 
 def partition_by_owner(keys: torch.Tensor, columns, world: int):
     """Stable partition of `columns` by owner rank: (partitioned columns, per-owner counts). On the GPU this is
-    the HIP counting sort of the native library (sm_app partition kernel, one read of the key + one read and
-    write of each column); host tensors (the gloo CPU tests) take the equivalent torch form."""
+    the HIP counting sort of the native library (one read of the key + one read and write of each column); host
+    tensors (the gloo CPU tests) take the equivalent torch form."""
+    _check_keys(keys)
+    _check_columns(keys, columns)
     if keys.is_cuda:
-        import ctypes
-        from siddhi_amd import _lib
-        n = keys.numel()
         outs = [torch.empty_like(c) for c in columns]
-        k = len(columns)
-        widths = (ctypes.c_int32 * k)(*[c.element_size() for c in columns])
-        src = (ctypes.c_void_p * k)(*[c.data_ptr() for c in columns])
-        dst = (ctypes.c_void_p * k)(*[o.data_ptr() for o in outs])
-        counts = (ctypes.c_uint64 * world)()
-        stream = ctypes.c_void_p(torch.cuda.current_stream(keys.device).cuda_stream)
-        rc = _lib.lib().sm_partition_by_owner(keys.data_ptr(), keys.element_size(), n, world, k, widths, src, dst,
-                                              counts, stream)
-        if rc != _lib.SM_OK:
-            raise RuntimeError(_lib.lib().sm_last_error().decode(errors="replace"))
-        return outs, [int(c) for c in counts]
+        w = [c.element_size() for c in columns]
+        counts = _launch_partition(keys, world, [c.data_ptr() for c in columns], [o.data_ptr() for o in outs], w, w)
+        return outs, counts
     owner = owner_of(keys, world)
     order = torch.argsort(owner, stable=True)
     return [c[order] for c in columns], torch.bincount(owner, minlength=world).tolist()
 
 
+def record_layout(columns):
+    """Packed record of one event: fields in decreasing width (so each is aligned to its width), the record
+    padded to 8 bytes. Returns ([(offset, width)] in column order, record bytes)."""
+    order = sorted(range(len(columns)), key=lambda c: -columns[c].element_size())
+    off, lay = 0, [None] * len(columns)
+    for c in order:
+        w = columns[c].element_size()
+        lay[c] = (off, w)
+        off += w
+    return lay, (off + 7) // 8 * 8
+
+
+def pack_by_owner(keys: torch.Tensor, columns, world: int):
+    """Partition by owner and pack in one pass: an int64 (n, R/8) record tensor grouped by owner rank (arrival
+    order within an owner) + per-owner counts. On the GPU the partition kernel writes the records directly
+    (sm_partition_by_owner with strides = R)."""
+    _check_keys(keys)
+    _check_columns(keys, columns)
+    lay, R = record_layout(columns)
+    n = keys.numel()
+    rec = torch.empty((n, R // 8), dtype=torch.int64, device=keys.device)
+    if keys.is_cuda:
+        base = rec.data_ptr()
+        counts = _launch_partition(keys, world, [c.data_ptr() for c in columns], [base + o for o, _ in lay],
+                                   [w for _, w in lay], [R] * len(columns))
+        return rec, counts, lay
+    owner = owner_of(keys, world)
+    order = torch.argsort(owner, stable=True)
+    for c, (o, w) in zip(columns, lay):
+        rec.view(_BY_WIDTH[w]).view(n, R // w)[:, o // w] = c[order].view(_BY_WIDTH[w])
+    return rec, torch.bincount(owner, minlength=world).tolist(), lay
+
+
+def unpack(rec: torch.Tensor, lay, dtypes):
+    """Columns (contiguous) of a packed record tensor."""
+    m = rec.shape[0]
+    R = rec.shape[1] * 8 if rec.dim() == 2 else 8
+    out = []
+    for (o, w), dt in zip(lay, dtypes):
+        out.append(rec.view(_BY_WIDTH[w]).view(m, R // w)[:, o // w].contiguous().view(dt))
+    return out
+
+
+def _all_to_all_counts(send_counts, device, group):
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=device)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    return rc.tolist()
+
+
 def exchange_by_key(keys: torch.Tensor, columns, world: int, group=None):
     """All-to-all-v of `columns` (list of 1-D tensors aligned with `keys`) so that each rank receives the rows
-    whose key it owns. Returns (received columns, received counts per source rank). Row order in the result:
-    by source rank, then original order — i.e. global arrival order when rank r holds the r-th contiguous slice."""
+    whose key it owns, as ONE packed record per row through ONE collective. Returns (received columns, received
+    counts per source rank). Row order in the result: by source rank, then original order — i.e. global arrival
+    order when rank r holds the r-th contiguous slice."""
+    _check_keys(keys)
     if world == 1:
         return list(columns), [keys.numel()]
-    parted, sc = partition_by_owner(keys, columns, world)
-    send_counts = torch.tensor(sc, dtype=torch.int64, device=keys.device)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    rc = recv_counts.tolist()
-    out = []
-    for col in parted:
-        buf = torch.empty(sum(rc), dtype=col.dtype, device=col.device)
-        dist.all_to_all_single(buf, col, rc, sc, group=group)
-        out.append(buf)
-    return out, rc
+    rec, sc, lay = pack_by_owner(keys, columns, world)
+    rc = _all_to_all_counts(sc, keys.device, group)
+    buf = torch.empty((sum(rc), rec.shape[1]), dtype=torch.int64, device=keys.device)
+    dist.all_to_all_single(buf, rec, rc, sc, group=group)
+    return unpack(buf, lay, [c.dtype for c in columns]), rc
 
 
-def exchange_with_ordinals(keys: torch.Tensor, columns, world: int, lo: int, group=None):
+def slice_starts(lo: int, world: int, device, group=None):
+    """First global ordinal of every rank's ingest slice (all-gathered; a list of world ints)."""
+    los = torch.tensor([lo], dtype=torch.int64, device=device)
+    all_lo = [torch.empty_like(los) for _ in range(world)]
+    dist.all_gather(all_lo, los, group=group)
+    return [int(x.item()) for x in all_lo]
+
+
+def exchange_with_ordinals(keys: torch.Tensor, columns, world: int, lo: int, group=None, starts=None, offsets=None):
     """exchange_by_key plus the global arrival ordinal of every received row. The ordinal is not shipped as an
-    int64: each row carries its uint32 offset inside its source rank's contiguous slice, and the receiver adds
-    the source slice's first ordinal (all-gathered once), saving 4 of the bytes per event that cross xGMI.
+    int64: each record carries the row's uint32 offset inside its source rank's contiguous slice, and the receiver
+    adds the source slice's first ordinal (`starts`, all-gathered once and reusable across steps), saving 4 of the
+    bytes per event that cross xGMI. `offsets` (int32 arange of the slice) may be passed to reuse it across steps.
     Returns (received columns, received int64 ordinals, received counts per source rank)."""
     n = keys.numel()
     if world == 1:
         return list(columns), torch.arange(lo, lo + n, dtype=torch.int64, device=keys.device), [n]
     if n >= 2**31:
         raise ValueError("exchange_with_ordinals: more than 2^31 events in one rank's slice")
-    off = torch.arange(n, dtype=torch.int32, device=keys.device)
+    off = offsets if offsets is not None else torch.arange(n, dtype=torch.int32, device=keys.device)
     out, rc = exchange_by_key(keys, list(columns) + [off], world, group=group)
-    los = torch.tensor([lo], dtype=torch.int64, device=keys.device)
-    all_lo = [torch.empty_like(los) for _ in range(world)]
-    dist.all_gather(all_lo, los, group=group)
-    base = torch.repeat_interleave(torch.cat(all_lo), torch.tensor(rc, device=keys.device))
+    if starts is None:
+        starts = slice_starts(lo, world, keys.device, group)
+    base = torch.repeat_interleave(torch.tensor(starts, dtype=torch.int64, device=keys.device),
+                                   torch.tensor(rc, dtype=torch.int64, device=keys.device))
     return out[:-1], base + out[-1].to(torch.int64), rc
+
+
+def pack_pairs(e1: torch.Tensor, e2: torch.Tensor) -> torch.Tensor:
+    """(e2 << 32) | uint32(e1) as int64 — the layout of the device match tuples (uint32 e1, e2 interleaved)."""
+    return (e2.to(torch.int64) << 32) | (e1.to(torch.int64) & 0xFFFFFFFF)
+
+
+def unpack_pairs(p: torch.Tensor):
+    """(e1, e2) int64 tensors of packed tuples (e1 as signed 32-bit)."""
+    e1 = (p & 0xFFFFFFFF)
+    e1 = torch.where(e1 >= 1 << 31, e1 - (1 << 32), e1)
+    return e1, p >> 32
+
+
+def order_matches(pairs: torch.Tensor, lo: int, hi: int) -> torch.Tensor:
+    """Received match tuples (int64 packed, every e2 in [lo, hi); a concatenation of runs each in (e2, e1) order,
+    one e2's tuples all in one run) → the reference's output order for that slice. GPU: sm_order_matches (count
+    per e2, scan, place: HBM-bound, no comparison sort); host tensors: a stable sort by e2."""
+    if pairs.dtype != torch.int64 or pairs.dim() != 1:
+        raise TypeError("pairs must be a 1-D int64 tensor of packed (e2 << 32 | e1) tuples")
+    if pairs.numel() == 0:
+        return pairs.clone()
+    if pairs.is_cuda:
+        import ctypes
+        from siddhi_amd import _lib
+        out = torch.empty_like(pairs)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(pairs.device).cuda_stream)
+        rc = _lib.lib().sm_order_matches(pairs.data_ptr(), pairs.numel(), lo, hi, out.data_ptr(), stream)
+        if rc != _lib.SM_OK:
+            raise RuntimeError(_lib.lib().sm_last_error().decode(errors="replace"))
+        return out
+    e2 = pairs >> 32
+    if int(e2.min()) < lo or int(e2.max()) >= hi:
+        raise ValueError("a match tuple's e2 lies outside the slice")
+    return pairs[torch.argsort(e2, stable=True)]
+
+
+def return_matches(pairs: torch.Tensor, starts, hi_last: int, world: int, group=None) -> torch.Tensor:
+    """Send every match tuple (int64 packed, this rank's tuples in reference order for its keys) to the rank whose
+    ingest slice holds its e2 (`starts` = slice_starts, the last slice ending at hi_last), then order what this
+    rank received (order_matches). One all-to-all-v of 8 bytes per tuple; the split points are a binary search
+    since the tuples are e2-ordered. Returns this rank's slice of the global output, in reference order."""
+    rank = dist.get_rank(group)
+    lo = starts[rank]
+    hi = starts[rank + 1] if rank + 1 < world else hi_last
+    if world == 1:
+        return pairs
+    e2 = pairs >> 32
+    bnd = torch.searchsorted(e2, torch.tensor(starts[1:], dtype=torch.int64, device=pairs.device))
+    cuts = [0] + bnd.tolist() + [pairs.numel()]
+    sc = [cuts[r + 1] - cuts[r] for r in range(world)]
+    rc = _all_to_all_counts(sc, pairs.device, group)
+    buf = torch.empty(sum(rc), dtype=torch.int64, device=pairs.device)
+    dist.all_to_all_single(buf, pairs, rc, sc, group=group)
+    return order_matches(buf, lo, hi)
+
+
+def concat_ordered(rows: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """Index-range shards (config 2: rank r filtered the r-th contiguous slice of the arrival order): every rank's
+    kept rows (global ordinals, ordered) concatenated in rank order = the single-process output order. All-gather
+    of the per-rank counts, then of the rows padded to the largest count; every rank gets the whole output."""
+    if world == 1:
+        return rows
+    cnt = torch.tensor([rows.numel()], dtype=torch.int64, device=rows.device)
+    cnts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    cs = [int(c.item()) for c in cnts]
+    mx = max(cs)
+    pad = torch.zeros(mx, dtype=rows.dtype, device=rows.device)
+    pad[:rows.numel()] = rows
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, cs)])
 
 
 def merge_matches(parts):
     """Merge per-rank match tuples (each an (n, 2) int array of global (e1, e2) ordinals in reference order for
     that rank's keys) into the reference's global order: by e2 ordinal; ties (same e2) come from one rank and
-    keep that rank's order. Host-side (numpy) helper."""
+    keep that rank's order. Host-side (numpy) helper for tests."""
     import numpy as np
     parts = [np.asarray(p, dtype=np.int64).reshape(-1, 2) for p in parts]
     if not parts:

@@ -132,6 +132,16 @@ class ProductApp:
         _call(lib().sm_app_device_matches(self.h, query.encode(), ctypes.byref(p), ctypes.byref(n)))
         return p.value, n.value
 
+    def copy_device_matches(self, query, dst):
+        """The last device batch's tuples into the device tensor `dst` (int64 per tuple = (e2 << 32) | e1, or int32
+        kept rows of a filter) on the current stream; returns the tuple count."""
+        import torch
+        n = ctypes.c_size_t()
+        s = ctypes.c_void_p(torch.cuda.current_stream(dst.device).cuda_stream)
+        _call(lib().sm_app_copy_device_matches(self.h, query.encode(), ctypes.c_void_p(dst.data_ptr()),
+                                               dst.numel() * dst.element_size(), ctypes.byref(n), s))
+        return n.value
+
     def get_stat(self, key):
         v = ctypes.c_double()
         _call(lib().sm_app_get_stat(self.h, key.encode(), ctypes.byref(v)))

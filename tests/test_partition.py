@@ -1,10 +1,10 @@
 """HIP stable partition by owner rank (sm_partition_by_owner), the send side of the multi-GPU key exchange:
-identical to a stable sort by owner (key mod world, non-negative) for int32 / int64 keys, negative keys, ragged
-sizes and 1/2/4/8-byte columns."""
+identical to a stable sort by owner (shard.owner_of, the splitmix64 key hash) for int32 / int64 keys, negative
+keys, ragged sizes and 1/2/4/8-byte columns; the packed-record form and the match-ordering kernel."""
 import pytest
 import torch
 
-from siddhi_amd.shard import partition_by_owner
+from siddhi_amd.shard import owner_of, pack_by_owner, partition_by_owner, order_matches, pack_pairs, unpack
 
 pytestmark = pytest.mark.gpu
 
@@ -21,8 +21,43 @@ def test_partition_equals_stable_sort(n, world, kdt):
             torch.randint(0, 999, (n,), generator=g, dtype=torch.int16)]
     dev = torch.device("cuda", 0)
     got, counts = partition_by_owner(keys.to(dev), [c.to(dev) for c in cols], world)
-    owner = torch.remainder(keys.to(torch.int64), world)
+    owner = owner_of(keys, world)
     order = torch.argsort(owner, stable=True)
     assert counts == torch.bincount(owner, minlength=world).tolist()
     for a, c in zip(got, cols):
         assert torch.equal(a.cpu(), c[order])
+    rec, pc, lay = pack_by_owner(keys.to(dev), [c.to(dev) for c in cols], world)
+    assert pc == counts
+    rec_h, _, _ = pack_by_owner(keys, cols, world)  # the torch (gloo / CPU) form
+    if n:
+        assert torch.equal(rec.cpu().view(torch.uint8).view(n, -1)[:, :sum(w for _, w in lay)],
+                           rec_h.view(torch.uint8).view(n, -1)[:, :sum(w for _, w in lay)])
+    for a, c in zip(unpack(rec, lay, [c.dtype for c in cols]), cols):
+        assert torch.equal(a.cpu(), c[order])
+
+
+def test_partition_rejects_float_keys():
+    dev = torch.device("cuda", 0)
+    with pytest.raises(TypeError):
+        partition_by_owner(torch.rand(10, device=dev), [torch.rand(10, device=dev)], 2)
+
+
+@pytest.mark.parametrize("n_src,per", [(1, 1000), (3, 50000), (8, 200000)])
+def test_order_matches_kernel_equals_stable_sort(n_src, per):
+    """sm_order_matches over runs the way return_matches receives them (each run e2-ordered, an e2's tuples in
+    one run) equals a stable sort by e2."""
+    g = torch.Generator().manual_seed(n_src * 7 + per)
+    lo, hi = 1000, 1000 + 4 * per * n_src
+    e2all = torch.randperm(hi - lo, generator=g)[:per * n_src] + lo
+    runs = []
+    for r in range(n_src):
+        e2 = torch.sort(e2all[r::n_src]).values
+        rep = torch.randint(1, 4, (e2.numel(),), generator=g)
+        e2 = torch.repeat_interleave(e2, rep)
+        e1 = e2 - torch.randint(1, 900, (e2.numel(),), generator=g)
+        # within one e2, e1 in reference order (arbitrary but fixed): keep generation order
+        runs.append(pack_pairs(e1, e2))
+    pairs = torch.cat(runs)
+    exp = pairs[torch.argsort(pairs >> 32, stable=True)]
+    got = order_matches(pairs.to(torch.device("cuda", 0)), lo, hi)
+    assert torch.equal(got.cpu(), exp)

@@ -1,6 +1,8 @@
 """Multi-rank path of the partitioned pattern (config 4) on CPU with the gloo backend, world size 2 and 3:
-contiguous ingest slices → key exchange (siddhi_amd.shard.exchange_by_key, the same code bench.py runs over
-RCCL) → per-rank matching with global ordinals → merge_matches must equal the single-process reference output.
+contiguous ingest slices → key exchange (siddhi_amd.shard.exchange_with_ordinals: one packed record per event,
+the same code bench.py runs over RCCL) → per-rank matching with global ordinals → return_matches (every tuple to
+the rank that ingested its e2, ordered there) — the ranks' outputs concatenated in rank order must equal the
+single-process reference output. Config 2 (filter, index-range shards): concat_ordered of the per-rank kept rows.
 The per-rank matcher here is the CPU oracle (this test checks the sharding logic, not the kernels; the GPU
 kernels on a rank's key subset are checked in tests/test_device_batch.py::test_sharded_ordinals_match_oracle_subset)."""
 import ctypes
@@ -56,11 +58,16 @@ def _worker(rank, world, port, outfile):
         (w_sym, w_price), w_ord, w_counts = exchange_with_ordinals(t[0], [t[0], t[1]], world, lo)
         assert w_counts == counts and torch.equal(w_ord, r_ord)
         assert torch.equal(w_sym, r_sym) and torch.equal(w_price, r_price)
-        assert (np.remainder(r_sym.numpy(), world) == rank).all()
+        from siddhi_amd.shard import owner_of, pack_pairs, return_matches, slice_starts, unpack_pairs
+        assert (owner_of(r_sym, world) == rank).all()
         local = oracle_refs([r_sym.numpy(), r_price.numpy(), r_vol.numpy(), r_tsa.numpy()], r_ts.numpy())
-        glob = ords[local] if len(local) else local
+        glob = ords[local] if len(local) else local.reshape(-1, 2)
+        packed = pack_pairs(torch.from_numpy(glob[:, 0]), torch.from_numpy(glob[:, 1]))
+        mine = return_matches(packed, slice_starts(lo, world, packed.device), N, world)
+        e1, e2 = unpack_pairs(mine)
+        assert ((e2 >= lo) & (e2 < hi)).all()
         parts = [None] * world
-        dist.all_gather_object(parts, glob.tolist())
+        dist.all_gather_object(parts, [glob.tolist(), torch.stack([e1, e2], 1).tolist()])
         if rank == 0:
             with open(outfile, "w") as f:
                 json.dump(parts, f)
@@ -84,11 +91,113 @@ def test_sharded_exchange_and_merge_equal_single_process(world, tmp_path):
     mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
     with open(out) as f:
         parts = json.load(f)
-    got = merge_matches(parts)
     sym, price, vol, tsa, ts = synth.gen_stock(0, N, K, DIV, synth.seed_for(4))
     exp = oracle_refs([sym, price, vol, tsa], ts)
     assert len(exp) > 1000
+    np.testing.assert_array_equal(merge_matches([p[0] for p in parts]), exp)  # host merge of per-key-rank tuples
+    returned = np.concatenate([np.asarray(p[1], dtype=np.int64).reshape(-1, 2) for p in parts])
+    np.testing.assert_array_equal(returned, exp)  # per-slice outputs in rank order = the single output
+
+
+APP2 = ("define stream StockStream (symbol int, price double, volume long, timestamp long); "
+        "@info(name='q') from StockStream[price > 70 and volume < 1000] select timestamp insert into Out;")
+
+
+def oracle_filter(cols, ts):
+    a = OracleApp(APP2)
+    a.start()
+    cs = [np.ascontiguousarray(c) for c in cols]
+    ptrs = (ctypes.c_void_p * len(cs))(*[c.ctypes.data for c in cs])
+    err = ctypes.create_string_buffer(512)
+    ts = np.ascontiguousarray(ts, dtype=np.int64)
+    rc = olib().cr_send_columns(a.h, a.stream_index("StockStream"), len(ts), ts.ctypes.data, ptrs, err, 512)
+    assert rc == 0, err.value
+    out = a.outputs()["streams"].get("Out", [])
+    a.close()
+    return np.array([r[1][0] for r in out], dtype=np.int64)  # the selected timestamp = global ordinal
+
+
+def _worker2(rank, world, port, outfile):
+    from siddhi_amd.shard import concat_ordered
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = N * rank // world, N * (rank + 1) // world
+        sym, price, vol, tsa, ts = synth.gen_stock(lo, hi, K, 1, synth.seed_for(2))
+        kept = oracle_filter([sym, price, vol, tsa], ts)  # the timestamp attribute = global ordinal
+        assert ((kept >= lo) & (kept < hi)).all()
+        allrows = concat_ordered(torch.from_numpy(kept), world)
+        if rank == 0:
+            with open(outfile, "w") as f:
+                json.dump(allrows.tolist(), f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 3])
+def test_config2_index_range_shards_concat_equal_single_process(world, tmp_path):
+    out = str(tmp_path / "rows.json")
+    mp.start_processes(_worker2, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    got = np.asarray(json.load(open(out)), dtype=np.int64)
+    sym, price, vol, tsa, ts = synth.gen_stock(0, N, K, 1, synth.seed_for(2))
+    exp = oracle_filter([sym, price, vol, tsa], ts)
+    assert len(exp) > 1000
     np.testing.assert_array_equal(got, exp)
+
+
+def test_owner_hash_spreads_structured_keys():
+    """Keys that are all multiples of the world size still spread over every rank (a plain key mod world would
+    send them all to rank 0), and the owner is a function of the key only."""
+    from siddhi_amd.shard import owner_of
+    keys = torch.arange(0, 8 * 10000, 8, dtype=torch.int64)
+    cnt = torch.bincount(owner_of(keys, 8), minlength=8)
+    assert int(cnt.min()) > 1000
+    assert torch.equal(owner_of(keys.to(torch.int32), 8), owner_of(keys, 8))
+    with pytest.raises(TypeError):
+        owner_of(keys.to(torch.float64), 8)
+
+
+def test_owner_hash_known_values():
+    """hi32(splitmix64 finaliser) of a few keys, computed independently with Python integers."""
+    from siddhi_amd.shard import owner_of
+
+    def ref(k, world):
+        z = k & (2**64 - 1)
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+        z ^= z >> 31
+        return (z >> 32) % world
+    keys = [0, 1, -1, 7, 123456789, -(2**40) + 3, 2**62 + 11, -(2**63)]
+    for w in (2, 3, 7, 8, 64):
+        got = owner_of(torch.tensor(keys, dtype=torch.int64), w).tolist()
+        assert got == [ref(k, w) for k in keys]
+
+
+def test_pack_unpack_round_trip():
+    from siddhi_amd.shard import pack_by_owner, unpack, owner_of
+    g = torch.Generator().manual_seed(3)
+    n = 1000
+    keys = torch.randint(-50, 50, (n,), generator=g, dtype=torch.int64).to(torch.int32)
+    cols = [keys, torch.rand(n, generator=g, dtype=torch.float64), torch.arange(n, dtype=torch.int64),
+            torch.randint(0, 255, (n,), generator=g, dtype=torch.uint8), torch.arange(n, dtype=torch.int32)]
+    rec, counts, lay = pack_by_owner(keys, cols, 5)
+    assert rec.shape == (n, 4)  # 8 + 8 + 4 + 4 + 1 -> 32 bytes
+    got = unpack(rec, lay, [c.dtype for c in cols])
+    order = torch.argsort(owner_of(keys, 5), stable=True)
+    for a, c in zip(got, cols):
+        assert torch.equal(a, c[order])
+    assert counts == torch.bincount(owner_of(keys, 5), minlength=5).tolist()
+
+
+def test_order_matches_host():
+    from siddhi_amd.shard import order_matches, pack_pairs, unpack_pairs
+    runs = [[(1, 10), (3, 10), (2, 12)], [(0, 11), (5, 13), (4, 13)], [(6, 14)]]
+    e1 = torch.tensor([p[0] for r in runs for p in r])
+    e2 = torch.tensor([p[1] for r in runs for p in r])
+    a, b = unpack_pairs(order_matches(pack_pairs(e1, e2), 10, 15))
+    assert b.tolist() == [10, 10, 11, 12, 13, 13, 14] and a.tolist() == [1, 3, 0, 2, 5, 4, 6]
 
 
 def test_merge_keeps_same_trigger_order():
