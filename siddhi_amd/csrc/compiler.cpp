@@ -634,6 +634,10 @@ CompiledQuery compile_query(const App& app, const Query& q, int order, int parti
   h.nrecv = (int)recvs.size();
   h.nwithin = (int)withins.size();
   h.nsel = (int)cq.sel_types.size();
+  h.nrefs_vis = (int)refs.size() / 2;
+  if (cq.fast_every_within) {  // hidden (e1, e2) ordinals for the NFA fallback of device batches
+    refs.insert(refs.end(), {0, 0, 1, 0});
+  }
   h.nrefs = (int)refs.size() / 2;
   h.nconst = (int)consts.size();
   // per-key state layout (int64 words)

@@ -40,6 +40,9 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
 // Per-event index arrays of a device-resident interleaved batch (the device restatement of stage_record);
 // returns the number of clock-advance points written to adv_*.
 // sid[i] = stream index, or NFA_TICK (-1) for a playback heartbeat (clock advance without an event).
+// out[i] = start + i
+void iota_i64(int64_t* out, int64_t n, int64_t start, hipStream_t s);
+
 int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const int64_t* ts, const int64_t* ord_in,
                           int64_t ord_base, bool playback, int64_t clock_in, int64_t* ev_row, int64_t* ev_ord,
                           int64_t* ev_clock, int64_t* adv_pos, int64_t* adv_clock, int64_t* adv_wall,

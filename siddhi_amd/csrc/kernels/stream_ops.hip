@@ -733,6 +733,16 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
   return hv;
 }
 
+namespace {
+__global__ void iota_kernel(int64_t* __restrict__ out, int64_t n, int64_t start) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = start + i;
+}
+}  // namespace
+
+void iota_i64(int64_t* out, int64_t n, int64_t start, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(iota_kernel, grid_for(n), dim3(256), 0, s, out, n, start);
+}
 
 int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const int64_t* ts, const int64_t* ord_in,
                           int64_t ord_base, bool playback, int64_t clock_in, int64_t* ev_row, int64_t* ev_ord,

@@ -111,7 +111,9 @@ struct DQuery {
   int32_t nreset, nupdate;
   int32_t reset_seq[2 * kMaxSlots], update_seq[2 * kMaxSlots];
   int32_t nsel;         // output attributes
-  int32_t nrefs;        // select variable references (parity tuples)
+  int32_t nrefs;        // variable references written per output: the select's (parity tuples), then for a
+                        // closed-form query two hidden ones, (e1, e2), read by the NFA fallback of device batches
+  int32_t nrefs_vis;    // the select's references (the first nrefs_vis)
   int32_t nconst;
   int32_t slot_nattr[kMaxSlots];   // attributes stored per chain node of each slot (its stream's width)
   int32_t slot_stream[kMaxSlots];  // app stream index of each slot

@@ -20,6 +20,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/siddhi_amd.h"
@@ -101,6 +102,7 @@ struct HostOut {
   std::vector<DVal> vals;
   std::vector<int64_t> refs;
   int qidx;
+  int64_t e1 = -1, e2 = -1;  // closed-form queries: ordinals of the match's two events (hidden references)
 };
 
 struct Callback {
@@ -119,8 +121,17 @@ struct PreparedChunk {
   size_t n_stream_cbs = 0;
   std::vector<sm_event> evs;
   std::vector<sm_value> vals;
-  std::deque<std::string> strs;   // stable addresses for STRING values
+  std::vector<std::unique_ptr<std::string>> strs;  // owned STRING values (stable addresses)
+  PreparedChunk() = default;
+  PreparedChunk(PreparedChunk&&) noexcept = default;
+  PreparedChunk& operator=(PreparedChunk&&) noexcept = default;
+  PreparedChunk(const PreparedChunk&) = delete;
+  PreparedChunk& operator=(const PreparedChunk&) = delete;
 };
+// evs point into vals and vals into strs: chunks must only ever move (a vector grows by moving its elements only
+// when their move cannot throw; a copy would leave the pointers in the freed originals)
+static_assert(std::is_nothrow_move_constructible<PreparedChunk>::value && !std::is_copy_constructible<PreparedChunk>::value,
+              "PreparedChunk must move, never copy");
 
 struct QueryRt {
   CompiledQuery cq;
@@ -140,7 +151,9 @@ struct QueryRt {
   FastState fast;            // v2 kernels' persistent look-back state
   FastCarry carry;           // open partials carried across device batches (closed-form queries)
   bool nfa_used = false;     // host-API batches ran through the NFA kernel (partials live in ks / heap)
-  int fast_path_used = 0;    // 3 = bucket stack, 2 = onesweep form, 1 = general form (last device batch)
+  bool nfa_mode = false;     // a closed-form query handed to the NFA kernel for good (nfa_device_batch)
+  int fast_path_used = 0;    // 5 = NFA kernel, 3 = bucket stack, 2 = onesweep form, 1 = general form (last device
+                             // batch)
   ~QueryRt() { carry.release(); }
 };
 
@@ -221,7 +234,7 @@ struct sm_app {
   hipStream_t stream = nullptr;
   sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_ev_ord, d_adv_pos, d_adv_clock, d_adv_wall, d_adv_upto, d_streams,
       d_err, d_count,
-      d_keyoff, scratch;
+      d_keyoff, scratch, d_rp, d_rp_streams;
   sm::Scratch sc;
 };
 
@@ -486,8 +499,8 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
       to_sm_values(a, h, cq, vals);
       for (auto& v : vals)
         if (v.type == T_STRING && !v.is_null) {
-          ch.strs.emplace_back(v.s);
-          v.s = ch.strs.back().c_str();
+          ch.strs.push_back(std::make_unique<std::string>(v.s));
+          v.s = ch.strs.back()->c_str();
         }
       ch.vals.insert(ch.vals.end(), vals.begin(), vals.end());
     }
@@ -527,8 +540,12 @@ void read_outputs(sm_app* a, int qidx, const void* dev, int64_t n, std::vector<H
     memcpy(&h.r, b, sizeof(OutRec));
     h.vals.resize(cq.hdr.nsel);
     memcpy(h.vals.data(), b + sizeof(OutRec), cq.hdr.nsel * sizeof(DVal));
-    h.refs.resize(cq.hdr.nrefs);
-    memcpy(h.refs.data(), b + sizeof(OutRec) + cq.hdr.nsel * sizeof(DVal), cq.hdr.nrefs * sizeof(int64_t));
+    const int64_t* rf = (const int64_t*)(b + sizeof(OutRec) + cq.hdr.nsel * sizeof(DVal));
+    h.refs.assign(rf, rf + cq.hdr.nrefs_vis);
+    if (cq.hdr.nrefs == cq.hdr.nrefs_vis + 2) {
+      h.e1 = rf[cq.hdr.nrefs_vis];
+      h.e2 = rf[cq.hdr.nrefs_vis + 1];
+    }
     h.qidx = qidx;
     outs.push_back(std::move(h));
   }
@@ -675,6 +692,140 @@ size_t batch_scratch(const sm_app* a, int64_t N) {
   for (auto& q : a->queries)
     if (q->cq.hdr.kind != 0) lane_words = std::max<int64_t>(lane_words, LaneEv::words(q->cq.hdr.node_words));
   return (size_t)N * (100 + 8 * (size_t)lane_words) + (64 << 20);
+}
+
+// A closed-form query handed to the general NFA kernel for the rest of its life (QueryRt::nfa_mode) when a device
+// batch leaves the closed form's premise: event time decreasing inside the batch or against the carried state,
+// a condition outside the v2 kernels' envelope with partials to carry, or matching state already held by the NFA
+// (host-API events). The reference has no such switch: it always runs the NFA (StreamPreStateProcessor
+// processAndReturn :274-327), and the closed form is only a shortcut of it for monotone event time.
+// The carried open partials move into the NFA state by replaying their e1 events in front of the batch, in
+// arrival order: each replayed event passes c1 again and re-creates its partial, and as an e2 candidate it meets
+// only replayed partials of its own key that it already failed when it first arrived (a partial is still open
+// only because every later event of its key failed c2 without expiring it: isExpired :102-121), so the replay
+// emits nothing. The batch's matches go to dev_pairs as in the closed form: (e1, e2) relative to ordinal_base,
+// in reference order.
+int64_t nfa_device_batch(sm_app* a, int qi, int s, size_t n, const int64_t* d_ts, const void* const* d_cols,
+                         const int64_t* d_ordinals, int64_t ordinal_base, hipStream_t hs) {
+  QueryRt& q = *a->queries[qi];
+  const auto& attrs = a->streams[s].def->attrs;
+  const int nattr = (int)attrs.size();
+  const int64_t nc = q.nfa_mode ? 0 : q.carry.n;
+  const int64_t N = nc + (int64_t)n;
+  q.nfa_mode = true;
+  q.carry.reset();  // its partials are handed over below; a failure from here on marks the app failed
+  if (N == 0) return 0;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t off = 0;
+  std::vector<size_t> col_off(nattr);
+  for (int k = 0; k < nattr; ++k) {
+    col_off[k] = off;
+    off += al((size_t)N * width_of((int)attrs[k].type));
+  }
+  const size_t ts_off = off;
+  off += al((size_t)N * 8);
+  const size_t ord_off = off;
+  off += al((size_t)N * 8);
+  const size_t sid_off = off;
+  off += al((size_t)N * 4);
+  a->d_rp.ensure(off);
+  char* base = (char*)a->d_rp.p;
+  std::vector<std::vector<char>> hcols(nattr);
+  std::vector<int64_t> hts, hord;
+  if (nc > 0) {
+    const int w = q.carry.width;
+    std::vector<int64_t> rows((size_t)nc * w);
+    SM_HIP(hipMemcpyAsync(rows.data(), q.carry.rows, rows.size() * 8, hipMemcpyDeviceToHost, hs));
+    SM_HIP(hipStreamSynchronize(hs));
+    for (int k = 0; k < nattr; ++k) {
+      const int t = (int)attrs[k].type, cw = width_of(t);
+      hcols[k].resize((size_t)nc * cw);
+      for (int64_t r = 0; r < nc; ++r) {
+        const int64_t v = rows[(size_t)r * w + 3 + k];  // canonical: integers as int64, FLOAT / DOUBLE as double bits
+        char* d = hcols[k].data() + (size_t)r * cw;
+        if (t == T_INT || t == T_STRING) {
+          const int32_t x = (int32_t)v;
+          memcpy(d, &x, 4);
+        } else if (t == T_FLOAT) {
+          double x;
+          memcpy(&x, &v, 8);
+          const float f = (float)x;
+          memcpy(d, &f, 4);
+        } else if (t == T_LONG || t == T_DOUBLE) {
+          memcpy(d, &v, 8);
+        } else {
+          const uint8_t x = (uint8_t)(v != 0);
+          memcpy(d, &x, 1);
+        }
+      }
+      SM_HIP(hipMemcpyAsync(base + col_off[k], hcols[k].data(), hcols[k].size(), hipMemcpyHostToDevice, hs));
+    }
+    hts.resize(nc);
+    hord.resize(nc);
+    for (int64_t r = 0; r < nc; ++r) {
+      hord[r] = rows[(size_t)r * w + 1];
+      hts[r] = rows[(size_t)r * w + 2];
+    }
+    SM_HIP(hipMemcpyAsync(base + ts_off, hts.data(), nc * 8, hipMemcpyHostToDevice, hs));
+    SM_HIP(hipMemcpyAsync(base + ord_off, hord.data(), nc * 8, hipMemcpyHostToDevice, hs));
+  }
+  for (int k = 0; k < nattr; ++k) {
+    const size_t cw = width_of((int)attrs[k].type);
+    if (n) SM_HIP(hipMemcpyAsync(base + col_off[k] + nc * cw, d_cols[k], n * cw, hipMemcpyDeviceToDevice, hs));
+  }
+  if (n) SM_HIP(hipMemcpyAsync(base + ts_off + nc * 8, d_ts, n * 8, hipMemcpyDeviceToDevice, hs));
+  if (d_ordinals) {
+    if (n) SM_HIP(hipMemcpyAsync(base + ord_off + nc * 8, d_ordinals, n * 8, hipMemcpyDeviceToDevice, hs));
+  } else {
+    iota_i64((int64_t*)(base + ord_off) + nc, (int64_t)n, ordinal_base, hs);
+  }
+  SM_HIP(hipMemsetD32Async((hipDeviceptr_t)(base + sid_off), s, (size_t)N, hs));
+  std::vector<NfaStream> nst(a->streams.size());
+  memset(nst.data(), 0, nst.size() * sizeof(NfaStream));
+  nst[s].nattr = nattr;
+  for (int k = 0; k < nattr; ++k) {
+    nst[s].types[k] = (int)attrs[k].type;
+    nst[s].cols[k] = base + col_off[k];
+  }
+  a->d_rp_streams.ensure(nst.size() * sizeof(NfaStream));
+  SM_HIP(hipMemcpyAsync(a->d_rp_streams.p, nst.data(), nst.size() * sizeof(NfaStream), hipMemcpyHostToDevice, hs));
+  for (DBuf* d : {&a->d_ev_row, &a->d_ev_clock, &a->d_ev_ord, &a->d_adv_pos, &a->d_adv_clock, &a->d_adv_wall,
+                  &a->d_adv_upto})
+    d->ensure((size_t)N * 8);
+  a->d_err.ensure(16);
+  a->d_count.ensure(16);
+  ensure_scratch(a, batch_scratch(a, N));
+  a->sc.used = 0;
+  const int32_t* sid = (const int32_t*)(base + sid_off);
+  const int64_t* ts = (const int64_t*)(base + ts_off);
+  int64_t clock_out = a->clock;  // the closed form leaves the playback clock alone: so does its fallback
+  const int64_t nadv = build_event_index(N, sid, (int32_t)a->streams.size(), ts, (const int64_t*)(base + ord_off), 0,
+                                         a->ast.playback, a->clock, (int64_t*)a->d_ev_row.p, (int64_t*)a->d_ev_ord.p,
+                                         (int64_t*)a->d_ev_clock.p, (int64_t*)a->d_adv_pos.p,
+                                         (int64_t*)a->d_adv_clock.p, (int64_t*)a->d_adv_wall.p,
+                                         (int64_t*)a->d_adv_upto.p, &clock_out, a->sc, hs);
+  const EvArrays ev{sid, (const int64_t*)a->d_ev_row.p, ts, (const int64_t*)a->d_ev_clock.p,
+                    (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_rp_streams.p, (const int64_t*)a->d_adv_pos.p,
+                    (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p, (const int64_t*)a->d_adv_upto.p,
+                    nadv, a->clock};
+  std::vector<HostOut> outs;
+  a->sc.used = 0;
+  run_pattern_query(a, qi, ev, N, outs, hs);
+  std::stable_sort(outs.begin(), outs.end(), [](const HostOut& x, const HostOut& y) {
+    return x.r.pos != y.r.pos ? x.r.pos < y.r.pos : x.r.seq < y.r.seq;
+  });
+  std::vector<uint32_t> pairs(outs.size() * 2);
+  for (size_t k = 0; k < outs.size(); ++k) {
+    if (outs[k].r.pos < nc || outs[k].e1 < 0 || outs[k].e2 < 0)
+      throw std::runtime_error("query '" + q.cq.name + "': internal error in the hand-over of carried partials");
+    pairs[2 * k] = (uint32_t)(outs[k].e1 - ordinal_base);
+    pairs[2 * k + 1] = (uint32_t)(outs[k].e2 - ordinal_base);
+  }
+  q.dev_pairs.ensure(std::max<size_t>(pairs.size() * 4, 16));
+  if (!pairs.empty())
+    SM_HIP(hipMemcpyAsync(q.dev_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, hs));
+  SM_HIP(hipStreamSynchronize(hs));
+  return (int64_t)outs.size();
 }
 
 void flush(sm_app* a) {
@@ -868,7 +1019,7 @@ using namespace sm;
 
 // snapshot encoding helpers (sm_app_snapshot / sm_app_restore)
 namespace {
-constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '1'};
+constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '2'};
 
 struct SnapWriter {
   std::vector<uint8_t> b;
@@ -1140,7 +1291,7 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       a->started = false;
       a->failed = false;
       a->failed_why.clear();
-      for (auto& q : a->queries) q->nfa_used = false;
+      for (auto& q : a->queries) q->nfa_used = q->nfa_mode = false;
       if (value) {  // reset and start again
         a->started = true;
         stage_record(a, NFA_START, -1, a->clock, 0);
@@ -1163,10 +1314,10 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
     if (s < 0) throw sql::ValidationError("unknown stream");
     flush(a);  // staged host events come first (arrival order)
     for (auto& qp : a->queries)
-      if (qp->cq.hdr.kind != 0 && qp->nfa_used &&
+      if (qp->cq.hdr.kind != 0 && !qp->cq.fast_every_within &&
           std::find(qp->cq.streams.begin(), qp->cq.streams.end(), s) != qp->cq.streams.end())
-        throw sql::UnsupportedError("query '" + qp->cq.name + "' holds partial matches from host-API events; device "
-                                    "batches of its streams need a fresh (or reset) app");
+        throw sql::UnsupportedError("device batches support filter queries and `every e1 -> e2 within T` patterns; "
+                                    "query '" + qp->cq.name + "' takes sm_app_process_device_events or the host API");
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
     StreamStage& st = a->streams[s];
     NfaStream d;
@@ -1190,8 +1341,9 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
                                                    nc * (160 + 8 * wc) + ((size_t)640 << 20));
     }
     ensure_scratch(a, need);
-    for (auto& qp : a->queries) {
-      QueryRt& q = *qp;
+    try {
+    for (size_t qi = 0; qi < a->queries.size(); ++qi) {
+      QueryRt& q = *a->queries[qi];
       const CompiledQuery& cq = q.cq;
       if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
       a->sc.used = 0;
@@ -1208,9 +1360,11 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
         q.fast_path_used = typed ? 4 : 3;
         continue;
       }
-      if (!cq.fast_every_within)
-        throw sql::UnsupportedError("device batches support filter queries and `every e1 -> e2 within T` patterns; "
-                                    "query '" + cq.name + "' needs the host API");
+      if (q.nfa_mode || q.nfa_used) {  // matching state held by the NFA kernel
+        q.dev_n = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs);
+        q.fast_path_used = 5;
+        continue;
+      }
       FastArgs fa{};
       fa.n = (int64_t)n;
       fa.ts = d_ts;
@@ -1256,16 +1410,23 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
         m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
                                  a->fast_timing ? &a->fast_tm : nullptr, a->fast_stack);
       q.fast_path_used = q.fast.last_path;
-      if (m == FAST_NON_MONOTONE)
-        throw std::runtime_error("query '" + cq.name + "': event time decreases in a device batch");
-      if (m < 0) {
-        if (q.carry.n > 0)
-          throw sql::UnsupportedError("query '" + cq.name + "': partial matches carried from an earlier device batch "
-                                      "need the closed-form kernels");
+      if (m == FAST_OUTSIDE && a->force_general_fast && q.carry.n == 0) {
+        // diagnostic (option "fast_general"): the stateless general closed form, one batch at a time
         m = fast_every_within(fa, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs, a->fast_timing ? &a->fast_tm : nullptr);
         q.fast_path_used = 1;
+      } else if (m < 0) {
+        // event time not monotone, or a condition outside the v2 envelope: the NFA kernel takes the query over
+        // (carried partials included) and keeps it, so later batches and host events see one matching state
+        m = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs);
+        q.fast_path_used = 5;
       }
       q.dev_n = m;
+    }
+    } catch (const std::exception& e) {
+      a->failed = true;
+      a->failed_why = std::string("a device batch failed half-way (") + e.what() +
+                      "); the matching state is inconsistent: restore a snapshot or reset the app";
+      throw;
     }
   });
 }
@@ -1355,8 +1516,10 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
 // snapshot holds what the reference's Snapshotables hold for the hot path: every partition instance (key table),
 // each instance's pending / new-and-every partial matches with their event chains (per-key state words + heap,
 // StreamPreStateProcessor.currentState :339-353), pending scheduler timers (Scheduler.currentState), the
-// playback clock and the arrival ordinal, plus the string dictionary the device values refer to. Staged events
-// are flushed first, so the snapshot is taken at a batch boundary.
+// playback clock and the arrival ordinal, plus the string dictionary the device values refer to. Closed-form
+// queries fed by device batches keep their open partials as carry rows instead (FastCarry): those rows, the
+// last batch's event time and the query's hand-over flags are part of the snapshot too. Staged events are flushed
+// first, so the snapshot is taken at a batch boundary.
 
 int sm_app_snapshot(sm_app* a, uint8_t* buf, size_t cap, size_t* len) {
   return locked(a, [&] {
@@ -1398,6 +1561,15 @@ int sm_app_snapshot(sm_app* a, uint8_t* buf, size_t cap, size_t* len) {
         std::vector<int64_t> heap((size_t)n * heap_words);
         SM_HIP(hipMemcpy(heap.data(), q.heap.p, heap.size() * 8, hipMemcpyDeviceToHost));
         w.raw(heap.data(), heap.size() * 8);
+      }
+      w.put<uint8_t>((uint8_t)(q.nfa_used | (q.nfa_mode << 1) | (q.carry.active << 2)));
+      w.put<int64_t>(q.carry.ts_last);
+      w.put<int64_t>(q.carry.n);
+      w.put<int32_t>(q.carry.width);
+      if (q.carry.n > 0) {
+        std::vector<int64_t> rows((size_t)q.carry.n * q.carry.width);
+        SM_HIP(hipMemcpy(rows.data(), q.carry.rows, rows.size() * 8, hipMemcpyDeviceToHost));
+        w.raw(rows.data(), rows.size() * 8);
       }
     }
     *len = w.b.size();
@@ -1476,10 +1648,29 @@ int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
       } else if (q.state_slots) {
         SM_HIP(hipMemset(q.ks.p, 0, (size_t)q.state_slots * kw * 8));
       }
+      const uint8_t fl = r.get<uint8_t>();
+      q.nfa_used = fl & 1;
+      q.nfa_mode = (fl >> 1) & 1;
+      q.carry.reset();
+      q.carry.active = (fl >> 2) & 1;
+      q.carry.ts_last = r.get<int64_t>();
+      const int64_t cn = r.get<int64_t>();
+      const int32_t cw = r.get<int32_t>();
+      if (cn < 0 || cw < 0 || (cn > 0 && cw < 3)) throw std::runtime_error("CannotRestoreSiddhiAppStateException: bad carry");
+      if (cn > 0) {
+        std::vector<int64_t> rows((size_t)cn * cw);
+        r.raw(rows.data(), rows.size() * 8);
+        q.carry.reserve(cn, cw);
+        SM_HIP(hipMemcpy(q.carry.rows, rows.data(), rows.size() * 8, hipMemcpyHostToDevice));
+        q.carry.n = cn;
+      }
+      q.carry.width = cw;
     }
     if (r.o != len) throw std::runtime_error("CannotRestoreSiddhiAppStateException: trailing bytes");
   });
 }
+
+}  // extern "C"
 
 // Scratch of the app-less multi-GPU helpers, one per device (a process may drive several devices).
 namespace {
@@ -1514,6 +1705,8 @@ struct HelperLock {
   ~HelperLock() { h.mu.unlock(); }
 };
 }  // namespace
+
+extern "C" {
 
 // Multi-GPU key exchange helper (no app handle): stable partition of a device batch by owner rank.
 int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t world, int ncols,

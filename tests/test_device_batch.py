@@ -99,14 +99,14 @@ def test_variants_match_oracle(variant):
         kw["c1"] = "[price > 30 and volume < 1500]"
     elif variant == "c2_const":
         kw["c2"] = "price > e1.price + 5.0"
-        expect_path = 1  # not a fixed compare of the carried attribute: general kernels
+        expect_path = 5  # not a fixed compare of the carried attribute: the NFA kernel takes the query
     elif variant == "no_within":
         kw["within"] = ""
     elif variant == "no_c1":
         kw["c1"] = ""
     elif variant == "two_attrs":
         kw["c2"] = "price > e1.price and volume < e1.volume"
-        expect_path = 1
+        expect_path = 5
     elif variant == "c2_ge":
         kw["c2"] = "e1.price <= price"
     cols, ts = stock(n, K, div, key_dtype=kd, key_offset=ko)

@@ -193,3 +193,117 @@ def test_stack_equals_walk_large():
     np.testing.assert_array_equal(a, b)
     c = run_stream(text, cols, ts, pieces(n, [1_000_003, 999_999]), stack=1, expect_path=3)
     np.testing.assert_array_equal(c, a)
+
+
+# ---- the NFA hand-over (runtime.cpp nfa_device_batch): when a batch leaves the closed form's premise the general
+# NFA kernel takes the query over, carried partials included, and keeps it; outputs stay the reference's.
+
+def _shuffle_times(ts, lo, hi, seed=5):
+    """Event time no longer monotone inside [lo, hi): swap a few neighbouring timestamps."""
+    ts = ts.copy()
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(np.arange(lo, hi - 1), size=max(1, (hi - lo) // 50), replace=False)
+    for i in idx:
+        ts[i], ts[i + 1] = ts[i + 1], ts[i]
+    assert (np.diff(ts[lo:hi]) < 0).any()
+    return ts
+
+
+@pytest.mark.parametrize("stack", [1, 2])
+def test_non_monotone_batch_hands_over_to_nfa(stack):
+    n, K, div = 30000, 150, 5
+    cols, ts = stock(n, K, div)
+    ts = _shuffle_times(ts, 16000, 24000)
+    text = app_text()
+    exp = oracle_pairs(text, cols, ts)
+    import torch
+    from siddhi_amd.testing import ProductApp
+    app = ProductApp(text, fast_stack=stack)
+    dev = torch.device("cuda", 0)
+    got, paths = [], []
+    for lo, hi in [(0, 8000), (8000, 16000), (16000, 24000), (24000, 30000)]:
+        tcols = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
+        tts = torch.from_numpy(np.ascontiguousarray(ts[lo:hi])).to(dev)
+        app.process_device_batch("StockStream", tts, tcols, ordinal_base=lo)
+        got.append(app.device_matches_host("q").view(np.int32).astype(np.int64) + lo)
+        paths.append(app.get_stat("fast_path:q"))
+    app.close()
+    assert paths == [3 if stack == 1 else 2] * 2 + [5, 5]  # taken over at the first non-monotone batch, for good
+    np.testing.assert_array_equal(np.concatenate(got), exp)
+
+
+def test_batch_earlier_than_carried_state_hands_over():
+    """A batch whose first event is older than the last carried one (time going back across batches)."""
+    n, K, div = 20000, 100, 5
+    cols, ts = stock(n, K, div)
+    ts = ts.copy()
+    ts[10000:] -= 3  # a step back at the batch boundary, monotone afterwards
+    text = app_text()
+    exp = oracle_pairs(text, cols, ts)
+    got = run_stream(text, cols, ts, [(0, 10000), (10000, n)])
+    np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("c2", ["price > e1.price and volume < e1.volume", "price > e1.price + 5.0"])
+def test_outside_envelope_streams_through_nfa(c2):
+    """Conditions outside the v2 kernels' envelope keep their partials across batches through the NFA kernel."""
+    n, K, div = 24000, 120, 5
+    cols, ts = stock(n, K, div)
+    text = app_text(c2=c2)
+    exp = oracle_pairs(text, cols, ts)
+    got = run_stream(text, cols, ts, pieces(n, [5000, 1, 7000]), expect_path=5)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_host_events_then_device_batches():
+    """Partials opened by host-API events (NFA state) continue into device batches."""
+    import torch
+    from siddhi_amd.testing import ProductApp
+    n, K, div = 20000, 80, 5
+    cols, ts = stock(n, K, div)
+    text = app_text()
+    exp = oracle_pairs(text, cols, ts)
+    app = ProductApp(text)
+    app.start()
+    h = 7000
+    app.send_columns("StockStream", np.ascontiguousarray(ts[:h]), [np.ascontiguousarray(c[:h]) for c in cols])
+    app.flush()
+    host = np.array([r[2] for r in app.outputs()["streams"].get("OutputStream", [])], dtype=np.int64).reshape(-1, 2)
+    dev = torch.device("cuda", 0)
+    got = [host]
+    for lo, hi in [(h, 15000), (15000, n)]:
+        tcols = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
+        tts = torch.from_numpy(np.ascontiguousarray(ts[lo:hi])).to(dev)
+        app.process_device_batch("StockStream", tts, tcols, ordinal_base=lo)
+        assert app.get_stat("fast_path:q") == 5
+        got.append(app.device_matches_host("q").view(np.int32).astype(np.int64) + lo)
+    app.close()
+    np.testing.assert_array_equal(np.concatenate(got), exp)
+
+
+@pytest.mark.parametrize("stack", [1, 2])
+def test_snapshot_restore_keeps_carried_partials(stack):
+    """SiddhiAppRuntime.snapshot / restore between device batches: the carried partials travel in the snapshot."""
+    import torch
+    from siddhi_amd.testing import ProductApp
+    n, K, div = 20000, 90, 5
+    cols, ts = stock(n, K, div)
+    text = app_text()
+    exp = oracle_pairs(text, cols, ts)
+    dev = torch.device("cuda", 0)
+
+    def batch(app, lo, hi):
+        tcols = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
+        tts = torch.from_numpy(np.ascontiguousarray(ts[lo:hi])).to(dev)
+        app.process_device_batch("StockStream", tts, tcols, ordinal_base=lo)
+        return app.device_matches_host("q").view(np.int32).astype(np.int64) + lo
+
+    a = ProductApp(text, fast_stack=stack)
+    first = batch(a, 0, 9000)
+    snap = a.snapshot()
+    a.close()
+    b = ProductApp(text, fast_stack=stack)
+    b.restore(snap)
+    second = batch(b, 9000, n)
+    b.close()
+    np.testing.assert_array_equal(np.concatenate([first, second]), exp)
