@@ -532,10 +532,14 @@ struct Output {
   std::vector<int64_t> refs;
 };
 
+struct PartitionRt;
+
 struct QueryRt {
   OApp* app = nullptr;
   int query_index = 0;  // position in app.order
   bool partitioned = false;  // clone inside a partition: QueryCallbacks are not inherited (PartitionRuntime)
+  PartitionRt* part = nullptr;  // partition instance this clone belongs to (inner streams stay inside it)
+  int inst = -1;
   const Query* q = nullptr;
   bool sequence = false;
   std::vector<MetaStream> metas;
@@ -558,7 +562,7 @@ struct AppStream {
   const StreamDef* def;
   // subscribers in subscription order: (query runtime index in non-partitioned list) or partition receiver
   struct Sub {
-    int kind;  // 0 = plain query, 1 = partition
+    int kind;  // 0 = plain query, 1 = partition (keyed), 2 = partition (stream without a key: broadcast)
     int index;
   };
   std::vector<Sub> subs;
@@ -617,6 +621,7 @@ void post_process(Post* po, const STP& s);
 void absent_timer(Pre* p, int64_t now);
 void selector_emit(QueryRt* q, const STP& s);
 void notifyAt(Scheduler* sc, int64_t t);
+void publish(QueryRt* q, std::vector<Value> vals, int64_t ts);
 
 STP new_state(QueryRt* q) {
   auto s = std::make_shared<StateEvent>();
@@ -1167,7 +1172,6 @@ void selector_emit(QueryRt* q, const STP& s) {
   OApp* a = q->app;
   const std::string& out = q->q->insert_into;
   a->stream_count[out]++;
-  if (!a->collect) return;
   Output o;
   o.ts = s->timestamp;
   EvalCtx c;
@@ -1179,15 +1183,17 @@ void selector_emit(QueryRt* q, const STP& s) {
       o.refs.push_back(se && se->row ? se->row->ordinal : -1);
     }
   }
-  a->stream_out[out].push_back(o);
-  if (!q->partitioned) a->query_out[q->q->name].calls.push_back({o.ts, {o}});
+  if (a->collect) {
+    a->stream_out[out].push_back(o);
+    if (!q->partitioned) a->query_out[q->q->name].calls.push_back({o.ts, {o}});
+  }
+  publish(q, std::move(o.vals), o.ts);
 }
 
 void selector_emit_row(QueryRt* q, const Row& row, int64_t ts) {
   OApp* a = q->app;
   const std::string& out = q->q->insert_into;
   a->stream_count[out]++;
-  if (!a->collect) return;
   Output o;
   o.ts = ts;
   EvalCtx c;
@@ -1196,8 +1202,11 @@ void selector_emit_row(QueryRt* q, const Row& row, int64_t ts) {
     o.vals.push_back(eval(*q->select[k], c));
     for (size_t v = 0; v < q->select_vars[k].size(); ++v) o.refs.push_back(row.ordinal);
   }
-  a->stream_out[out].push_back(o);
-  if (!q->partitioned) a->query_out[q->q->name].calls.push_back({o.ts, {o}});
+  if (a->collect) {
+    a->stream_out[out].push_back(o);
+    if (!q->partitioned) a->query_out[q->q->name].calls.push_back({o.ts, {o}});
+  }
+  publish(q, std::move(o.vals), o.ts);
 }
 
 // ---------------------------------------------------------------- lowering (StateInputStreamParser)
@@ -1555,6 +1564,10 @@ void selector_process_list(QueryRt* q, std::vector<STP>& ret) {
   for (auto& s : ret) selector_emit(q, s);
 }
 
+bool reads(const QueryRt* q, const std::string& sid) {
+  return q->q->input == InputKind::SINGLE ? q->q->stream_id == sid : q->receivers.count(sid) != 0;
+}
+
 // Receivers for one event of stream `sid` into one query runtime.
 void deliver(QueryRt* q, const std::string& sid, const RowP& row, int64_t ts) {
   if (q->q->input == InputKind::SINGLE) {
@@ -1655,12 +1668,20 @@ void advance_clock(OApp* a, int64_t ts) {
   }
 }
 
-void send_row(OApp* a, int si, int64_t ts, RowP row) {
+// StreamJunction.sendEvent: every receiver of the stream, in subscription order
+void dispatch(OApp* a, int si, const RowP& row, int64_t ts) {
   AppStream& st = a->streams[si];
-  advance_clock(a, ts);  // StreamJunction.sendData :232-237
   for (auto& sub : st.subs) {
     if (sub.kind == 0) {
       deliver(a->queries[sub.index].get(), st.def->id, row, ts);
+    } else if (sub.kind == 2) {
+      // PartitionStreamReceiver.send(ComplexEvent) :271-275: a stream the partition does not key is sent to every
+      // existing instance. The reference iterates a ConcurrentHashMap of the instances' junctions; instances are
+      // visited here in creation order (the same whenever one instance exists when the event arrives).
+      PartitionRt* pr = a->partitions[sub.index].get();
+      for (size_t inst = 0; inst < pr->instances.size(); ++inst)
+        for (auto& qrt : pr->instances[inst])
+          if (reads(qrt.get(), st.def->id)) deliver(qrt.get(), st.def->id, row, ts);
     } else {
       PartitionRt* pr = a->partitions[sub.index].get();
       // PartitionStreamReceiver.receive(long, Object[]) :156-168
@@ -1685,15 +1706,42 @@ void send_row(OApp* a, int si, int64_t ts, RowP row) {
                 order_index = (int)o;
             pr->instances.back().push_back(build_query(a, pr->p->queries[qi], order_index));
             pr->instances.back().back()->partitioned = true;
+            pr->instances.back().back()->part = pr;
+            pr->instances.back().back()->inst = inst;
           }
         } else {
           inst = f->second;
         }
         // inner junction (stream+key): receivers subscribed in query order
-        for (auto& qrt : pr->instances[inst]) deliver(qrt.get(), st.def->id, row, ts);
+        for (auto& qrt : pr->instances[inst])
+          if (reads(qrt.get(), st.def->id)) deliver(qrt.get(), st.def->id, row, ts);
       }
     }
   }
+}
+
+void send_row(OApp* a, int si, int64_t ts, RowP row) {
+  advance_clock(a, ts);  // StreamJunction.sendData :232-237
+  dispatch(a, si, row, ts);
+}
+
+// InsertIntoStreamCallback.send → StreamJunction.sendEvent (no clock update: only sendData advances the playback
+// clock). A query's output event goes on to the queries reading its stream, depth first, before the next input
+// event; an inner stream ('#name') only to the queries of the same partition instance (PartitionRuntime
+// localStreamJunctionMap, keyed by stream id + partition key).
+void publish(QueryRt* q, std::vector<Value> vals, int64_t ts) {
+  OApp* a = q->app;
+  const std::string& out = q->q->insert_into;
+  auto row = std::make_shared<Row>();
+  row->ordinal = -1;  // not an input event: no arrival ordinal
+  row->vals = std::move(vals);
+  if (out[0] == '#') {
+    for (auto& qrt : q->part->instances[q->inst])
+      if (reads(qrt.get(), out)) deliver(qrt.get(), out, row, ts);
+    return;
+  }
+  const int si = a->stream_index(out);
+  if (si >= 0 && !a->streams[si].subs.empty()) dispatch(a, si, row, ts);
 }
 
 void build_app(OApp* a) {
@@ -1761,21 +1809,13 @@ void build_app(OApp* a) {
         else ins.insert(ins.end(), probe->receiver_order.begin(), probe->receiver_order.end());
       }
       for (auto& id : ins) {
-        if (!pr->key_exec.count(id))
-          throw UnsupportedError("non-partitioned stream '" + id + "' inside a partition is not supported");
-        sub_stream(id, 1, (int)a->partitions.size());
+        if (id[0] == '#') continue;  // inner stream: fed by the instance's own queries (publish)
+        // keyed streams go to their key's instance, the others to every instance (PartitionStreamReceiver)
+        sub_stream(id, pr->key_exec.count(id) ? 1 : 2, (int)a->partitions.size());
       }
       a->partitions.push_back(std::move(pr));
     }
   }
-  // queries may not consume streams produced by other queries (query chaining is out of scope)
-  std::set<std::string> produced;
-  for (auto& q : a->ast.queries) produced.insert(q.insert_into);
-  for (auto& p : a->ast.partitions)
-    for (auto& q : p.queries) produced.insert(q.insert_into);
-  for (auto& s : a->streams)
-    if (!s.subs.empty() && produced.count(s.def->id))
-      throw UnsupportedError("query chaining (stream '" + s.def->id + "' is both produced and consumed) is not supported");
 }
 
 Value from_c(OApp* a, AttrType t, const cr_value& v) {

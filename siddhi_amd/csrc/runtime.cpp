@@ -312,6 +312,10 @@ void build_app(sm_app* a) {
     const sql::Query& qd = pi < 0 ? a->ast.queries[qi] : a->ast.partitions[pi].queries[qi];
     auto q = std::make_unique<QueryRt>();
     q->cq = compile_query(a->ast, qd, (int)o, pi, a->dict);
+    for (int s : q->cq.streams)
+      if (a->ast.streams[s].implicit)
+        throw sql::UnsupportedError("query '" + q->cq.name + "' reads stream '" + a->ast.streams[s].id +
+                                    "', which a query produces: query chaining runs in the CPU oracle only");
     if (pi >= 0) {
       q->part = &a->parts[pi];
       for (int s : q->cq.streams)

@@ -53,8 +53,12 @@ struct Attribute {
 };
 
 struct StreamDef {
-  std::string id;
+  std::string id;  // "#name" for a partition's inner stream
   std::vector<Attribute> attrs;
+  // defined by a query's `insert into` (SiddhiApp.defineStream from the query's output attributes) rather than by
+  // `define stream`; partition = the partition an inner stream belongs to (-1: app-level stream)
+  bool implicit = false;
+  int partition = -1;
   int index_of(const std::string& n) const {
     for (size_t i = 0; i < attrs.size(); ++i)
       if (attrs[i].name == n) return (int)i;

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <functional>
 #include <map>
 
 namespace sql {
@@ -408,9 +409,13 @@ struct Parser {
 
   // ---- sources ----
   // basic_source: source basic_source_stream_handlers?  (filters only: '#'? '[' expression ']')
+  // source: inner='#'? stream_id (SiddhiQL.g4 `source`); an inner stream keeps its '#' in the id
+  std::string source_id() {
+    if (accept_sym("#")) return "#" + ident();
+    return ident();
+  }
   void basic_source(StateElem& s) {
-    if (is_sym("#")) throw UnsupportedError("inner streams (#) are outside the hot-path subset");
-    s.stream_id = ident();
+    s.stream_id = source_id();
     for (;;) {
       if (is_sym("#") && is_sym("[", 1)) ++p;
       if (accept_sym("[")) {
@@ -663,7 +668,6 @@ struct Parser {
     expect_kw("from");
     q.input = classify_input();
     if (q.input == InputKind::SINGLE) {
-      if (is_sym("#")) throw UnsupportedError("inner streams (#) are outside the hot-path subset");
       StateElem tmp;
       basic_source(tmp);
       q.stream_id = tmp.stream_id;
@@ -702,8 +706,7 @@ struct Parser {
       if (accept_kw("current")) { expect_kw("events"); }
       else if (is_kw("expired") || is_kw("all")) throw UnsupportedError("only current events are supported");
       expect_kw("into");
-      if (is_sym("#")) throw UnsupportedError("inner streams (#) are outside the hot-path subset");
-      q.insert_into = ident();
+      q.insert_into = source_id();
     } else if (is_kw("delete") || is_kw("update") || is_kw("return")) {
       throw UnsupportedError("table operations / return are outside the hot-path subset");
     } else {
@@ -808,32 +811,116 @@ void collect_stream_ids(const StateElem* e, std::vector<std::string>& out) {
   }
 }
 
+namespace {
+
+void collect_refs(const StateElem* e, std::vector<std::pair<std::string, std::string>>& out) {
+  switch (e->kind) {
+    case StateKind::LOGICAL:
+    case StateKind::NEXT: collect_refs(e->a.get(), out); collect_refs(e->b.get(), out); break;
+    case StateKind::COUNT:
+    case StateKind::EVERY: collect_refs(e->a.get(), out); break;
+    case StateKind::STREAM:
+    case StateKind::ABSENT: out.push_back({e->event_ref, e->stream_id}); break;
+  }
+}
+
+// Type of a select expression (Java binary numeric promotion for arithmetic, as the executors'
+// MathExpressionExecutor* classes return: double > float > long > int; compare / logic → BOOL).
+AttrType infer_type(const Expr& x, const std::function<AttrType(const Expr&)>& var_type) {
+  switch (x.kind) {
+    case ExprKind::CONST: return x.ctype;
+    case ExprKind::VAR: return var_type(x);
+    case ExprKind::MATH: {
+      const AttrType a = infer_type(*x.ch[0], var_type), b = infer_type(*x.ch[1], var_type);
+      auto num = [](AttrType t) { return t == AttrType::INT || t == AttrType::LONG || t == AttrType::FLOAT || t == AttrType::DOUBLE; };
+      if (!num(a) || !num(b)) throw ValidationError("arithmetic operands must be numeric");
+      if (a == AttrType::DOUBLE || b == AttrType::DOUBLE) return AttrType::DOUBLE;
+      if (a == AttrType::FLOAT || b == AttrType::FLOAT) return AttrType::FLOAT;
+      if (a == AttrType::LONG || b == AttrType::LONG) return AttrType::LONG;
+      return AttrType::INT;
+    }
+    default: return AttrType::BOOL;
+  }
+}
+
+}  // namespace
+
+// Validation common to both lowerings, in app order (SiddhiAppParser adds queries one by one): every stream a
+// query reads is defined by `define stream` or by the `insert into` of an earlier query; an `insert into` of an
+// undefined stream defines it from the query's output attributes (names and types: QueryParser →
+// OutputParser / SiddhiApp.defineStream). Inner streams ('#name') exist only inside their partition
+// (PartitionRuntime.addQuery :118-142, localStreamDefinitionMap).
 App parse_app(const std::string& text) {
   Parser ps;
   ps.tk = lex(text);
   ps.parse();
-  // Validation common to both lowerings: streams referenced must exist.
-  std::vector<std::string> produced;
-  for (auto& q : ps.app.queries) produced.push_back(q.insert_into);
-  for (auto& pt : ps.app.partitions)
-    for (auto& q : pt.queries) produced.push_back(q.insert_into);
-  auto check_stream = [&](const std::string& id) {
-    if (std::find(produced.begin(), produced.end(), id) != produced.end())
-      throw UnsupportedError("query chaining (stream '" + id + "' is produced by a query) is not supported");
-    if (!ps.app.find_stream(id)) throw ValidationError("stream '" + id + "' is not defined");
+  App& app = ps.app;
+  auto find_in = [&](const std::string& id, int part) -> const StreamDef* {
+    for (auto& s : app.streams)
+      if (s.id == id && (id[0] != '#' || s.partition == part)) return &s;
+    return nullptr;
   };
-  std::vector<const Query*> all;
-  for (auto& q : ps.app.queries) all.push_back(&q);
-  for (auto& pt : ps.app.partitions) {
-    for (auto& w : pt.with) check_stream(w.stream_id);
-    for (auto& q : pt.queries) all.push_back(&q);
-  }
-  for (const Query* q : all) {
-    if (q->input == InputKind::SINGLE) check_stream(q->stream_id);
-    else {
-      std::vector<std::string> ids;
-      collect_stream_ids(q->state.get(), ids);
-      for (auto& id : ids) check_stream(id);
+  auto check_stream = [&](const std::string& id, int part) -> const StreamDef* {
+    if (id[0] == '#' && part < 0) throw ValidationError("inner stream '" + id + "' used outside a partition");
+    const StreamDef* d = find_in(id, part);
+    if (!d) throw ValidationError("stream '" + id + "' is not defined");
+    return d;
+  };
+  for (auto& pt : app.partitions)
+    for (auto& w : pt.with) {
+      if (w.stream_id[0] == '#') throw ValidationError("partition key on inner stream '" + w.stream_id + "'");
+      check_stream(w.stream_id, -1);
+    }
+  for (auto [pi, qi] : app.order) {
+    Query& q = pi < 0 ? app.queries[qi] : app.partitions[pi].queries[qi];
+    // input streams (copies: app.streams may grow below)
+    std::vector<std::pair<std::string, StreamDef>> ins;  // (event reference, stream)
+    if (q.input == InputKind::SINGLE) {
+      ins.push_back({"", *check_stream(q.stream_id, pi)});
+    } else {
+      std::vector<std::pair<std::string, std::string>> refs;
+      collect_refs(q.state.get(), refs);
+      for (auto& r : refs) ins.push_back({r.first, *check_stream(r.second, pi)});
+    }
+    auto var_type = [&](const Expr& v) -> AttrType {
+      for (auto& in : ins)
+        if (v.stream_ref.empty() || v.stream_ref == in.first || v.stream_ref == in.second.id) {
+          const int a = in.second.index_of(v.attr);
+          if (a >= 0) return in.second.attrs[a].type;
+        }
+      throw ValidationError("attribute '" + v.attr + "' is not defined");
+    };
+    std::vector<Attribute> out;
+    if (q.select_all) {
+      for (auto& in : ins)
+        for (auto& at : in.second.attrs) {
+          bool dup = false;
+          for (auto& o : out) dup |= o.name == at.name;
+          if (dup) {
+            if (q.input == InputKind::SINGLE) continue;
+            throw ValidationError("Duplicate attribute exist in streams");
+          }
+          out.push_back(at);
+        }
+    } else {
+      for (auto& oa : q.select) out.push_back({oa.rename, infer_type(*oa.expr, var_type)});
+    }
+    const std::string& id = q.insert_into;
+    if (id[0] == '#' && pi < 0) throw ValidationError("inner stream '" + id + "' used outside a partition");
+    if (const StreamDef* d = find_in(id, pi)) {
+      if (d->attrs.size() != out.size())
+        throw ValidationError("query '" + q.name + "' inserts " + std::to_string(out.size()) +
+                              " attributes into stream '" + id + "' of " + std::to_string(d->attrs.size()));
+    } else {
+      if (id[0] == '#')
+        for (auto& s : app.streams)
+          if (s.id == id) throw UnsupportedError("inner stream '" + id + "' defined in two partitions");
+      StreamDef nd;
+      nd.id = id;
+      nd.attrs = out;
+      nd.implicit = true;
+      nd.partition = id[0] == '#' ? pi : -1;
+      app.streams.push_back(std::move(nd));
     }
   }
   return std::move(ps.app);

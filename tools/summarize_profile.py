@@ -40,8 +40,13 @@ FAMILIES = [("walk_kernel<", "walk"), ("downsweep_wc_kernel<0", "key_pass0"), ("
             ("lane_index_kernel", "nfa_setup")]
 
 
-def family(name):
-    for pat, lab in FAMILIES:
+# the closed-form pipelines (configs 3 / 4) use the radix sort only to order the carried partials
+CARRY_FAMILIES = [("rs_downsweep", "carry_out"), ("rs_upsweep", "carry_out"), ("carry_rows_kernel", "carry_out"),
+                  ("gather_u64_kernel", "carry_out"), ("gather_rows_kernel", "carry_out")]
+
+
+def family(name, config=4):
+    for pat, lab in (CARRY_FAMILIES if config in (3, 4) else []) + FAMILIES:
         if pat in name:
             return lab
     return None
@@ -89,7 +94,7 @@ def main():
     traffic = {}
     stats = csv_in("prof_stats", "kernel_stats.csv")
     for r in csv.DictReader(open(stats)):
-        fam = family(r["Name"])
+        fam = family(r["Name"], config)
         if not fam:
             continue
         nm = short(r["Name"])
