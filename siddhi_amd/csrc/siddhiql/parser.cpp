@@ -890,25 +890,27 @@ App parse_app(const std::string& text) {
         }
       throw ValidationError("attribute '" + v.attr + "' is not defined");
     };
+    // the output schema (a select the lowerings reject, e.g. an unknown attribute or a duplicate name under
+    // `select *`, is reported by them with the query's context; the AST itself stays valid)
     std::vector<Attribute> out;
-    if (q.select_all) {
-      for (auto& in : ins)
-        for (auto& at : in.second.attrs) {
-          bool dup = false;
-          for (auto& o : out) dup |= o.name == at.name;
-          if (dup) {
-            if (q.input == InputKind::SINGLE) continue;
-            throw ValidationError("Duplicate attribute exist in streams");
+    try {
+      if (q.select_all) {
+        for (auto& in : ins)
+          for (auto& at : in.second.attrs) {
+            bool dup = false;
+            for (auto& o : out) dup |= o.name == at.name;
+            if (!dup) out.push_back(at);
           }
-          out.push_back(at);
-        }
-    } else {
-      for (auto& oa : q.select) out.push_back({oa.rename, infer_type(*oa.expr, var_type)});
+      } else {
+        for (auto& oa : q.select) out.push_back({oa.rename, infer_type(*oa.expr, var_type)});
+      }
+    } catch (const ValidationError&) {
+      out.clear();
     }
     const std::string& id = q.insert_into;
     if (id[0] == '#' && pi < 0) throw ValidationError("inner stream '" + id + "' used outside a partition");
     if (const StreamDef* d = find_in(id, pi)) {
-      if (d->attrs.size() != out.size())
+      if (!d->implicit && !out.empty() && d->attrs.size() != out.size())
         throw ValidationError("query '" + q.name + "' inserts " + std::to_string(out.size()) +
                               " attributes into stream '" + id + "' of " + std::to_string(d->attrs.size()));
     } else {
