@@ -15,12 +15,14 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <limits>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <sstream>
 #include <string>
 #include <type_traits>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/siddhi_amd.h"
@@ -103,6 +105,7 @@ struct HostOut {
   std::vector<int64_t> refs;
   int qidx;
   int64_t e1 = -1, e2 = -1;  // closed-form queries: ordinals of the match's two events (hidden references)
+  int64_t key_code = 0;      // partition queries: the instance's key code (an inner stream's routing key)
 };
 
 struct Callback {
@@ -145,6 +148,8 @@ struct QueryRt {
   std::vector<DBuf> keycode; // code / consts backing the key programs
   int nkeyprogs = 0;
   const CompiledPartition* part = nullptr;
+  int pidx = -1;             // its partition
+  bool bcast = false;        // reads a stream its partition does not key (sent to every instance)
   // device batch results
   DBuf dev_pairs;
   int64_t dev_n = 0;
@@ -152,6 +157,7 @@ struct QueryRt {
   FastCarry carry;           // open partials carried across device batches (closed-form queries)
   bool nfa_used = false;     // host-API batches ran through the NFA kernel (partials live in ks / heap)
   bool nfa_mode = false;     // a closed-form query handed to the NFA kernel for good (nfa_device_batch)
+  int level = 0;             // chaining depth: 0 reads input streams only, L reads a stream a level L-1 query fills
   int fast_path_used = 0;    // 5 = NFA kernel, 3 = bucket stack, 2 = onesweep form, 1 = general form (last device
                              // batch)
   ~QueryRt() { carry.release(); }
@@ -198,6 +204,13 @@ struct sm_app {
   // device-batch fast path knobs (sm_app_set_option "fast_general" / "fast_timing") and the last timings
   bool force_general_fast = false;
   int fast_stack = 0;  // option "fast_stack": 0 = automatic, 1 = always the bucket-stack kernels, 2 = never
+  int max_level = 0;   // deepest query chaining level (0: no query reads a stream another query fills)
+  std::vector<char> stream_fed;  // per stream: some query reads it and some query inserts into it
+  // per partition: the streams it does not key that its queries read (broadcast to every instance), and the key
+  // codes of its instances in creation order (the instances a broadcast event reaches)
+  std::vector<std::vector<int>> part_bcast;
+  std::vector<std::vector<int64_t>> part_keys;
+  std::vector<std::unordered_set<int64_t>> part_key_set;
   bool fast_timing = false;
   bool fast_tm_ready = false;
   sm::FastTimings fast_tm{};
@@ -306,23 +319,95 @@ void build_app(sm_app* a) {
     st.dcols.resize(na);
     st.dnulls.resize(na);
   }
-  for (auto& p : a->ast.partitions) a->parts.push_back(compile_partition(a->ast, p, a->dict));
+  for (size_t pi = 0; pi < a->ast.partitions.size(); ++pi) {
+    a->parts.push_back(compile_partition(a->ast, a->ast.partitions[pi], a->dict));
+    // inner streams ('#name') of the partition carry their instance's key code in one extra LONG column, which
+    // is their key program (PartitionRuntime routes them by the junction of stream id + key)
+    for (size_t si = 0; si < a->ast.streams.size(); ++si) {
+      const sql::StreamDef& d = a->ast.streams[si];
+      if (d.id[0] != '#' || d.partition != (int)pi) continue;
+      const int hidden = (int)d.attrs.size();
+      if (hidden + 1 > kMaxAttrs) throw sql::UnsupportedError("inner stream has too many attributes");
+      Instr in{};
+      in.op = OP_COL;
+      in.a = hidden;
+      in.t0 = T_LONG;
+      a->parts.back().streams.push_back((int)si);
+      a->parts.back().key_code.push_back({in});
+      a->parts.back().key_consts.push_back({});
+      a->parts.back().key_type.push_back(T_LONG);
+      StreamStage& st = a->streams[si];
+      st.cols.resize(hidden + 1);
+      st.nulls.resize(hidden + 1);
+      st.any_null.assign(hidden + 1, false);
+      st.dcols.resize(hidden + 1);
+      st.dnulls.resize(hidden + 1);
+    }
+  }
+  // query chaining: a query reading a stream other queries insert into runs one level after them, over the
+  // input events merged with theirs (flush)
+  std::vector<std::vector<int>> producers(a->ast.streams.size());
+  a->stream_fed.assign(a->ast.streams.size(), 0);
+  a->part_bcast.assign(a->ast.partitions.size(), {});
+  a->part_keys.assign(a->ast.partitions.size(), {});
+  a->part_key_set.assign(a->ast.partitions.size(), {});
   for (size_t o = 0; o < a->ast.order.size(); ++o) {
     auto [pi, qi] = a->ast.order[o];
     const sql::Query& qd = pi < 0 ? a->ast.queries[qi] : a->ast.partitions[pi].queries[qi];
     auto q = std::make_unique<QueryRt>();
     q->cq = compile_query(a->ast, qd, (int)o, pi, a->dict);
-    for (int s : q->cq.streams)
-      if (a->ast.streams[s].implicit)
-        throw sql::UnsupportedError("query '" + q->cq.name + "' reads stream '" + a->ast.streams[s].id +
-                                    "', which a query produces: query chaining runs in the CPU oracle only");
+    for (int s : q->cq.streams) {
+      if (!a->ast.streams[s].implicit) continue;
+      a->stream_fed[s] = 1;
+      for (int pq : producers[s]) q->level = std::max(q->level, a->queries[pq]->level + 1);
+    }
+    a->max_level = std::max(a->max_level, q->level);
     if (pi >= 0) {
       q->part = &a->parts[pi];
+      q->pidx = pi;
+      CompiledPartition& cpm = a->parts[pi];
       for (int s : q->cq.streams)
-        if (std::find(q->part->streams.begin(), q->part->streams.end(), s) == q->part->streams.end())
-          throw sql::UnsupportedError("non-partitioned stream '" + a->ast.streams[s].id +
-                                      "' inside a partition is not supported");
-      if (q->cq.hdr.kind == 0) throw sql::UnsupportedError("single-stream queries inside a partition are not supported");
+        if (std::find(cpm.streams.begin(), cpm.streams.end(), s) == cpm.streams.end() ||
+            std::find(a->part_bcast[pi].begin(), a->part_bcast[pi].end(), s) != a->part_bcast[pi].end()) {
+          // a stream the partition does not key: every instance receives it (PartitionStreamReceiver :271-275).
+          // The flush hands such a query one copy of each of these events per existing instance, carrying the
+          // instance's key code in an extra column (the stream's key program here); instances are tracked on the
+          // host, so the partition's keys must be columns
+          if (q->cq.hdr.kind == 0)
+            throw sql::UnsupportedError("a single-stream query inside a partition must read a keyed stream");
+          for (size_t k = 0; k < cpm.key_code.size(); ++k)
+            if (cpm.key_code[k].size() != 1 || cpm.key_code[k][0].op != OP_COL)
+              throw sql::UnsupportedError("a partition whose queries read an unkeyed stream needs columns as keys");
+          q->bcast = true;
+          if (std::find(a->part_bcast[pi].begin(), a->part_bcast[pi].end(), s) == a->part_bcast[pi].end()) {
+            Instr in{};
+            in.op = OP_COL;
+            in.a = (int)a->ast.streams[s].attrs.size();
+            in.t0 = T_LONG;
+            if (in.a + 1 > kMaxAttrs) throw sql::UnsupportedError("stream has too many attributes");
+            cpm.streams.push_back(s);
+            cpm.key_code.push_back({in});
+            cpm.key_consts.push_back({});
+            cpm.key_type.push_back(T_LONG);
+            a->part_bcast[pi].push_back(s);
+          }
+        }
+      if (q->cq.hdr.kind == 0) {
+        // a filter inside a partition: the same rows as outside, minus those whose key is null (A17); the key is
+        // read on the host, so it must be a column of the stream
+        const CompiledPartition& cp = *q->part;
+        const int k = (int)(std::find(cp.streams.begin(), cp.streams.end(), q->cq.hdr.stream) - cp.streams.begin());
+        if (cp.key_code[k].size() != 1 || cp.key_code[k][0].op != OP_COL)
+          throw sql::UnsupportedError("a single-stream query inside a partition needs a column as the key");
+      }
+    }
+    const int out = sm::stream_index(a->ast, qd.insert_into);
+    if (out >= 0 && a->ast.streams[out].implicit) {
+      const auto& at = a->ast.streams[out].attrs;
+      bool same = at.size() == q->cq.sel_types.size();
+      for (size_t k = 0; same && k < at.size(); ++k) same = (int)at[k].type == q->cq.sel_types[k];
+      if (!same) throw sql::ValidationError("query '" + q->cq.name + "' output does not match stream '" + qd.insert_into + "'");
+      producers[out].push_back((int)a->queries.size());
     }
     a->queries.push_back(std::move(q));
   }
@@ -427,20 +512,22 @@ void to_sm_values(const sm_app* a, const HostOut& h, const CompiledQuery& cq, st
 // Outputs in the reference's emission order (trigger position, timer phase, listener order, query order,
 // emission order), grouped into one chunk per (trigger, emitting query instance): the collect dump is appended
 // here, the callbacks run later (run_callbacks) outside the app lock.
+bool out_before(const OutRec& x, const OutRec& y) {
+  if (x.pos != y.pos) return x.pos < y.pos;
+  if (x.phase != y.phase) return x.phase < y.phase;
+  if (x.phase == 0) {
+    if (x.time != y.time) return x.time < y.time;
+    int gx = x.create >= 0, gy = y.create >= 0;  // non-partitioned listeners registered first
+    if (gx != gy) return gx < gy;
+    if (x.create != y.create) return x.create < y.create;
+    if (x.query != y.query) return x.query < y.query;
+    return x.sched < y.sched;
+  }
+  return x.query < y.query;
+}
+
 void deliver(sm_app* a, std::vector<HostOut>& outs) {
-  auto key_less = [](const OutRec& x, const OutRec& y) {
-    if (x.pos != y.pos) return x.pos < y.pos;
-    if (x.phase != y.phase) return x.phase < y.phase;
-    if (x.phase == 0) {
-      if (x.time != y.time) return x.time < y.time;
-      int gx = x.create >= 0, gy = y.create >= 0;  // non-partitioned listeners registered first
-      if (gx != gy) return gx < gy;
-      if (x.create != y.create) return x.create < y.create;
-      if (x.query != y.query) return x.query < y.query;
-      return x.sched < y.sched;
-    }
-    return x.query < y.query;
-  };
+  auto key_less = [](const OutRec& x, const OutRec& y) { return out_before(x, y); };
   std::stable_sort(outs.begin(), outs.end(), [&](const HostOut& x, const HostOut& y) {
     if (key_less(x.r, y.r)) return true;
     if (key_less(y.r, x.r)) return false;
@@ -832,18 +919,107 @@ int64_t nfa_device_batch(sm_app* a, int qi, int s, size_t n, const int64_t* d_ts
   return (int64_t)outs.size();
 }
 
-void flush(sm_app* a) {
-  const int64_t N = (int64_t)a->ev_stream.size();
-  if (N == 0) return;
-  // ---- upload the batch
-  std::vector<NfaStream> nst(a->streams.size());
-  for (size_t s = 0; s < a->streams.size(); ++s) {
-    StreamStage& st = a->streams[s];
+// Host side of one batch in arrival order: the staged input (flush), or a chaining level's merged batch.
+struct EvHost {
+  std::vector<int32_t>* stream;
+  std::vector<int64_t>*row, *ts, *clock, *ord, *adv_pos, *adv_clock, *adv_wall;
+};
+
+// Key code (the int64 the key table hashes: key_eval_kernel) of a row's key column, false if it is null.
+bool host_key_code(const StreamStage& st, int col, int64_t row, int64_t* code) {
+  if (st.any_null[col] && st.nulls[col][row]) return false;
+  const uint8_t* b = st.cols[col].data();
+  const int t = col < (int)st.def->attrs.size() ? (int)st.def->attrs[col].type : T_LONG;
+  switch (t) {
+    case T_INT:
+    case T_STRING: { int32_t x; memcpy(&x, b + row * 4, 4); *code = x; break; }
+    case T_LONG: memcpy(code, b + row * 8, 8); break;
+    case T_FLOAT: {
+      float f;
+      memcpy(&f, b + row * 4, 4);
+      double d = f;
+      if (d != d) d = std::numeric_limits<double>::quiet_NaN();
+      memcpy(code, &d, 8);
+      if (d != d) *code = 0x7ff8000000000000ll;
+      break;
+    }
+    case T_DOUBLE: {
+      double d;
+      memcpy(&d, b + row * 8, 8);
+      memcpy(code, &d, 8);
+      if (d != d) *code = 0x7ff8000000000000ll;
+      break;
+    }
+    default: *code = b[row]; break;
+  }
+  return true;
+}
+
+// A batch assembled on the host (chaining levels, broadcast copies): per-stream rows plus the arrival-order
+// arrays. Streams listed in `hidden` get one more column (a LONG key code) than the rows they copy.
+struct BatchBuilder {
+  std::vector<StreamStage> stages;
+  std::vector<int32_t> stream;
+  std::vector<int64_t> row, ts, clock, ord, adv_pos, adv_clock, adv_wall;
+  EvHost ev() { return EvHost{&stream, &row, &ts, &clock, &ord, &adv_pos, &adv_clock, &adv_wall}; }
+  void init(const std::vector<StreamStage>& like, const std::vector<int>& hidden = {}) {
+    stages.resize(like.size());
+    for (size_t s = 0; s < like.size(); ++s) {
+      StreamStage& d = stages[s];
+      d.def = like[s].def;
+      size_t nc = like[s].cols.size();
+      if (std::find(hidden.begin(), hidden.end(), (int)s) != hidden.end()) ++nc;
+      d.cols.resize(nc);
+      d.nulls.resize(nc);
+      d.any_null.assign(nc, false);
+      d.dcols.resize(nc);
+      d.dnulls.resize(nc);
+    }
+  }
+  static int width(const StreamStage& st, int k) {
+    return k < (int)st.def->attrs.size() ? width_of((int)st.def->attrs[k].type) : 8;
+  }
+  // a new event record; its row (if any) is appended with put_bytes / copy_row
+  int64_t put(int32_t s, int64_t t, int64_t clk, int64_t o) {
+    const int64_t pos = (int64_t)stream.size();
+    stream.push_back(s);
+    ts.push_back(t);
+    clock.push_back(clk);
+    ord.push_back(o);
+    if (s < 0) {
+      row.push_back(-1);
+    } else {
+      StreamStage& d = stages[s];
+      row.push_back(d.rows++);
+      d.row_pos.push_back(pos);
+    }
+    return pos;
+  }
+  void put_bytes(int s, size_t k, const uint8_t* b, int w, bool nul) {
+    StreamStage& d = stages[s];
+    d.cols[k].insert(d.cols[k].end(), b, b + w);
+    d.nulls[k].push_back(nul ? 1 : 0);
+    if (nul) d.any_null[k] = true;
+  }
+  void copy_row(int s, const StreamStage& src, int64_t r) {
+    for (size_t k = 0; k < src.cols.size(); ++k) {
+      const int w = width(src, (int)k);
+      put_bytes(s, k, src.cols[k].data() + r * w, w, src.any_null[k] && src.nulls[k][r]);
+    }
+  }
+};
+
+// Upload a batch for the query kernels; the returned view is valid until the next upload.
+EvArrays upload_batch(sm_app* a, std::vector<StreamStage>& stages, const EvHost& e) {
+  const int64_t N = (int64_t)e.stream->size();
+  std::vector<NfaStream> nst(stages.size());
+  for (size_t s = 0; s < stages.size(); ++s) {
+    StreamStage& st = stages[s];
     NfaStream& d = nst[s];
     memset(&d, 0, sizeof(d));
-    d.nattr = (int)st.def->attrs.size();
+    d.nattr = (int)st.cols.size();  // an extra key column included
     for (int k = 0; k < d.nattr; ++k) {
-      d.types[k] = (int)st.def->attrs[k].type;
+      d.types[k] = k < (int)st.def->attrs.size() ? (int)st.def->attrs[k].type : T_LONG;
       upload(a, st.dcols[k], st.cols[k]);
       d.cols[k] = st.dcols[k].p;
       if (st.any_null[k]) {
@@ -854,31 +1030,339 @@ void flush(sm_app* a) {
     upload(a, st.drow_pos, st.row_pos);
   }
   upload(a, a->d_streams, nst);
-  upload(a, a->d_ev_stream, a->ev_stream);
-  upload(a, a->d_ev_row, a->ev_row);
-  upload(a, a->d_ev_ts, a->ev_ts);
-  upload(a, a->d_ev_clock, a->ev_clock);
-  upload(a, a->d_ev_ord, a->ev_ord);
-  upload(a, a->d_adv_pos, a->adv_pos);
-  upload(a, a->d_adv_clock, a->adv_clock);
-  upload(a, a->d_adv_wall, a->adv_wall);
-  {
-    std::vector<int64_t> upto(N);
-    size_t j = 0;
-    for (int64_t p = 0; p < N; ++p) {
-      while (j < a->adv_pos.size() && a->adv_pos[j] <= p) ++j;
-      upto[p] = (int64_t)j;
-    }
-    upload(a, a->d_adv_upto, upto);
+  upload(a, a->d_ev_stream, *e.stream);
+  upload(a, a->d_ev_row, *e.row);
+  upload(a, a->d_ev_ts, *e.ts);
+  upload(a, a->d_ev_clock, *e.clock);
+  upload(a, a->d_ev_ord, *e.ord);
+  upload(a, a->d_adv_pos, *e.adv_pos);
+  upload(a, a->d_adv_clock, *e.adv_clock);
+  upload(a, a->d_adv_wall, *e.adv_wall);
+  std::vector<int64_t> upto(N);
+  size_t j = 0;
+  for (int64_t p = 0; p < N; ++p) {
+    while (j < e.adv_pos->size() && (*e.adv_pos)[j] <= p) ++j;
+    upto[p] = (int64_t)j;
   }
+  upload(a, a->d_adv_upto, upto);
+  SM_HIP(hipStreamSynchronize(a->stream));
   a->d_err.ensure(16);
   a->d_count.ensure(16);
   ensure_scratch(a, batch_scratch(a, N));
+  return EvArrays{(const int32_t*)a->d_ev_stream.p, (const int64_t*)a->d_ev_row.p, (const int64_t*)a->d_ev_ts.p,
+                  (const int64_t*)a->d_ev_clock.p, (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p,
+                  (const int64_t*)a->d_adv_pos.p, (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p,
+                  (const int64_t*)a->d_adv_upto.p, (int64_t)e.adv_pos->size(), a->clock_batch_in};
+}
+
+// Instances of partition pi in creation order after the events of a batch: `keys` / `kset` start as the
+// instances before the batch; each keyed event (a key column that is not null) of a new key appends one.
+// at[p] = instances existing when position p is delivered (its own instance included).
+void walk_instances(const sm_app* a, int pi, const std::vector<StreamStage>& stages, const EvHost& e,
+                    std::vector<int64_t>& keys, std::unordered_set<int64_t>& kset, std::vector<int64_t>* at) {
+  const CompiledPartition& cp = a->parts[pi];
+  const std::vector<int>& bc = a->part_bcast[pi];
+  const int64_t N = (int64_t)e.stream->size();
+  if (at) at->resize(N);
+  for (int64_t p = 0; p < N; ++p) {
+    const int s = (*e.stream)[p];
+    if (s >= 0 && a->ast.streams[s].id[0] != '#' && std::find(bc.begin(), bc.end(), s) == bc.end()) {
+      const auto it = std::find(cp.streams.begin(), cp.streams.end(), s);
+      if (it != cp.streams.end()) {
+        int64_t code;
+        if (host_key_code(stages[s], cp.key_code[it - cp.streams.begin()][0].a, (*e.row)[p], &code) &&
+            kset.insert(code).second)
+          keys.push_back(code);
+      }
+    }
+    if (at) (*at)[p] = (int64_t)keys.size();
+  }
+}
+
+// A query reading a stream its partition does not key, over a copy of the batch in which each such event is
+// repeated once per instance existing at that point, in creation order (the reference iterates a
+// ConcurrentHashMap of the instances' junctions; with one instance the orders agree), the copy's extra column
+// holding the instance's key code. Its outputs move back to the original event's position; an output of the
+// k-th copy ranks after those of copies < k (seq).
+void run_bcast_query(sm_app* a, int qi, std::vector<StreamStage>& stages, const EvHost& e, std::vector<HostOut>& outs) {
+  QueryRt& q = *a->queries[qi];
+  const int pi = q.pidx;
+  const std::vector<int>& bc = a->part_bcast[pi];
+  std::vector<int64_t> keys = a->part_keys[pi];
+  std::unordered_set<int64_t> kset = a->part_key_set[pi];
+  std::vector<int64_t> at;
+  walk_instances(a, pi, stages, e, keys, kset, &at);
+  BatchBuilder b;
+  b.init(stages, bc);
+  const int64_t N = (int64_t)e.stream->size();
+  std::vector<int64_t> map, rank;
+  std::vector<int64_t> newpos(N);
+  for (int64_t p = 0; p < N; ++p) {
+    const int s = (*e.stream)[p];
+    const bool rep = s >= 0 && std::find(bc.begin(), bc.end(), s) != bc.end();
+    const int64_t copies = rep ? at[p] : 1;
+    newpos[p] = (int64_t)b.stream.size();
+    for (int64_t k = 0; k < copies; ++k) {
+      b.put(s, (*e.ts)[p], (*e.clock)[p], (*e.ord)[p]);
+      map.push_back(p);
+      rank.push_back(rep ? k : -1);
+      if (s < 0) continue;
+      b.copy_row(s, stages[s], (*e.row)[p]);
+      if (rep) b.put_bytes(s, stages[s].cols.size(), (const uint8_t*)&keys[k], 8, false);
+    }
+  }
+  for (size_t k = 0; k < e.adv_pos->size(); ++k) {
+    b.adv_pos.push_back(newpos[(*e.adv_pos)[k]]);
+    b.adv_clock.push_back((*e.adv_clock)[k]);
+    b.adv_wall.push_back((*e.adv_wall)[k]);
+  }
+  const EvArrays ev = upload_batch(a, b.stages, b.ev());
+  const size_t first = outs.size();
+  a->sc.used = 0;
+  run_pattern_query(a, qi, ev, (int64_t)b.stream.size(), outs, a->stream);
+  q.nfa_used = true;
+  std::vector<int64_t> slot_keys(q.keys.nslots);
+  if (!slot_keys.empty())
+    SM_HIP(hipMemcpy(slot_keys.data(), q.keys.slot_keys, slot_keys.size() * 8, hipMemcpyDeviceToHost));
+  for (size_t i = first; i < outs.size(); ++i) {
+    HostOut& h = outs[i];
+    if (h.r.key >= 0 && h.r.key < (int32_t)slot_keys.size()) h.key_code = slot_keys[h.r.key];
+    const int64_t r = rank[h.r.pos];
+    h.r.pos = map[h.r.pos];
+    if (r >= 0) h.r.seq = (int32_t)(r * (1 << 20) + h.r.seq);
+  }
+}
+
+// Upload one batch and run the queries of chaining level `level` over it; their outputs (positions in this
+// batch) are appended to outs. Outputs of a partition query carry their instance's key code (key_code).
+void run_level(sm_app* a, std::vector<StreamStage>& stages, const EvHost& e, int level, std::vector<HostOut>& outs) {
+  const int64_t N = (int64_t)e.stream->size();
+  const EvArrays ev = upload_batch(a, stages, e);
+  for (size_t qi = 0; qi < a->queries.size(); ++qi) {
+    QueryRt& q = *a->queries[qi];
+    if (q.level != level || q.bcast) continue;
+    const DQuery& h = q.cq.hdr;
+    a->sc.used = 0;
+    size_t stride = sizeof(OutRec) + h.nsel * sizeof(DVal) + h.nrefs * sizeof(int64_t);
+    const size_t first = outs.size();
+    if (h.kind == 0) {
+      StreamStage& st = stages[h.stream];
+      if (st.rows == 0) continue;
+      const NfaStream* sd = (const NfaStream*)a->d_streams.p + h.stream;
+      int64_t* rows = (int64_t*)a->sc.take(st.rows * 8);
+      const char* blob = (const char*)q.blob.p;
+      const DQuery* hd = &h;
+      int64_t nm = filter_rows(sd, st.rows, (const Instr*)(blob + hd->off_code) + h.filt_off, h.filt_len,
+                               (const DVal*)(blob + hd->off_const), rows, a->sc, a->stream);
+      q.out.ensure(std::max<size_t>((size_t)nm * stride, 16));
+      project_rows(sd, rows, nm, (const int64_t*)st.drow_pos.p, (const int64_t*)a->d_ev_ts.p, (const int64_t*)a->d_ev_ord.p, blob,
+                   h.query_order, (char*)q.out.p, (uint32_t)stride, a->stream);
+      read_outputs(a, (int)qi, q.out.p, nm, outs);
+      if (q.part) {
+        // PartitionStreamReceiver drops an event whose key is null before any instance sees it
+        const CompiledPartition& cp = *q.part;
+        const int k = (int)(std::find(cp.streams.begin(), cp.streams.end(), h.stream) - cp.streams.begin());
+        const int col = cp.key_code[k][0].a;
+        size_t w = first;
+        for (size_t i = first; i < outs.size(); ++i) {
+          int64_t code;
+          if (!host_key_code(st, col, (*e.row)[outs[i].r.pos], &code)) continue;
+          outs[i].key_code = code;
+          if (w != i) outs[w] = std::move(outs[i]);
+          ++w;
+        }
+        outs.resize(w);
+      }
+      continue;
+    }
+    run_pattern_query(a, (int)qi, ev, N, outs, a->stream);
+    for (int s : q.cq.streams)
+      if (stages[s].rows > 0) q.nfa_used = true;
+    if (q.part && outs.size() > first) {  // instance key of each output (its lane's key slot)
+      std::vector<int64_t> keys(q.keys.nslots);
+      if (!keys.empty())
+        SM_HIP(hipMemcpy(keys.data(), q.keys.slot_keys, keys.size() * 8, hipMemcpyDeviceToHost));
+      for (size_t i = first; i < outs.size(); ++i)
+        if (outs[i].r.key >= 0 && outs[i].r.key < (int32_t)keys.size()) outs[i].key_code = keys[outs[i].r.key];
+    }
+  }
+  for (size_t qi = 0; qi < a->queries.size(); ++qi)  // their batches replace the uploaded one: last
+    if (a->queries[qi]->level == level && a->queries[qi]->bcast) run_bcast_query(a, (int)qi, stages, e, outs);
+}
+
+bool out_before(const OutRec& x, const OutRec& y);
+
+// Query chaining (InsertIntoStreamCallback → StreamJunction.sendEvent → the reading queries, depth first, before
+// the junction moves on to its next receiver). Every event and output gets an order key:
+//   input event at position p: (p, 2); an output: its trigger's key (an input event's: (p)), then
+//   (phase 1: 1, query, seq | timer phase 0: 0, time, listener group, create, query, scheduler, seq);
+//   an event a query inserts into a stream later queries read: the key of that output.
+// Level L runs over the previous level's batch merged with the events level L-1's queries inserted, in key
+// order: an inserted event precedes its root input event, because every query reading it was defined (and so
+// subscribed to that event's stream) after the query inserting it; it keeps the trigger's playback clock
+// (sendEvent does not advance it) and has no arrival ordinal. Outputs are delivered in key order.
+void run_chained(sm_app* a, std::vector<HostOut>& outs) {
+  using Key = std::vector<int64_t>;
+  struct Level {
+    std::vector<StreamStage> stages;
+    std::vector<int32_t> stream;
+    std::vector<int64_t> row, ts, clock, ord, adv_pos, adv_clock, adv_wall;
+    std::vector<Key> key;
+    EvHost ev() { return EvHost{&stream, &row, &ts, &clock, &ord, &adv_pos, &adv_clock, &adv_wall}; }
+  };
+  auto out_key = [](const Key& trig, const OutRec& r) {
+    Key k = trig.size() == 2 && trig[1] == 2 ? Key{trig[0]} : trig;
+    if (r.phase == 1) k.insert(k.end(), {1, r.query, r.seq});
+    else k.insert(k.end(), {0, r.time, r.create >= 0 ? 1 : 0, r.create, r.query, r.sched, r.seq});
+    return k;
+  };
+  std::vector<std::unique_ptr<Level>> lv;
+  std::vector<StreamStage>* pst = &a->streams;
+  EvHost pe{&a->ev_stream, &a->ev_row, &a->ev_ts, &a->ev_clock, &a->ev_ord, &a->adv_pos, &a->adv_clock, &a->adv_wall};
+  std::vector<Key> pkey(a->ev_stream.size());
+  for (size_t p = 0; p < pkey.size(); ++p) pkey[p] = Key{(int64_t)p, 2};
+  std::vector<Key> okey(outs.size());
+  size_t done = 0;  // outputs whose key is known
+  auto key_outs = [&](const std::vector<Key>& ek) {
+    okey.resize(outs.size());
+    for (; done < outs.size(); ++done) okey[done] = out_key(ek[outs[done].r.pos], outs[done].r);
+  };
+  key_outs(pkey);
+  size_t lstart = 0;
+  for (int L = 1; L <= a->max_level; ++L) {
+    const size_t lend = outs.size();
+    // this level's new events: outputs of level L-1 into streams a query reads
+    std::vector<size_t> der;
+    for (size_t i = lstart; i < lend; ++i) {
+      const int s = stream_index(a->ast, a->queries[outs[i].qidx]->cq.insert_into);
+      if (s >= 0 && a->stream_fed[s]) der.push_back(i);
+    }
+    lstart = lend;
+    std::stable_sort(der.begin(), der.end(), [&](size_t x, size_t y) { return okey[x] < okey[y]; });
+    auto nl = std::make_unique<Level>();
+    nl->stages.resize(pst->size());
+    for (size_t s = 0; s < pst->size(); ++s) {
+      StreamStage& d = nl->stages[s];
+      const StreamStage& o = (*pst)[s];
+      d.def = o.def;
+      d.cols.resize(o.cols.size());
+      d.nulls.resize(o.cols.size());
+      d.any_null.assign(o.cols.size(), false);
+      d.dcols.resize(o.cols.size());
+      d.dnulls.resize(o.cols.size());
+    }
+    const int64_t Np = (int64_t)pe.stream->size();
+    std::vector<int64_t> map(Np);
+    auto col_width = [](const StreamStage& st, int k) {
+      return k < (int)st.def->attrs.size() ? width_of((int)st.def->attrs[k].type) : 8;
+    };
+    auto put_event = [&](int32_t s, int64_t ts, int64_t clk, int64_t ord, const Key& k) {
+      nl->stream.push_back(s);
+      nl->ts.push_back(ts);
+      nl->clock.push_back(clk);
+      nl->ord.push_back(ord);
+      nl->key.push_back(k);
+      if (s < 0) {
+        nl->row.push_back(-1);
+        return;
+      }
+      StreamStage& d = nl->stages[s];
+      nl->row.push_back(d.rows);
+      d.row_pos.push_back((int64_t)nl->stream.size() - 1);
+      ++d.rows;
+    };
+    auto copy_event = [&](int64_t p) {
+      const int32_t s = (*pe.stream)[p];
+      map[p] = (int64_t)nl->stream.size();
+      const int64_t r = (*pe.row)[p];
+      put_event(s, (*pe.ts)[p], (*pe.clock)[p], (*pe.ord)[p], pkey[p]);
+      if (s < 0) return;
+      StreamStage& d = nl->stages[s];
+      const StreamStage& o = (*pst)[s];
+      for (size_t k = 0; k < o.cols.size(); ++k) {
+        const int w = col_width(o, (int)k);
+        d.cols[k].insert(d.cols[k].end(), o.cols[k].begin() + r * w, o.cols[k].begin() + (r + 1) * w);
+        const uint8_t nul = o.any_null[k] ? o.nulls[k][r] : 0;
+        d.nulls[k].push_back(nul);
+        if (nul) d.any_null[k] = true;
+      }
+    };
+    auto derived_event = [&](size_t oi) {
+      const HostOut& h = outs[oi];
+      const int s = stream_index(a->ast, a->queries[h.qidx]->cq.insert_into);
+      put_event(s, h.r.ts, (*pe.clock)[h.r.pos], -1, okey[oi]);
+      StreamStage& d = nl->stages[s];
+      const size_t na = d.def->attrs.size();
+      for (size_t k = 0; k < d.cols.size(); ++k) {
+        uint8_t b[8];
+        int w;
+        uint8_t nul = 0;
+        if (k < na) {
+          const int t = (int)d.def->attrs[k].type;
+          w = width_of(t);
+          const DVal& v = h.vals[k];
+          nul = v.null ? 1 : 0;
+          if (t == T_FLOAT) {
+            const float f = (float)v.d;
+            memcpy(b, &f, 4);
+          } else if (t == T_DOUBLE) {
+            memcpy(b, &v.d, 8);
+          } else if (t == T_LONG) {
+            memcpy(b, &v.i, 8);
+          } else if (t == T_BOOL) {
+            b[0] = (uint8_t)(v.i != 0);
+          } else {
+            const int32_t x = (int32_t)v.i;
+            memcpy(b, &x, 4);
+          }
+        } else {  // inner stream: the producing instance's key code
+          w = 8;
+          memcpy(b, &h.key_code, 8);
+        }
+        d.cols[k].insert(d.cols[k].end(), b, b + w);
+        d.nulls[k].push_back(nul);
+        if (nul) d.any_null[k] = true;
+      }
+    };
+    size_t di = 0;
+    for (int64_t p = 0; p < Np; ++p) {
+      while (di < der.size() && okey[der[di]] < pkey[p]) derived_event(der[di++]);
+      copy_event(p);
+    }
+    while (di < der.size()) derived_event(der[di++]);
+    for (size_t k = 0; k < pe.adv_pos->size(); ++k) {
+      nl->adv_pos.push_back(map[(*pe.adv_pos)[k]]);
+      nl->adv_clock.push_back((*pe.adv_clock)[k]);
+      nl->adv_wall.push_back((*pe.adv_wall)[k]);
+    }
+    run_level(a, nl->stages, nl->ev(), L, outs);
+    key_outs(nl->key);
+    pst = &nl->stages;
+    pkey = nl->key;
+    lv.push_back(std::move(nl));
+    pe = lv.back()->ev();
+  }
+  // delivery order: by key; one position per (trigger, query) so that deliver keeps it and groups its chunks
+  std::vector<size_t> ord(outs.size());
+  for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+  std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return okey[x] < okey[y]; });
+  std::vector<HostOut> sorted;
+  sorted.reserve(outs.size());
+  int64_t rank = -1;
+  for (size_t k = 0; k < ord.size(); ++k) {
+    const Key& cur = okey[ord[k]];
+    if (k == 0 || !std::equal(cur.begin(), cur.end() - 1, okey[ord[k - 1]].begin(), okey[ord[k - 1]].end() - 1)) ++rank;
+    sorted.push_back(std::move(outs[ord[k]]));
+    sorted.back().r.pos = rank;
+    sorted.back().r.phase = 1;
+  }
+  outs.swap(sorted);
+}
+
+void flush(sm_app* a) {
+  const int64_t N = (int64_t)a->ev_stream.size();
+  if (N == 0) return;
   std::vector<HostOut> outs;
-  const EvArrays ev{(const int32_t*)a->d_ev_stream.p, (const int64_t*)a->d_ev_row.p, (const int64_t*)a->d_ev_ts.p,
-                    (const int64_t*)a->d_ev_clock.p, (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p,
-                    (const int64_t*)a->d_adv_pos.p, (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p,
-                    (const int64_t*)a->d_adv_upto.p, (int64_t)a->adv_pos.size(), a->clock_batch_in};
   // the batch is consumed whatever happens below: a query that fails half-way leaves the matching state
   // inconsistent (earlier queries advanced, outputs lost), so the app refuses further events until it is restored
   // or reset, instead of running the same events again
@@ -901,30 +1385,13 @@ void flush(sm_app* a) {
     }
   } done{a, N};
   try {
-  for (size_t qi = 0; qi < a->queries.size(); ++qi) {
-    QueryRt& q = *a->queries[qi];
-    const DQuery& h = q.cq.hdr;
-    a->sc.used = 0;
-    size_t stride = sizeof(OutRec) + h.nsel * sizeof(DVal) + h.nrefs * sizeof(int64_t);
-    if (h.kind == 0) {
-      StreamStage& st = a->streams[h.stream];
-      if (st.rows == 0) continue;
-      const NfaStream* sd = (const NfaStream*)a->d_streams.p + h.stream;
-      int64_t* rows = (int64_t*)a->sc.take(st.rows * 8);
-      const char* blob = (const char*)q.blob.p;
-      const DQuery* hd = &h;
-      int64_t nm = filter_rows(sd, st.rows, (const Instr*)(blob + hd->off_code) + h.filt_off, h.filt_len,
-                               (const DVal*)(blob + hd->off_const), rows, a->sc, a->stream);
-      q.out.ensure(std::max<size_t>((size_t)nm * stride, 16));
-      project_rows(sd, rows, nm, (const int64_t*)st.drow_pos.p, (const int64_t*)a->d_ev_ts.p, (const int64_t*)a->d_ev_ord.p, blob,
-                   h.query_order, (char*)q.out.p, (uint32_t)stride, a->stream);
-      read_outputs(a, (int)qi, q.out.p, nm, outs);
-      continue;
-    }
-    run_pattern_query(a, (int)qi, ev, N, outs, a->stream);
-    for (int s : q.cq.streams)
-      if (a->streams[s].rows > 0) q.nfa_used = true;
-  }
+    const EvHost e0{&a->ev_stream, &a->ev_row, &a->ev_ts, &a->ev_clock, &a->ev_ord, &a->adv_pos, &a->adv_clock,
+                    &a->adv_wall};
+    run_level(a, a->streams, e0, 0, outs);
+    if (a->max_level > 0) run_chained(a, outs);
+    for (size_t pi = 0; pi < a->part_bcast.size(); ++pi)  // instances this batch created, for later broadcasts
+      if (!a->part_bcast[pi].empty())
+        walk_instances(a, (int)pi, a->streams, e0, a->part_keys[pi], a->part_key_set[pi], nullptr);
   } catch (const std::exception& e) {
     a->failed = true;
     a->failed_why = std::string("a batch failed half-way (") + e.what() +
@@ -1023,7 +1490,7 @@ using namespace sm;
 
 // snapshot encoding helpers (sm_app_snapshot / sm_app_restore)
 namespace {
-constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '2'};
+constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '3'};
 
 struct SnapWriter {
   std::vector<uint8_t> b;
@@ -1126,6 +1593,8 @@ int sm_app_input_handler(sm_app* a, const char* stream_id, sm_input** out) {
   return guarded([&] {
     int s = stream_index(a->ast, stream_id ? stream_id : "");
     if (s < 0) throw sql::ValidationError(std::string("stream '") + (stream_id ? stream_id : "") + "' is not defined");
+    if (a->ast.streams[s].id[0] == '#')
+      throw sql::ValidationError(std::string("inner stream '") + stream_id + "' is only visible inside its partition");
     auto in = std::make_unique<sm_input>();
     in->app = a;
     in->stream = s;
@@ -1296,6 +1765,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       a->failed = false;
       a->failed_why.clear();
       for (auto& q : a->queries) q->nfa_used = q->nfa_mode = false;
+      for (auto& k : a->part_keys) k.clear();
+      for (auto& k : a->part_key_set) k.clear();
       if (value) {  // reset and start again
         a->started = true;
         stage_record(a, NFA_START, -1, a->clock, 0);
@@ -1317,6 +1788,10 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
     int s = stream_index(a->ast, stream_id ? stream_id : "");
     if (s < 0) throw sql::ValidationError("unknown stream");
     flush(a);  // staged host events come first (arrival order)
+    if (a->max_level > 0)
+      throw sql::UnsupportedError("apps whose queries read streams other queries fill run through the host API");
+    for (auto& bc : a->part_bcast)
+      if (!bc.empty()) throw sql::UnsupportedError("partitions reading unkeyed streams run through the host API");
     for (auto& qp : a->queries)
       if (qp->cq.hdr.kind != 0 && !qp->cq.fast_every_within &&
           std::find(qp->cq.streams.begin(), qp->cq.streams.end(), s) != qp->cq.streams.end())
@@ -1445,6 +1920,10 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
   return locked(a, [&] {
     flush(a);
     if (n == 0) return;
+    if (a->max_level > 0)
+      throw sql::UnsupportedError("apps whose queries read streams other queries fill run through the host API");
+    for (auto& bc : a->part_bcast)
+      if (!bc.empty()) throw sql::UnsupportedError("partitions reading unkeyed streams run through the host API");
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
     // every stream a query reads must carry the batch schema (the schema of the first such stream)
     const std::vector<sql::Attribute>* schema = nullptr;
@@ -1542,6 +2021,11 @@ int sm_app_snapshot(sm_app* a, uint8_t* buf, size_t cap, size_t* len) {
       w.put<uint32_t>((uint32_t)str.size());
       w.raw(str.data(), str.size());
     }
+    w.put<uint32_t>((uint32_t)a->part_keys.size());  // partition instances (broadcast targets), creation order
+    for (auto& k : a->part_keys) {
+      w.put<uint64_t>(k.size());
+      w.raw(k.data(), k.size() * 8);
+    }
     w.put<uint32_t>((uint32_t)a->queries.size());
     const size_t heap_words = 2 * (size_t)a->heap_half + 64;
     for (auto& qp : a->queries) {
@@ -1621,6 +2105,12 @@ int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
       if (i >= d.strs.size() || d.strs[i] != a->dict.strs[i])
         throw std::runtime_error("CannotRestoreSiddhiAppStateException: string dictionary mismatch");
     a->dict = d;
+    if (r.get<uint32_t>() != a->part_keys.size()) throw std::runtime_error("CannotRestoreSiddhiAppStateException: plan mismatch");
+    for (size_t pi = 0; pi < a->part_keys.size(); ++pi) {
+      a->part_keys[pi].resize(r.get<uint64_t>());
+      r.raw(a->part_keys[pi].data(), a->part_keys[pi].size() * 8);
+      a->part_key_set[pi] = std::unordered_set<int64_t>(a->part_keys[pi].begin(), a->part_keys[pi].end());
+    }
     if (r.get<uint32_t>() != a->queries.size())
       throw std::runtime_error("CannotRestoreSiddhiAppStateException: query count mismatch");
     for (auto& qp : a->queries)

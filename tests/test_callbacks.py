@@ -77,7 +77,8 @@ def _product():
 
 def _values(outs):
     """(stream events as (ts, values), query events flattened per query as (ts, values))."""
-    st = {k: [(e[0], e[1]) for e in v] for k, v in outs["streams"].items() if v}
+    # inner streams ('#name') are visible inside their partition only: no callback can subscribe to them
+    st = {k: [(e[0], e[1]) for e in v] for k, v in outs["streams"].items() if v and not k.startswith("#")}
     qs = {k: [ev for call in v for ev in call[1]] for k, v in outs["queries"].items() if v}
     return st, qs
 
