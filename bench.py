@@ -49,6 +49,18 @@ APP5 = ("@app:playback " + " ".join(f"define stream {x} (symbol int, price doubl
         "@info(name='q') from every e1=A, e2=B[price>e1.price]<2:5>, (e3=C or e4=D), not E for 5 sec "
         "select e1.timestamp as a, e2[0].timestamp as b0, e2[last].timestamp as bl, e3.timestamp as c, "
         "e4.timestamp as d insert into Out; end;")
+# Config 5 variant that emits: the same streams and conditions as a pattern ('->'), so that
+# partials survive the interleaving (the sequence form emits nothing at this scale: CountPostStateProcessor
+# re-adds a sequence partial only once n >= min, StateStreamRuntime resets it before the second B)
+VARIANTS5 = {
+    "pattern_count_not5s": "every e1=A -> e2=B[price>e1.price]<2:5> -> (e3=C or e4=D) -> not E for 5 sec",
+}
+
+
+def app5_variant(body):
+    return APP5.replace("every e1=A, e2=B[price>e1.price]<2:5>, (e3=C or e4=D), not E for 5 sec", body)
+
+
 HBM_PEAK = 8.0e12
 GAMMA = 0x9E3779B97F4A7C15
 METRIC = "input events/sec + % HBM peak, partitioned pattern query, 1/2/4/8 MI355X"
@@ -341,8 +353,20 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stack", type=int, default=0, choices=(0, 1, 2),
                     help="device-batch pipeline for configs 3/4: 0 automatic, 1 bucket stack, 2 sort / walk")
+    ap.add_argument("--variant", default=None, choices=sorted(VARIANTS5),
+                    help="config 5: the named emitting variant of the query")
+    ap.add_argument("--heap-words", type=int, default=None,
+                    help="NFA per-key partial-match arena (words per semispace; option heap_words)")
     args = ap.parse_args()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.variant:
+        if args.config != 5:
+            ap.error("--variant applies to config 5")
+        cfg["app"] = app5_variant(VARIANTS5[args.variant])
+        cfg["workload"] = f"config 5 variant {args.variant}: @app:playback partition with (symbol of A..E) " \
+                          f"{VARIANTS5[args.variant]}"
+        # a pattern keeps every A's partial until it completes (no `within`): a larger per-key arena
+        cfg["options"] = {"heap_words": 4096}
 
     import torch
     import torch.distributed as dist
@@ -379,7 +403,12 @@ def main():
     out_local = [0]
     torch.cuda.synchronize()
 
-    app = ProductApp(cfg["app"], fast_stack=args.stack)
+    opts = dict(cfg.get("options", {}))
+    if args.heap_words:
+        opts["heap_words"] = args.heap_words
+    app = ProductApp(cfg["app"], fast_stack=args.stack, **opts)
+    # outputs are counted (the reference benchmark counts them in its callback), not collected as JSON
+    app.set_collect(False)
     stream = torch.cuda.current_stream(dev)
     hip_stream = ctypes.c_void_p(stream.cuda_stream)
     n_local = [hi - lo]

@@ -43,6 +43,12 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
 // out[i] = start + i
 void iota_i64(int64_t* out, int64_t n, int64_t start, hipStream_t s);
 
+// One query's n output records (stride bytes each, OutRec first) in delivery order (runtime.cpp deliver): by
+// (pos, phase), then for timer-phase records (time, listener group, key creation ordinal); a lane's own records
+// keep their emission order (the sorts are stable and a lane's slots ascend). Returns the ordered copy (scratch).
+const char* order_outputs(const char* recs, int64_t n, uint32_t stride, const int64_t* ev_clock, Scratch& sc,
+                          hipStream_t s);
+
 int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const int64_t* ts, const int64_t* ord_in,
                           int64_t ord_base, bool playback, int64_t clock_in, int64_t* ev_row, int64_t* ev_ord,
                           int64_t* ev_clock, int64_t* adv_pos, int64_t* adv_clock, int64_t* adv_wall,

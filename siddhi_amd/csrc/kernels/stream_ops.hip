@@ -744,6 +744,78 @@ void iota_i64(int64_t* out, int64_t n, int64_t start, hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(iota_kernel, grid_for(n), dim3(256), 0, s, out, n, start);
 }
 
+namespace {
+// sort keys of each record: key creation ordinal + 1 (0 = non-partitioned listener, first), time (sign-flipped),
+// (pos << 1) | phase; flag[0] |= 1 when a timer record's time differs from its position's clock (wall-clock
+// emulation: several steps at one advance point), which makes the time pass necessary
+__global__ void out_keys_kernel(const char* __restrict__ recs, int64_t n, uint32_t stride,
+                                const int64_t* __restrict__ ev_clock, uint64_t* __restrict__ kc,
+                                uint64_t* __restrict__ kt, uint64_t* __restrict__ kp, uint32_t* __restrict__ idx,
+                                uint32_t* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const OutRec& r = *(const OutRec*)(recs + (size_t)i * stride);
+  kc[i] = (uint64_t)(r.create + 1);
+  kt[i] = (uint64_t)r.time ^ 0x8000000000000000ull;
+  kp[i] = ((uint64_t)r.pos << 1) | (uint64_t)(r.phase & 1);
+  idx[i] = (uint32_t)i;
+  if (r.phase == 0 && r.time != ev_clock[r.pos]) atomicOr(flag, 1u);
+}
+
+__global__ void gather_key_kernel(const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx, int64_t n,
+                                  uint64_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+
+// a thread per 8-byte word of the ordered copy
+__global__ void gather_records_kernel(const char* __restrict__ recs, const uint32_t* __restrict__ idx, int64_t n,
+                                      uint32_t words, char* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * words) return;
+  const int64_t i = t / words, w = t - i * words;
+  ((uint64_t*)out)[i * words + w] = ((const uint64_t*)recs)[(int64_t)idx[i] * words + w];
+}
+
+}  // namespace
+
+const char* order_outputs(const char* recs, int64_t n, uint32_t stride, const int64_t* ev_clock, Scratch& sc,
+                          hipStream_t s) {
+  if (n >= (int64_t)UINT32_MAX) throw std::runtime_error("too many output records to order");
+  if (stride % 8) throw std::logic_error("output record stride");
+  uint64_t* kc = (uint64_t*)sc.take((size_t)n * 8);
+  uint64_t* kt = (uint64_t*)sc.take((size_t)n * 8);
+  uint64_t* kp = (uint64_t*)sc.take((size_t)n * 8);
+  uint64_t* k2 = (uint64_t*)sc.take((size_t)n * 8);
+  uint32_t* idx = (uint32_t*)sc.take((size_t)n * 4);
+  uint32_t* idx2 = (uint32_t*)sc.take((size_t)n * 4);
+  uint32_t* flag = (uint32_t*)sc.take(4);
+  char* out = (char*)sc.take((size_t)n * stride);
+  SM_HIP(hipMemsetAsync(flag, 0, 4, s));
+  hipLaunchKernelGGL(out_keys_kernel, grid_for(n), dim3(256), 0, s, recs, n, stride, ev_clock, kc, kt, kp, idx, flag);
+  uint32_t hflag = 0;
+  SM_HIP(hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  // least significant first: creation ordinal (40 bits cover any batch history), time (if it varies), (pos, phase)
+  uint32_t* cur = idx;
+  uint32_t* alt = idx2;
+  auto pass = [&](uint64_t* keys, int bits, bool gathered) {
+    uint64_t* k = keys;
+    if (gathered) {  // the keys in the current order
+      hipLaunchKernelGGL(gather_key_kernel, grid_for(n), dim3(256), 0, s, keys, cur, n, k2);
+      k = k2;
+    }
+    uint64_t* kalt = k == k2 ? keys : k2;
+    if (radix_sort_pairs<uint64_t>(k, kalt, cur, alt, (size_t)n, 0, bits, sc, s)) std::swap(cur, alt);
+  };
+  pass(kc, 41, false);
+  if (hflag) pass(kt, 64, true);
+  pass(kp, 33, true);  // positions < 2^32 (build_event_index)
+  const uint32_t words = stride / 8;
+  hipLaunchKernelGGL(gather_records_kernel, grid_for(n * words), dim3(256), 0, s, recs, cur, n, words, out);
+  return out;
+}
+
 int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const int64_t* ts, const int64_t* ord_in,
                           int64_t ord_base, bool playback, int64_t clock_in, int64_t* ev_row, int64_t* ev_ord,
                           int64_t* ev_clock, int64_t* adv_pos, int64_t* adv_clock, int64_t* adv_wall,

@@ -99,10 +99,13 @@ struct StreamStage {
   }
 };
 
+// One output record read back from the device. Its selected values and reference ordinals stay in the record
+// buffer it was read from (sm_app::out_arena, alive until the outputs are delivered): no allocation per output.
 struct HostOut {
   OutRec r;
-  std::vector<DVal> vals;
-  std::vector<int64_t> refs;
+  const DVal* vals = nullptr;
+  const int64_t* refs = nullptr;
+  int nvals = 0, nrefs = 0;
   int qidx;
   int64_t e1 = -1, e2 = -1;  // closed-form queries: ordinals of the match's two events (hidden references)
   int64_t key_code = 0;      // partition queries: the instance's key code (an inner stream's routing key)
@@ -153,6 +156,7 @@ struct QueryRt {
   // device batch results
   DBuf dev_pairs;
   int64_t dev_n = 0;
+  int64_t n_out = 0;         // output records read back since the counter was last taken
   FastState fast;            // v2 kernels' persistent look-back state
   FastCarry carry;           // open partials carried across device batches (closed-form queries)
   bool nfa_used = false;     // host-API batches ran through the NFA kernel (partials live in ks / heap)
@@ -244,6 +248,34 @@ struct sm_app {
   bool collect = false;
   std::map<std::string, std::vector<std::string>> collected_streams;  // JSON fragments
   std::map<std::string, std::vector<std::string>> collected_queries;
+  // output record buffers of the current call (HostOut points into them): pinned host memory, reused across calls
+  struct Pinned {
+    char* p = nullptr;
+    size_t cap = 0;
+  };
+  struct OutArena {
+    std::vector<Pinned> bufs;
+    size_t next = 0;  // buffers in use by the current call
+    char* take(size_t bytes) {
+      if (next == bufs.size()) bufs.emplace_back();
+      Pinned& b = bufs[next++];
+      if (b.cap < bytes) {
+        if (b.p) SM_HIP(hipHostFree(b.p));
+        b.p = nullptr;
+        b.cap = std::max(bytes, b.cap * 2);
+        SM_HIP(hipHostMalloc((void**)&b.p, b.cap, hipHostMallocDefault));
+      }
+      return b.p;
+    }
+    void clear() { next = 0; }
+    ~OutArena() {
+      for (auto& b : bufs)
+        if (b.p) (void)hipHostFree(b.p);
+    }
+  } out_arena;
+  // no JSON dump, no callback, no chaining: outputs are copied to the host and counted, no HostOut is built
+  bool outputs_unconsumed() const;
+  bool need_outs = false;  // set while a caller reads the output records itself (nfa_device_batch)
   hipStream_t stream = nullptr;
   sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_ev_ord, d_adv_pos, d_adv_clock, d_adv_wall, d_adv_upto, d_streams,
       d_err, d_count,
@@ -490,8 +522,8 @@ void json_val(std::ostringstream& o, const sm_app* a, const DVal& v, int t) {
 }
 
 void to_sm_values(const sm_app* a, const HostOut& h, const CompiledQuery& cq, std::vector<sm_value>& out) {
-  out.resize(h.vals.size());
-  for (size_t k = 0; k < h.vals.size(); ++k) {
+  out.resize(h.nvals);
+  for (int k = 0; k < h.nvals; ++k) {
     sm_value& v = out[k];
     int t = cq.sel_types[k];
     v.type = t;
@@ -512,6 +544,23 @@ void to_sm_values(const sm_app* a, const HostOut& h, const CompiledQuery& cq, st
 // Outputs in the reference's emission order (trigger position, timer phase, listener order, query order,
 // emission order), grouped into one chunk per (trigger, emitting query instance): the collect dump is appended
 // here, the callbacks run later (run_callbacks) outside the app lock.
+}  // namespace
+}  // namespace sm
+
+bool sm_app::outputs_unconsumed() const {
+  if (collect || need_outs || max_level > 0) return false;
+  for (auto& q : queries) {
+    auto it = stream_cbs.find(q->cq.insert_into);
+    if (it != stream_cbs.end() && !it->second.empty()) return false;
+    auto qt = query_cbs.find(q->cq.name);
+    if (q->cq.partition < 0 && qt != query_cbs.end() && !qt->second.empty()) return false;
+  }
+  return true;
+}
+
+namespace sm {
+namespace {
+
 bool out_before(const OutRec& x, const OutRec& y) {
   if (x.pos != y.pos) return x.pos < y.pos;
   if (x.phase != y.phase) return x.phase < y.phase;
@@ -527,12 +576,18 @@ bool out_before(const OutRec& x, const OutRec& y) {
 }
 
 void deliver(sm_app* a, std::vector<HostOut>& outs) {
+  if (a->outputs_unconsumed()) {  // nothing to hand out: the outputs were only counted
+    a->out_arena.clear();
+    return;
+  }
   auto key_less = [](const OutRec& x, const OutRec& y) { return out_before(x, y); };
-  std::stable_sort(outs.begin(), outs.end(), [&](const HostOut& x, const HostOut& y) {
+  const auto before = [&](const HostOut& x, const HostOut& y) {
     if (key_less(x.r, y.r)) return true;
     if (key_less(y.r, x.r)) return false;
     return x.r.seq < y.r.seq;
-  });
+  };
+  // the device orders one query's records already (order_outputs); several queries' outputs still interleave here
+  if (!std::is_sorted(outs.begin(), outs.end(), before)) std::stable_sort(outs.begin(), outs.end(), before);
   size_t i = 0;
   while (i < outs.size()) {
     size_t j = i + 1;  // the chunk: same trigger and emitting query instance
@@ -563,12 +618,12 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
       if (a->collect) {
         std::ostringstream o;
         o << "[" << h.r.ts << ",[";
-        for (size_t q = 0; q < h.vals.size(); ++q) {
+        for (int q = 0; q < h.nvals; ++q) {
           if (q) o << ",";
           json_val(o, a, h.vals[q], cq.sel_types[q]);
         }
         o << "],[";
-        for (size_t q = 0; q < h.refs.size(); ++q) {
+        for (int q = 0; q < h.nrefs; ++q) {
           if (q) o << ",";
           o << h.refs[q];
         }
@@ -577,7 +632,7 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
         if (cq.partition < 0) {
           std::ostringstream qo;
           qo << "[" << h.r.ts << ",[[";
-          for (size_t q = 0; q < h.vals.size(); ++q) {
+          for (int q = 0; q < h.nvals; ++q) {
             if (q) qo << ",";
             json_val(qo, a, h.vals[q], cq.sel_types[q]);
           }
@@ -602,6 +657,7 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
     }
     i = j;
   }
+  a->out_arena.clear();  // the chunks own copies of everything they hand out
 }
 
 // Callbacks of the prepared chunks, on the calling thread, with the app lock released: a callback may send into
@@ -622,23 +678,27 @@ void read_outputs(sm_app* a, int qidx, const void* dev, int64_t n, std::vector<H
   if (n <= 0) return;
   const CompiledQuery& cq = a->queries[qidx]->cq;
   size_t stride = sizeof(OutRec) + cq.hdr.nsel * sizeof(DVal) + cq.hdr.nrefs * sizeof(int64_t);
-  std::vector<char> host((size_t)n * stride);
-  SM_HIP(hipMemcpyAsync(host.data(), dev, host.size(), hipMemcpyDeviceToHost, a->stream));
+  char* host = a->out_arena.take((size_t)n * stride);
+  SM_HIP(hipMemcpyAsync(host, dev, (size_t)n * stride, hipMemcpyDeviceToHost, a->stream));
   SM_HIP(hipStreamSynchronize(a->stream));
+  a->queries[qidx]->n_out += n;
+  if (a->outputs_unconsumed()) return;
+  outs.reserve(outs.size() + (size_t)n);
   for (int64_t k = 0; k < n; ++k) {
-    const char* b = host.data() + (size_t)k * stride;
+    const char* b = host + (size_t)k * stride;
     HostOut h;
     memcpy(&h.r, b, sizeof(OutRec));
-    h.vals.resize(cq.hdr.nsel);
-    memcpy(h.vals.data(), b + sizeof(OutRec), cq.hdr.nsel * sizeof(DVal));
+    h.vals = (const DVal*)(b + sizeof(OutRec));
+    h.nvals = cq.hdr.nsel;
     const int64_t* rf = (const int64_t*)(b + sizeof(OutRec) + cq.hdr.nsel * sizeof(DVal));
-    h.refs.assign(rf, rf + cq.hdr.nrefs_vis);
+    h.refs = rf;
+    h.nrefs = cq.hdr.nrefs_vis;
     if (cq.hdr.nrefs == cq.hdr.nrefs_vis + 2) {
       h.e1 = rf[cq.hdr.nrefs_vis];
       h.e2 = rf[cq.hdr.nrefs_vis + 1];
     }
     h.qidx = qidx;
-    outs.push_back(std::move(h));
+    outs.push_back(h);
   }
 }
 
@@ -773,7 +833,16 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
     if (he & NFA_ERR_NPE) why += " NullPointerException/IllegalStateException path of the reference;";
     throw std::runtime_error("query '" + q.cq.name + "':" + why);
   }
-  read_outputs(a, qi, q.out.p, std::min<int64_t>(hc, cap), outs);
+  const int64_t nout = std::min<int64_t>(hc, cap);
+  // lanes claim output slots with an atomic, so the records are unordered across lanes: order a large set on the
+  // device (a few radix passes) instead of sorting it on the host
+  const char* recs = (const char*)q.out.p;
+  const size_t need = (size_t)nout * (48 + stride) + (16 << 20);  // keys, indices, ordered copy, sort passes
+  if (nout >= 2048 && a->sc.used + need <= a->sc.cap) {
+    recs = order_outputs(recs, nout, (uint32_t)stride, ev.ev_clock, a->sc, hs);
+    SM_HIP(hipStreamSynchronize(hs));
+  }
+  read_outputs(a, qi, recs, nout, outs);
 }
 
 // Scratch of one batch: record selection + key grouping (~96 B per record) and the LaneEv records of the widest
@@ -901,6 +970,11 @@ int64_t nfa_device_batch(sm_app* a, int qi, int s, size_t n, const int64_t* d_ts
                     nadv, a->clock};
   std::vector<HostOut> outs;
   a->sc.used = 0;
+  a->need_outs = true;
+  struct Reset {
+    bool& f;
+    ~Reset() { f = false; }
+  } reset_need{a->need_outs};
   run_pattern_query(a, qi, ev, N, outs, hs);
   std::stable_sort(outs.begin(), outs.end(), [](const HostOut& x, const HostOut& y) {
     return x.r.pos != y.r.pos ? x.r.pos < y.r.pos : x.r.seq < y.r.seq;
@@ -916,6 +990,7 @@ int64_t nfa_device_batch(sm_app* a, int qi, int s, size_t n, const int64_t* d_ts
   if (!pairs.empty())
     SM_HIP(hipMemcpyAsync(q.dev_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, hs));
   SM_HIP(hipStreamSynchronize(hs));
+  a->out_arena.clear();
   return (int64_t)outs.size();
 }
 
@@ -1984,10 +2059,10 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
     std::vector<HostOut> outs;
     for (size_t qi = 0; qi < a->queries.size(); ++qi) {
       a->sc.used = 0;
+      a->queries[qi]->n_out = 0;
       run_pattern_query(a, (int)qi, ev, N, outs, hs, tm);
-      a->queries[qi]->dev_n = 0;
+      a->queries[qi]->dev_n = a->queries[qi]->n_out;
     }
-    for (auto& h : outs) a->queries[h.qidx]->dev_n++;
     a->clock = clock_out;
     a->clock_batch_in = a->clock;
     if (!d_ordinals) a->next_ordinal = std::max<int64_t>(a->next_ordinal, ordinal_base + N);

@@ -97,6 +97,10 @@ class ProductApp:
         L.sm_app_dump_outputs(self.h, buf, n + 1)
         return json.loads(buf.value.decode())
 
+    def set_collect(self, on):
+        """Keep (on) or drop (off) the JSON dump of delivered outputs; output counts are kept either way."""
+        _call(lib().sm_app_set_collect(self.h, 1 if on else 0))
+
     def set_option(self, key, value):
         _call(lib().sm_app_set_option(self.h, key.encode(), int(value)))
 
