@@ -21,6 +21,8 @@
  *                                   QueryCallback.java:51): no Java counterpart, one JVM has one output queue
  *   sm_app_copy_device_matches      the device tuples of the last batch into a caller buffer (for collectives)
  *   sm_compile_dump                 SiddhiCompiler.parse (siddhi-query-compiler .../SiddhiCompiler.java:56)
+ *   sm_nfa_jit_compile              QueryParser.parse (core/util/parser/QueryParser.java:79) for one query, as the
+ *                                   query-specialised NFA kernel (no device needed): the build check of the JIT
  *   sm_app_process_device_events    a sequence of InputHandler.send calls over several streams of one
  *                                   schema (InputHandler.java:53 → StreamJunction.sendData :232), device-resident
  *
@@ -83,6 +85,11 @@ int sm_app_create(sm_manager* m, const char* siddhiql, sm_app** out);
 /* Parse only (no device needed): the app's query tree as canonical JSON (shapes in siddhiql/dump.cpp) into buf,
  * NUL-terminated when it fits in cap; *len = its length. Errors as sm_app_create reports them for the same text. */
 int sm_compile_dump(const char* siddhiql, char* buf, size_t cap, size_t* len);
+/* Compile query number `query` (app order) of the app into its query-specialised NFA kernel (the interpreter with
+ * the query's plan fixed at compile time, hiprtc for gfx950; no device needed). *code_size = the code object's
+ * size; on failure the compiler log is in log (NUL-terminated, at most cap bytes) and sm_last_error. The app option
+ * "nfa_jit" (1 / 0 / -1 = automatic, for batches of 2^20 query records or more) selects this kernel at run time. */
+int sm_nfa_jit_compile(const char* siddhiql, int query, char* log, size_t cap, size_t* code_size);
 void sm_app_destroy(sm_app* app);
 int sm_app_start(sm_app* app);
 int sm_app_flush(sm_app* app);

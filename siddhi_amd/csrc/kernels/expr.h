@@ -157,10 +157,19 @@ struct ColCtx {
 };
 
 // Generic evaluation. Loader must provide StackVal var(const Instr&) for OP_VAR / OP_COL.
+// SM_NFA_JIT_INLINE_ALL: the plan's programs are constants there; unrolled, the operand stack becomes registers
+#ifdef SM_NFA_JIT_INLINE_ALL
+#define SM_EXPR_INL __attribute__((always_inline))
+#define SM_EXPR_UNROLL _Pragma("unroll")
+#else
+#define SM_EXPR_INL
+#define SM_EXPR_UNROLL
+#endif
 template <typename Loader>
-__device__ StackVal eval_prog(const Instr* code, int len, const DVal* consts, const Loader& ld) {
+SM_EXPR_INL __device__ StackVal eval_prog(const Instr* code, int len, const DVal* consts, const Loader& ld) {
   StackVal st[kMaxStack];
   int sp = 0;
+  SM_EXPR_UNROLL
   for (int pc = 0; pc < len; ++pc) {
     const Instr in = code[pc];
     switch (in.op) {

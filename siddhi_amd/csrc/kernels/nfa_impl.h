@@ -64,6 +64,29 @@ struct Lane;
 #define SM_INL_FIRE
 #endif
 
+// Plan tables. The interpreter reads the plan from a device buffer (one build serves every query). A JIT build
+// (SM_NFA_JIT, nfa_jit.cpp) compiles this file once per query plan with the plan as a constant array
+// (sm::kPlanBlob): every PQ->field and table entry is then a compile-time constant, the plan's loops and kind
+// switches fold away and the filter / projection programs become straight-line code.
+#ifdef SM_NFA_JIT
+#define PQ ((const DQuery*)::sm::kPlanBlob)
+#define PPRE ((const DPre*)(::sm::kPlanBlob + PQ->off_pre))
+#define PPOST ((const DPost*)(::sm::kPlanBlob + PQ->off_post))
+#define PRECV ((const DReceiver*)(::sm::kPlanBlob + PQ->off_recv))
+#define PWITHIN ((const DWithin*)(::sm::kPlanBlob + PQ->off_within))
+#define PCODE ((const Instr*)(::sm::kPlanBlob + PQ->off_code))
+#define PCONSTS ((const DVal*)(::sm::kPlanBlob + PQ->off_const))
+#define PSEL ((const int32_t*)(::sm::kPlanBlob + PQ->off_sel))
+#define PREFS ((const int32_t*)(::sm::kPlanBlob + PQ->off_refs))
+#endif
+
+// SM_NFA_JIT_INLINE_ALL (JIT A/B): every member function on the event path inline into the kernel
+#ifdef SM_NFA_JIT_INLINE_ALL
+#define SM_JIT_INL SM_NFA_ALWAYS_INLINE
+#else
+#define SM_JIT_INL
+#endif
+
 struct StateLoader {  // OP_VAR loads for a run record
   const Lane* L;
   int rec;
@@ -83,16 +106,17 @@ struct LaneWords {
 
 struct Lane {
   // plan
-  const DQuery* q;
-  const DPre* pre;
-  const DPost* post;
-  const DInner* inner;
-  const DReceiver* recv;
-  const DWithin* within;
-  const Instr* code;
-  const DVal* consts;
-  const int32_t* sel;
-  const int32_t* refs;
+#ifndef SM_NFA_JIT
+  const DQuery* PQ;
+  const DPre* PPRE;
+  const DPost* PPOST;
+  const DReceiver* PRECV;
+  const DWithin* PWITHIN;
+  const Instr* PCODE;
+  const DVal* PCONSTS;
+  const int32_t* PSEL;
+  const int32_t* PREFS;
+#endif
   // state
   LaneWords ks;
   LaneWords heap;
@@ -108,7 +132,7 @@ struct Lane {
   int64_t clock;  // EventTimeBasedMillisTimestampGenerator.currentTime() as seen by this lane
 
   // ------------------------------------------------------------ heap
-  __device__ int64_t& misc(int k) const { return ks[q->ks_misc + k]; }
+  __device__ int64_t& misc(int k) const { return ks[PQ->ks_misc + k]; }
   __device__ int32_t alloc(int words) {
     int64_t space = misc(2);
     int64_t end = (space + 1) * half;
@@ -136,17 +160,17 @@ struct Lane {
     if (s & 1) w = (w & 0xFFFFFFFFll) | ((int64_t)(uint32_t)v << 32);
     else w = (w & ~0xFFFFFFFFll) | (int64_t)(uint32_t)v;
   }
-  __device__ int32_t new_rec() {
-    int32_t r = alloc(q->rec_words);
+  SM_JIT_INL __device__ int32_t new_rec() {
+    int32_t r = alloc(PQ->rec_words);
     heap[r] = K_REC;
     heap[r + 1] = -1;  // StateEvent.timestamp = -1
-    for (int k = 2; k < q->rec_words; ++k) heap[r + k] = -1;  // all slots null (two -1 halves)
+    for (int k = 2; k < PQ->rec_words; ++k) heap[r + k] = -1;  // all slots null (two -1 halves)
     return r;
   }
   // StateEventCloner.copyStateEvent :46-57 (shallow)
-  __device__ int32_t copy_rec(int32_t src) {
-    int32_t r = alloc(q->rec_words);
-    for (int k = 0; k < q->rec_words; ++k) heap[r + k] = heap[src + k];
+  SM_JIT_INL __device__ int32_t copy_rec(int32_t src) {
+    int32_t r = alloc(PQ->rec_words);
+    for (int k = 0; k < PQ->rec_words; ++k) heap[r + k] = heap[src + k];
     return r;
   }
   // chain node
@@ -155,26 +179,26 @@ struct Lane {
   __device__ int64_t nts(int32_t n) const { return heap[n + 1]; }
   __device__ int64_t nord(int32_t n) const { return heap[n + 2]; }
   SM_INL_SMALL __device__ int32_t copy_node(int32_t src) {  // StreamEventCloner.copyStreamEvent: next = null
-    int32_t n = alloc(q->node_words);
-    for (int k = 1; k < q->node_words; ++k) heap[n + k] = heap[src + k];
+    int32_t n = alloc(PQ->node_words);
+    for (int k = 1; k < PQ->node_words; ++k) heap[n + k] = heap[src + k];
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
     return n;
   }
-  __device__ int32_t empty_node() {  // streamEventPool.borrowEvent(): ts -1, null data
-    int32_t n = alloc(q->node_words);
+  SM_JIT_INL __device__ int32_t empty_node() {  // streamEventPool.borrowEvent(): ts -1, null data
+    int32_t n = alloc(PQ->node_words);
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
     heap[n + 1] = -1;
     heap[n + 2] = -1;
     heap[n + 3] = -1;  // every attribute null
-    for (int k = 4; k < q->node_words; ++k) heap[n + k] = 0;
+    for (int k = 4; k < PQ->node_words; ++k) heap[n + k] = 0;
     return n;
   }
   // the incoming event, materialised as a chain node once per delivery: a copy of the node image the
   // lane-events pass already built (LaneEv, nfa.h)
-  __device__ int32_t event_node(const int64_t* __restrict__ r) {
-    int32_t n = alloc(q->node_words);
+  SM_JIT_INL __device__ int32_t event_node(const int64_t* __restrict__ r) {
+    int32_t n = alloc(PQ->node_words);
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
-    for (int w = 1; w < q->node_words; ++w) heap[n + w] = r[LaneEv::kNode + w];
+    for (int w = 1; w < PQ->node_words; ++w) heap[n + w] = r[LaneEv::kNode + w];
     return n;
   }
   // StateEvent.addEvent :212-222
@@ -196,7 +220,7 @@ struct Lane {
     }
   }
   // StateEvent.getStreamEvent(int[] position) :138-182
-  __device__ int32_t at(int32_t r, int chain, int idx) const {
+  SM_JIT_INL __device__ int32_t at(int32_t r, int chain, int idx) const {
     int32_t e = slot(r, chain);
     if (e < 0) return -1;
     if (idx >= 0) {
@@ -220,7 +244,7 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ lists (LinkedList<StateEvent>)
-  __device__ int64_t& lw(int p, int which) const { return ks[q->ks_pre + p * kPreWords + which]; }
+  __device__ int64_t& lw(int p, int which) const { return ks[PQ->ks_pre + p * kPreWords + which]; }
   __device__ int32_t lhead(int p, int w) const { return (int32_t)lw(p, w); }
   __device__ int32_t ltail(int p, int w) const { return (int32_t)(lw(p, w) >> 32); }
   __device__ void lset(int p, int w, int32_t h, int32_t t) const {
@@ -285,11 +309,11 @@ struct Lane {
     else flags(p) &= ~f;
   }
   __device__ int64_t& lastArrival(int p) const { return lw(p, 3); }
-  __device__ int64_t& returned(int o) const { return ks[q->ks_post + o]; }
+  __device__ int64_t& returned(int o) const { return ks[PQ->ks_post + o]; }
 
   // ------------------------------------------------------------ timers (Scheduler FIFO)
-  __device__ LaneWords sq(int s) const { return ks.at(q->ks_sched + s * (2 + kSchedCap)); }
-  __device__ void notifyAt(int s, int64_t t) {  // Scheduler.notifyAt :66-74
+  __device__ LaneWords sq(int s) const { return ks.at(PQ->ks_sched + s * (2 + kSchedCap)); }
+  SM_JIT_INL __device__ void notifyAt(int s, int64_t t) {  // Scheduler.notifyAt :66-74
     LaneWords S = sq(s);
     if (S[1] >= kSchedCap) {
       err |= NFA_ERR_TIMERS;
@@ -311,18 +335,18 @@ struct Lane {
 
   // ------------------------------------------------------------ evaluation
   __device__ bool filter_pass(int p, int32_t rec) const {
-    const DPre& P = pre[p];
+    const DPre& P = PPRE[p];
     if (P.progLen == 0) return true;
     StateLoader ld{this, rec};
-    return truthy(eval_prog(code + P.progOff, P.progLen, consts, ld));
+    return truthy(eval_prog(PCODE + P.progOff, P.progLen, PCONSTS, ld));
   }
-  __device__ bool is_absent(int p) const { return pre[p].kind == PK_ABSENT_STREAM || pre[p].kind == PK_ABSENT_LOGICAL; }
+  __device__ bool is_absent(int p) const { return PPRE[p].kind == PK_ABSENT_STREAM || PPRE[p].kind == PK_ABSENT_LOGICAL; }
 
   // StreamPreStateProcessor.isExpired :102-121
   SM_INL_SMALL __device__ bool expired(int p, int32_t rec, int64_t now) {
-    const DPre& P = pre[p];
+    const DPre& P = PPRE[p];
     for (int w = 0; w < P.withinCnt; ++w) {
-      const DWithin& W = within[P.withinOff + w];
+      const DWithin& W = PWITHIN[P.withinOff + w];
       for (int k = 0; k < W.n; ++k) {
         int id = W.ids[k];
         int64_t ref;
@@ -344,7 +368,7 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ selector (QuerySelector.processNoGroupBy)
-  __device__ void emit(int32_t rec) {
+  SM_JIT_INL __device__ void emit(int32_t rec) {
     uint32_t idx = atomicAdd(b->out_count, 1u);
     if (idx >= b->out_cap) {
       err |= NFA_ERR_OUTPUT;
@@ -354,34 +378,34 @@ struct Lane {
     OutRec* o = (OutRec*)base;
     o->pos = pos;
     o->time = time;
-    o->create = q->partitioned ? misc(0) : -1;
+    o->create = PQ->partitioned ? misc(0) : -1;
     o->ts = rts(rec);
     o->phase = phase;
-    o->query = q->query_order;
+    o->query = PQ->query_order;
     o->sched = sched;
     o->seq = seq++;
     o->key = key;
     DVal* vals = (DVal*)(base + sizeof(OutRec));
     StateLoader ld{this, rec};
-    for (int k = 0; k < q->nsel; ++k) {
-      StackVal v = eval_prog(code + sel[3 * k], sel[3 * k + 1], consts, ld);
-      if (sel[3 * k + 2] == T_FLOAT || sel[3 * k + 2] == T_DOUBLE) vals[k].d = v.d;
+    for (int k = 0; k < PQ->nsel; ++k) {
+      StackVal v = eval_prog(PCODE + PSEL[3 * k], PSEL[3 * k + 1], PCONSTS, ld);
+      if (PSEL[3 * k + 2] == T_FLOAT || PSEL[3 * k + 2] == T_DOUBLE) vals[k].d = v.d;
       else vals[k].i = v.i;
       vals[k].null = v.null;
       vals[k].pad = 0;
     }
-    int64_t* rf = (int64_t*)(vals + q->nsel);
-    for (int k = 0; k < q->nrefs; ++k) {
-      int32_t n = at(rec, refs[2 * k], refs[2 * k + 1]);
+    int64_t* rf = (int64_t*)(vals + PQ->nsel);
+    for (int k = 0; k < PQ->nrefs; ++k) {
+      int32_t n = at(rec, PREFS[2 * k], PREFS[2 * k + 1]);
       rf[k] = n >= 0 ? nord(n) : -1;
     }
   }
 
   // ------------------------------------------------------------ pre-state processors
   // StreamPreStateProcessor.init :165-174
-  __device__ void pre_init(int p) {
-    const DPre& P = pre[p];
-    const DPost& TP = post[P.post];
+  SM_JIT_INL __device__ void pre_init(int p) {
+    const DPre& P = PPRE[p];
+    const DPost& TP = PPOST[P.post];
     if (P.isStart && (!fl(p, F_INITIALIZED) || TP.nextEveryPre >= 0 ||
                       (P.sequence && TP.nextPre >= 0 && is_absent(TP.nextPre)))) {
       int32_t r = new_rec();
@@ -407,7 +431,7 @@ struct Lane {
         continue;
       }
       if (a == ACT_MIN) {  // CountPostStateProcessor.processMinCountReached :73-85 (p = post index)
-        const DPost& O = post[p];
+        const DPost& O = PPOST[p];
         if (O.hasNext) {
           setfl(O.thisPre, F_STATE_CHANGED, true);
           returned(p) = 1;
@@ -420,7 +444,7 @@ struct Lane {
         if (O.nextPre >= 0) work[sp++] = (uint16_t)(O.nextPre << 2 | ACT_ADD);
         continue;
       }
-      const DPre& P = pre[p];
+      const DPre& P = PPRE[p];
       switch (P.kind) {
         case PK_STREAM:  // StreamPreStateProcessor.addState :208-221
           if (P.sequence) {
@@ -452,7 +476,7 @@ struct Lane {
           }
           if (P.kind == PK_ABSENT_LOGICAL && !P.isStart && P.waitingTime != -1) {
             notifyAt(P.sched, rts(r) + P.waitingTime);
-            if (pre[pt].kind == PK_ABSENT_LOGICAL) notifyAt(pre[pt].sched, rts(r) + pre[pt].waitingTime);
+            if (PPRE[pt].kind == PK_ABSENT_LOGICAL) notifyAt(PPRE[pt].sched, rts(r) + PPRE[pt].waitingTime);
           }
           break;
         }
@@ -470,15 +494,15 @@ struct Lane {
     }
   }
 
-  __device__ void addEveryState(int p, int32_t r) {
-    const DPre& P = pre[p];
+  SM_JIT_INL __device__ void addEveryState(int p, int32_t r) {
+    const DPre& P = PPRE[p];
     switch (P.kind) {
       case PK_LOGICAL: {  // LogicalPreStateProcessor.addEveryState :80-88
         int32_t c = copy_rec(r);
         set_slot(c, P.stateId, -1);
         lappend(p, 1, c);
         if (P.partner >= 0) {
-          set_slot(c, pre[P.partner].stateId, -1);
+          set_slot(c, PPRE[P.partner].stateId, -1);
           lappend(P.partner, 1, c);
         }
         break;
@@ -488,7 +512,7 @@ struct Lane {
         int32_t own = slot(c, P.stateId);
         if (own >= 0) rts(c) = nts(own);
         set_slot(c, P.stateId, -1);
-        set_slot(c, pre[P.partner].stateId, -1);
+        set_slot(c, PPRE[P.partner].stateId, -1);
         lappend(p, 1, c);
         lappend(P.partner, 1, c);
         break;
@@ -499,8 +523,8 @@ struct Lane {
     }
   }
 
-  __device__ void updateState(int p) {
-    const DPre& P = pre[p];
+  SM_JIT_INL __device__ void updateState(int p) {
+    const DPre& P = PPRE[p];
     if (P.kind == PK_COUNT && fl(p, F_START_RESET)) {  // CountPreStateProcessor.updateState :145-151
       setfl(p, F_START_RESET, false);
       pre_init(p);
@@ -510,19 +534,19 @@ struct Lane {
   }
 
   __device__ bool seq_guard(int p) const {
-    const DPre& P = pre[p];
-    const DPost& TP = post[P.post];
+    const DPre& P = PPRE[p];
+    const DPost& TP = PPOST[P.post];
     return P.sequence && TP.nextEveryPre < 0 && TP.nextPre >= 0 && !lempty(TP.nextPre, 0);
   }
 
-  __device__ void resetState(int p) {
-    const DPre& P = pre[p];
+  SM_JIT_INL __device__ void resetState(int p) {
+    const DPre& P = PPRE[p];
     switch (P.kind) {
       case PK_STREAM:
       case PK_COUNT:  // StreamPreStateProcessor.resetState :253-265
         lclear(p, 0);
         if (P.isStart && lempty(p, 1)) {
-          if (P.sequence && post[P.post].nextEveryPre < 0 && post[P.post].nextPre < 0) {
+          if (P.sequence && PPOST[P.post].nextEveryPre < 0 && PPOST[P.post].nextPre < 0) {
             err |= NFA_ERR_NPE;
             return;
           }
@@ -560,13 +584,13 @@ struct Lane {
   SM_INL_PRE __device__ void pre_process(int p, int32_t r) {
     setfl(p, F_STATE_CHANGED, false);
     if (!filter_pass(p, r)) return;
-    post_process(pre[p].post, r);
+    post_process(PPRE[p].post, r);
   }
 
   // processAndReturn of every pre kind; returned records are appended to the temporary list `ret`
   // (list words kept in ks slots 4/5 of the pre: the selector runs after the loop, as in the receivers).
   SM_INL_PAR __device__ void processAndReturn(int p, int32_t evnode, int64_t now) {
-    const DPre& P = pre[p];
+    const DPre& P = PPRE[p];
     const int sid = P.stateId;
     lclear(p, 4 - 0);  // ret list lives in word 4 (head|tail); word 5 spare
     switch (P.kind) {
@@ -597,7 +621,7 @@ struct Lane {
           } else {
             set_slot(s, sid, -1);
             ln = lerase(p, 0, prev, ln);
-            int cb = post[P.post].callbackPre;
+            int cb = PPOST[P.post].callbackPre;
             if (cb >= 0) count_startStateReset(cb);
           }
         }
@@ -609,7 +633,7 @@ struct Lane {
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
           int32_t s = ln_rec(ln);
-          if ((q->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (q->nslots > sid + 2 && slot(s, sid + 2) >= 0)) {
+          if ((PQ->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (PQ->nslots > sid + 2 && slot(s, sid + 2) >= 0)) {
             ln = lerase(p, 0, prev, ln);
             continue;
           }
@@ -646,7 +670,7 @@ struct Lane {
       }
       case PK_LOGICAL: {  // LogicalPreStateProcessor.processAndReturn :125-163
         int32_t prev = -1;
-        const int psid = pre[P.partner].stateId;
+        const int psid = PPRE[P.partner].stateId;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
           int32_t s = ln_rec(ln);
@@ -681,7 +705,7 @@ struct Lane {
       default: {  // PK_ABSENT_LOGICAL: AbsentLogicalPreStateProcessor.processAndReturn (always returns empty)
         if (!fl(p, F_ACTIVE)) return;
         int32_t prev = -1;
-        const int psid = pre[P.partner].stateId;
+        const int psid = PPRE[P.partner].stateId;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
           int32_t s = ln_rec(ln);
@@ -696,7 +720,7 @@ struct Lane {
           int32_t current = slot(s, sid);
           set_slot(s, sid, copy_node(evnode));
           pre_process(p, s);
-          if (P.waitingTime != -1 || (P.sequence && P.ltype == LT_AND && post[P.post].nextEveryPre >= 0))
+          if (P.waitingTime != -1 || (P.sequence && P.ltype == LT_AND && PPOST[P.post].nextEveryPre >= 0))
             set_slot(s, sid, current);
           bool removed = false;
           int tl = P.thisLast;
@@ -729,8 +753,8 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ post-state processors
-  __device__ void stream_post(int o, int32_t r) {  // StreamPostStateProcessor.process :53-72
-    const DPost& O = post[o];
+  SM_JIT_INL __device__ void stream_post(int o, int32_t r) {  // StreamPostStateProcessor.process :53-72
+    const DPost& O = PPOST[o];
     setfl(O.thisPre, F_STATE_CHANGED, true);
     rts(r) = nts(slot(r, O.stateId));
     if (O.hasNext) returned(o) = 1;
@@ -739,8 +763,8 @@ struct Lane {
     if (O.callbackPre >= 0) count_startStateReset(O.callbackPre);
   }
   // CountPostStateProcessor.processMinCountReached :73-85 (non-recursive: nested addState via the work list)
-  __device__ void count_minReached(int o, int32_t r) {
-    const DPost& O = post[o];
+  SM_JIT_INL __device__ void count_minReached(int o, int32_t r) {
+    const DPost& O = PPOST[o];
     if (O.hasNext) {
       setfl(O.thisPre, F_STATE_CHANGED, true);
       returned(o) = 1;
@@ -749,9 +773,9 @@ struct Lane {
     if (O.nextEveryPre >= 0) addEveryState(O.nextEveryPre, r);
   }
   // AbsentLogicalPreStateProcessor.partnerCanProceed
-  __device__ bool partnerCanProceed(int p, int32_t r) {
-    const DPre& P = pre[p];
-    const DPost& TP = post[P.post];
+  SM_JIT_INL __device__ bool partnerCanProceed(int p, int32_t r) {
+    const DPre& P = PPRE[p];
+    const DPost& TP = PPOST[P.post];
     if (P.sequence && TP.nextEveryPre < 0 && lastArrival(p) > 0) return false;
     if (P.waitingTime == -1) {
       if (TP.nextEveryPre < 0) return slot(r, P.stateId) < 0;
@@ -764,8 +788,8 @@ struct Lane {
     }
     return slot(r, P.stateId) >= 0;
   }
-  __device__ void post_process(int o, int32_t r) {
-    const DPost& O = post[o];
+  SM_JIT_INL __device__ void post_process(int o, int32_t r) {
+    const DPost& O = PPOST[o];
     switch (O.kind) {
       case PK_STREAM: stream_post(o, r); break;
       case PK_COUNT: {  // CountPostStateProcessor.process :45-71
@@ -778,7 +802,7 @@ struct Lane {
         setfl(O.thisPre, F_SUCCESS, true);
         rts(r) = nts(e);
         if (n >= O.minCount) {
-          if (pre[O.thisPre].sequence) {
+          if (PPRE[O.thisPre].sequence) {
             if (O.nextPre >= 0) addState(O.nextPre, r);
             if (n != O.maxCount) addState(O.thisPre, r);
           } else if (n == O.minCount) {
@@ -791,13 +815,13 @@ struct Lane {
       case PK_LOGICAL: {  // LogicalPostStateProcessor.process :59-87
         if (O.ltype == LT_AND) {
           bool proceed;
-          if (pre[O.partnerPre].kind == PK_ABSENT_LOGICAL) proceed = partnerCanProceed(O.partnerPre, r);
-          else proceed = slot(r, pre[O.partnerPre].stateId) >= 0;
+          if (PPRE[O.partnerPre].kind == PK_ABSENT_LOGICAL) proceed = partnerCanProceed(O.partnerPre, r);
+          else proceed = slot(r, PPRE[O.partnerPre].stateId) >= 0;
           if (proceed) stream_post(o, r);
           else setfl(O.thisPre, F_STATE_CHANGED, true);
         } else {
           stream_post(o, r);
-          if (post[O.partnerPost].hasNext && pre[O.thisPre].thisLast == O.partnerPost) returned(O.partnerPost) = 1;
+          if (PPOST[O.partnerPost].hasNext && PPRE[O.thisPre].thisLast == O.partnerPost) returned(O.partnerPost) = 1;
         }
         break;
       }
@@ -806,7 +830,7 @@ struct Lane {
         int32_t se = slot(r, O.stateId);
         rts(r) = nts(se);
         returned(o) = 1;
-        if (pre[O.thisPre].isStart && O.nextEveryPre >= 0 && O.nextEveryPre == O.thisPre)
+        if (PPRE[O.thisPre].isStart && O.nextEveryPre >= 0 && O.nextEveryPre == O.thisPre)
           addEveryState(O.nextEveryPre, r);
         lastArrival(O.thisPre) = nts(se);
         break;
@@ -821,16 +845,16 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ absent timers
-  __device__ void absent_sendEvent(int p, int32_t r) {  // AbsentStreamPreStateProcessor.sendEvent :200-215
-    const DPre& P = pre[p];
-    const DPost& TP = post[P.post];
+  SM_JIT_INL __device__ void absent_sendEvent(int p, int32_t r) {  // AbsentStreamPreStateProcessor.sendEvent :200-215
+    const DPre& P = PPRE[p];
+    const DPost& TP = PPOST[P.post];
     if (TP.hasNext) emit(r);
     if (TP.nextPre >= 0) addState(TP.nextPre, r);
     if (TP.nextEveryPre >= 0) {
       addEveryState(TP.nextEveryPre, r);
     } else if (P.isStart) {
       setfl(p, F_ACTIVE, false);
-      if (P.kind == PK_ABSENT_LOGICAL && P.ltype == LT_OR && pre[P.partner].kind == PK_ABSENT_LOGICAL)
+      if (P.kind == PK_ABSENT_LOGICAL && P.ltype == LT_OR && PPRE[P.partner].kind == PK_ABSENT_LOGICAL)
         setfl(P.partner, F_ACTIVE, false);
     }
     if (TP.callbackPre >= 0) count_startStateReset(TP.callbackPre);
@@ -838,8 +862,8 @@ struct Lane {
 
   // AbsentStreamPreStateProcessor.process(ComplexEventChunk) :129-198 /
   // AbsentLogicalPreStateProcessor.process(ComplexEventChunk)
-  __device__ void absent_timer(int p, int64_t now) {
-    const DPre& P = pre[p];
+  SM_JIT_INL __device__ void absent_timer(int p, int64_t now) {
+    const DPre& P = PPRE[p];
     if (!fl(p, F_ACTIVE)) return;
     bool notProcessed = true;
     const int sid = P.stateId;
@@ -847,7 +871,7 @@ struct Lane {
     if (now >= lastArrival(p) + P.waitingTime) {
       if (P.kind == PK_ABSENT_STREAM) {
         bool initialize = P.isStart && lempty(p, 1) && lempty(p, 0);
-        if (initialize && P.sequence && post[P.post].nextEveryPre < 0 && lastArrival(p) > 0) initialize = false;
+        if (initialize && P.sequence && PPOST[P.post].nextEveryPre < 0 && lastArrival(p) > 0) initialize = false;
         if (initialize) {
           addState(p, new_rec());
         } else if (P.sequence && !lempty(p, 1)) {
@@ -878,7 +902,7 @@ struct Lane {
           bool passed = own >= 0 ? now >= nts(own) + P.waitingTime : now >= rts(s) + P.waitingTime;
           if (passed) {
             ln = lerase(p, 0, prev, ln);
-            bool partner_has = slot(s, pre[P.partner].stateId) >= 0;
+            bool partner_has = slot(s, PPRE[P.partner].stateId) >= 0;
             if (P.ltype == LT_OR && !partner_has) {
               add_event(s, sid, empty_node());
               lappend(p, 4, s);
@@ -898,7 +922,7 @@ struct Lane {
       lclear(p, 4);
       lastArrival(p) = 0;
     }
-    const DPost& TP = post[P.post];
+    const DPost& TP = PPOST[P.post];
     bool rearm = (P.kind == PK_ABSENT_STREAM) ? (TP.nextEveryPre == p || (notProcessed && P.isStart))
                                               : (TP.nextEveryPre >= 0 || (notProcessed && P.isStart));
     if (rearm) {
@@ -913,7 +937,7 @@ struct Lane {
     if (o < 0) return o;
     int k = kind_of(o);
     if (k == K_FWD) return hi(o);
-    int words = (k == K_REC) ? q->rec_words : (k == K_NODE) ? q->node_words : 2;
+    int words = (k == K_REC) ? PQ->rec_words : (k == K_NODE) ? PQ->node_words : 2;
     int32_t n = (int32_t)top;
     for (int w = 0; w < words; ++w) heap[n + w] = heap[o + w];
     top += words;
@@ -924,7 +948,7 @@ struct Lane {
     int64_t space = misc(2);
     int64_t to = (1 - space) * half;
     int64_t top = to, scan = to;
-    for (int p = 0; p < q->npre; ++p)
+    for (int p = 0; p < PQ->npre; ++p)
       for (int w = 0; w < 2; ++w) {
         int32_t h = fwd(lhead(p, w), top);
         int32_t t = ltail(p, w) >= 0 ? fwd(ltail(p, w), top) : -1;
@@ -939,17 +963,17 @@ struct Lane {
         heap[o + 1] = fwd(nx, top);
         scan += 2;
       } else if (k == K_REC) {
-        for (int s = 0; s < q->nslots; ++s) set_slot(o, s, fwd(slot(o, s), top));
-        scan += q->rec_words;
+        for (int s = 0; s < PQ->nslots; ++s) set_slot(o, s, fwd(slot(o, s), top));
+        scan += PQ->rec_words;
       } else {
         set_hi(o, fwd(hi(o), top));
-        scan += q->node_words;
+        scan += PQ->node_words;
       }
     }
     misc(2) = 1 - space;
     misc(1) = top;
   }
-  __device__ void safe_point() {
+  SM_JIT_INL __device__ void safe_point() {
     int64_t used = misc(1) - misc(2) * half;
     if (used * 2 > half) gc();
   }
@@ -960,8 +984,8 @@ struct Lane {
     const int64_t p = r[LaneEv::kPos];
     const int s = (int)r[LaneEv::kStream];
     const DReceiver* R = nullptr;
-    for (int k = 0; k < q->nrecv; ++k)
-      if (recv[k].stream == s) R = &recv[k];
+    for (int k = 0; k < PQ->nrecv; ++k)
+      if (PRECV[k].stream == s) R = &PRECV[k];
     if (!R) return;
     pos = p;
     time = 0;
@@ -970,9 +994,9 @@ struct Lane {
     int32_t ev = event_node(r);
     int64_t now = r[LaneEv::kNode + 1];
     // stabilizeStates
-    if (q->kind == 2) {
-      for (int k = 0; k < q->nreset; ++k) resetState(q->reset_seq[k]);  // inner reset(), flattened (plan.h)
-      for (int k = 0; k < q->nupdate; ++k) updateState(q->update_seq[k]);
+    if (PQ->kind == 2) {
+      for (int k = 0; k < PQ->nreset; ++k) resetState(PQ->reset_seq[k]);  // inner reset(), flattened (plan.h)
+      for (int k = 0; k < PQ->nupdate; ++k) updateState(PQ->update_seq[k]);
     } else if (R->multi) {
       for (int k = 0; k < R->nstate; ++k) updateState(R->stateProcs[k]);
     } else if (R->nstate > 0) {
@@ -997,9 +1021,9 @@ struct Lane {
   // Playback listeners: every scheduler of this key drains its FIFO while head <= now (Scheduler.sendTimerEvents)
   SM_INL_FIRE __device__ void fire_all(int64_t now, int64_t at_pos, int64_t step_time) {
     clock = now;
-    for (int p = 0; p < q->npre; ++p) {
+    for (int p = 0; p < PQ->npre; ++p) {
       if (!is_absent(p)) continue;
-      int s = pre[p].sched;
+      int s = PPRE[p].sched;
       while (!qempty(s) && qhead(s) - now <= 0 && !err) {
         int64_t t = qhead(s);
         qpop(s);
@@ -1011,11 +1035,11 @@ struct Lane {
       }
     }
   }
-  __device__ bool min_head(int64_t& t) const {
+  SM_JIT_INL __device__ bool min_head(int64_t& t) const {
     bool any = false;
-    for (int p = 0; p < q->npre; ++p) {
+    for (int p = 0; p < PQ->npre; ++p) {
       if (!is_absent(p)) continue;
-      int s = pre[p].sched;
+      int s = PPRE[p].sched;
       if (!qempty(s)) {
         int64_t h = qhead(s);
         if (!any || h < t) t = h;
@@ -1160,20 +1184,24 @@ SM_TIMER_ATTR __device__ bool timer_fire(Lane& L, const NfaBatch& b, int64_t a1,
   return true;
 }
 
-__device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
+SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
                          int32_t heap_half, int64_t lanes, int32_t key, int32_t* err_out) {
-  const DQuery* q = (const DQuery*)blob;
   Lane L;
-  L.q = q;
-  L.pre = (const DPre*)(blob + q->off_pre);
-  L.post = (const DPost*)(blob + q->off_post);
-  L.inner = (const DInner*)(blob + q->off_inner);
-  L.recv = (const DReceiver*)(blob + q->off_recv);
-  L.within = (const DWithin*)(blob + q->off_within);
-  L.code = (const Instr*)(blob + q->off_code);
-  L.consts = (const DVal*)(blob + q->off_const);
-  L.sel = (const int32_t*)(blob + q->off_sel);
-  L.refs = (const int32_t*)(blob + q->off_refs);
+#ifdef SM_NFA_JIT
+  blob = (const char*)::sm::kPlanBlob;  // the kernel passes no plan buffer
+#else
+  L.PQ = (const DQuery*)blob;
+  L.PPRE = (const DPre*)(blob + L.PQ->off_pre);
+  L.PPOST = (const DPost*)(blob + L.PQ->off_post);
+  L.PRECV = (const DReceiver*)(blob + L.PQ->off_recv);
+  L.PWITHIN = (const DWithin*)(blob + L.PQ->off_within);
+  L.PCODE = (const Instr*)(blob + L.PQ->off_code);
+  L.PCONSTS = (const DVal*)(blob + L.PQ->off_const);
+  L.PSEL = (const int32_t*)(blob + L.PQ->off_sel);
+  L.PREFS = (const int32_t*)(blob + L.PQ->off_refs);
+  const DQuery* PQ = L.PQ;
+  const DPre* PPRE = L.PPRE;
+#endif
   L.ks = LaneWords{ks_all + key, lanes};
   L.half = heap_half;
   // the heap stays key-major: a lane's run records and chain nodes are private, pointer-chased objects, so
@@ -1186,21 +1214,21 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
   L.clock = b.clock_in;
 
   const int64_t ebeg = b.key_off[key], eend = b.key_off[key + 1];
-  const int64_t W = LaneEv::words(q->node_words);
-  const bool has_timers = q->nsched > 0;
+  const int64_t W = LaneEv::words(PQ->node_words);
+  const bool has_timers = PQ->nsched > 0;
   // lane creation: QueryRuntime constructor → init() seeds the start state (PartitionRuntime.clonePartition)
   if (L.misc(4) == 0) {
     if (ebeg == eend && !(b.create_all)) return;
-    const int32_t* init = (const int32_t*)(blob + q->filt_off);
-    for (int p = 0; p < q->npre; ++p) {
+    const int32_t* init = (const int32_t*)(blob + PQ->filt_off);
+    for (int p = 0; p < PQ->npre; ++p) {
       L.lset(p, 0, -1, -1);
       L.lset(p, 1, -1, -1);
       L.flags(p) = F_ACTIVE;
       L.lastArrival(p) = 0;
       L.lset(p, 4, -1, -1);
     }
-    for (int o = 0; o < q->npost; ++o) L.returned(o) = 0;
-    for (int s = 0; s < q->nsched; ++s) {
+    for (int o = 0; o < PQ->npost; ++o) L.returned(o) = 0;
+    for (int s = 0; s < PQ->nsched; ++s) {
       L.sq(s)[0] = 0;
       L.sq(s)[1] = 0;
     }
@@ -1243,9 +1271,9 @@ __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64
     L.clock = r[LaneEv::kClock];
     if (r[LaneEv::kStream] == NFA_START) {
       // SiddhiAppRuntime.start → AbsentStreamPreStateProcessor.start :261-269 (non-partitioned queries)
-      for (int pp = 0; pp < q->npre; ++pp)
-        if (L.is_absent(pp) && L.pre[pp].isStart && L.pre[pp].waitingTime != -1 && L.fl(pp, F_ACTIVE))
-          L.notifyAt(L.pre[pp].sched, L.clock + L.pre[pp].waitingTime);
+      for (int pp = 0; pp < PQ->npre; ++pp)
+        if (L.is_absent(pp) && PPRE[pp].isStart && PPRE[pp].waitingTime != -1 && L.fl(pp, F_ACTIVE))
+          L.notifyAt(PPRE[pp].sched, L.clock + PPRE[pp].waitingTime);
     } else {
       L.deliver(r);
     }

@@ -1,0 +1,171 @@
+// Query-specialised NFA kernels. The interpreter in kernels/nfa_impl.h serves every query from one build: it reads
+// the plan (state table, filter and projection programs) from a device buffer, so every plan field is a dependent
+// vector load, every plan loop and kind switch is a runtime branch, the filter programs run on an operand stack in
+// scratch, and the lane's state is passed between non-inlined member functions through scratch frames.
+//
+// Here the same source is compiled (hiprtc, gfx950) once per query plan with the plan as a constant array
+// (sm::kPlanBlob, SM_NFA_JIT): the plan's fields fold to constants, its loops unroll, kind switches drop their
+// dead cases and the programs become straight-line code, so the whole interpreter inlines into one kernel. This
+// is the device analogue of the reference compiling a query into its processor chain once, at app creation
+// (SiddhiAppParser / QueryParser.parse, core/util/parser/QueryParser.java:79): the semantics are the
+// interpreter's own, line for line; only the plan is fixed at compile time.
+#include "nfa_jit.h"
+
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "nfa_jit_body.inc"  // kNfaJitBody (embed_jit.py)
+
+namespace sm {
+
+namespace {
+
+struct JitKernel {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+};
+
+std::mutex g_mu;
+std::map<std::string, std::unique_ptr<JitKernel>>& cache() {
+  static std::map<std::string, std::unique_ptr<JitKernel>> c;
+  return c;
+}
+
+const char* kPrelude =
+    "#define SM_NFA_JIT 1\n"
+    // force the interpreter's member functions inline: with the plan constant they shrink to the plan's cases
+    "#define SM_NFA_INLINE_PAR 1\n"
+    "#define SM_NFA_INLINE_SMALL 1\n"
+    "#define SM_NFA_INLINE_ADD 1\n"
+    "#define SM_NFA_INLINE_FIRE 1\n"
+    "#define SM_TIMER_INLINE 1\n"
+    "typedef __hip_internal::int8_t int8_t;\n"
+    "typedef __hip_internal::int16_t int16_t;\n"
+    "typedef __hip_internal::int32_t int32_t;\n"
+    "typedef __hip_internal::int64_t int64_t;\n"
+    "typedef __hip_internal::uint8_t uint8_t;\n"
+    "typedef __hip_internal::uint16_t uint16_t;\n"
+    "typedef __hip_internal::uint32_t uint32_t;\n"
+    "typedef __hip_internal::uint64_t uint64_t;\n"
+    "#ifndef INT64_MAX\n#define INT64_MAX 9223372036854775807LL\n#endif\n"
+    "#ifndef INT32_MAX\n#define INT32_MAX 2147483647\n#endif\n"
+    "#ifndef INT32_MIN\n#define INT32_MIN (-2147483647 - 1)\n#endif\n"
+    "#ifndef INT64_MIN\n#define INT64_MIN (-9223372036854775807LL - 1)\n#endif\n"
+    "typedef struct ihipStream_t* hipStream_t;\n";
+
+const char* kKernel = R"SMJIT(
+extern "C" __global__ void __launch_bounds__(64) SM_NFA_JIT_ATTR sm_nfa_jit(sm::NfaBatch b, int64_t* ks_all, int64_t* heap_all,
+                                                            int32_t heap_half, int64_t lanes, int32_t nkeys,
+                                                            int32_t* err_out) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nkeys) return;
+  const int key = b.lane_perm ? (int)b.lane_perm[lane] : lane;
+  sm::nfa_lane(b, nullptr, ks_all, heap_all, heap_half, lanes, key, err_out);
+}
+)SMJIT";
+
+std::string blob_array(const std::vector<char>& blob) {
+  std::ostringstream s;
+  s << "namespace sm {\nstatic __device__ const unsigned char kPlanBlob[" << blob.size()
+    << "] __attribute__((aligned(16))) = {";
+  for (size_t i = 0; i < blob.size(); ++i) {
+    if (i % 32 == 0) s << "\n";
+    s << (unsigned)(unsigned char)blob[i] << ",";
+  }
+  s << "};\n}  // namespace sm\n";
+  return s.str();
+}
+
+}  // namespace
+
+std::string nfa_jit_source(const std::vector<char>& blob) {
+  std::string src = kPrelude;
+  // Occupancy: room for 3 waves per SIMD (170 VGPRs). Measured on config 5 (N = 1e8, heap_words 1024, NFA kernel
+  // ms): interpreter 74.3; JIT with the compiler's choice (268 VGPRs, 1 wave) 74.9, 2 waves 65.5, 4 waves 63.5;
+  // with every event-path function inline, 4 waves 64.4, 3 waves 60.6. A/B: SM_NFA_JIT_WAVES=<n> (0 = no hint).
+  const char* w = getenv("SM_NFA_JIT_WAVES");
+  const int waves = w ? atoi(w) : 3;
+  if (waves > 0)
+    src += "#define SM_NFA_JIT_ATTR __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))\n";
+  else
+    src += "#define SM_NFA_JIT_ATTR\n";
+  // every member function on the event path inline (A/B: SM_NFA_JIT_INLINE_ALL=0 leaves it to the compiler)
+  const char* e = getenv("SM_NFA_JIT_INLINE_ALL");
+  if (!e || atoi(e)) src += "#define SM_NFA_JIT_INLINE_ALL 1\n";
+  src += blob_array(blob);
+  src += kNfaJitBody;
+  src += kKernel;
+  return src;
+}
+
+bool nfa_jit_wanted(int option, int64_t records) {
+  static const char* env = getenv("SM_NFA_JIT");
+  if (env && *env) return atoi(env) != 0;
+  if (option >= 0) return option != 0;
+  return records >= (int64_t)1 << 20;  // the compile (seconds) pays off on large batches only
+}
+
+std::vector<char> nfa_jit_compile(const std::vector<char>& blob) {
+  const std::string src = nfa_jit_source(blob);
+  if (const char* dump = getenv("SM_NFA_JIT_DUMP")) {
+    if (FILE* f = fopen(dump, "w")) {
+      fwrite(src.data(), 1, src.size(), f);
+      fclose(f);
+    }
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "sm_nfa_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    throw std::runtime_error("nfa jit: hiprtcCreateProgram failed");
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pass-failed"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    std::string log(ls + 1, '\0');
+    hiprtcGetProgramLog(prog, &log[0]);
+    hiprtcDestroyProgram(&prog);
+    throw std::runtime_error("nfa jit: compile failed: " + log.substr(0, 4000));
+  }
+  size_t cs = 0;
+  hiprtcGetCodeSize(prog, &cs);
+  std::vector<char> code(cs);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  return code;
+}
+
+void* nfa_jit_function(const std::vector<char>& blob) {
+  int dev = 0;
+  SM_HIP(hipGetDevice(&dev));
+  std::string key = std::to_string(dev) + ":" + std::string(blob.begin(), blob.end());
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = cache().find(key);
+  if (it != cache().end()) return (void*)it->second->fn;
+  const std::vector<char> code = nfa_jit_compile(blob);
+  auto k = std::make_unique<JitKernel>();
+  SM_HIP(hipModuleLoadData(&k->mod, code.data()));
+  SM_HIP(hipModuleGetFunction(&k->fn, k->mod, "sm_nfa_jit"));
+  void* fn = (void*)k->fn;
+  cache()[key] = std::move(k);
+  return fn;
+}
+
+void launch_nfa_jit(void* fn, const NfaBatch& b, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
+                    int32_t nkeys, int32_t* err_dev, hipStream_t s) {
+  if (nkeys <= 0) return;
+  NfaBatch bb = b;
+  void* args[] = {&bb, &ks, &heap, &heap_half, &lanes, &nkeys, &err_dev};
+  const unsigned blocks = (unsigned)((nkeys + 63) / 64);
+  SM_HIP(hipModuleLaunchKernel((hipFunction_t)fn, blocks, 1, 1, 64, 1, 1, 0, s, args, nullptr));
+}
+
+}  // namespace sm

@@ -33,6 +33,7 @@
 #include "kernels/primitives.h"
 #include "kernels/stream_ops.h"
 #include "kernels/partition.h"
+#include "nfa_jit.h"
 #include "siddhiql/ast.h"
 
 namespace sm {
@@ -244,6 +245,8 @@ struct sm_app {
   // SM_NFA_BALANCE=<min keys> / option "lane_balance")
   int64_t lane_balance = 0;
   int64_t out_records = 0;  // option "output_records" (0 = automatic)
+  int nfa_jit = -1;         // option "nfa_jit": 1 = query-specialised NFA kernels (nfa_jit.cpp), 0 = the
+                            // interpreter, -1 = automatic (batches of 2^20 query records or more)
   uint64_t text_hash = 0;   // FNV-1a of the SiddhiQL text (snapshots restore only into the same app)
   bool collect = false;
   std::map<std::string, std::vector<std::string>> collected_streams;  // JSON fragments
@@ -816,8 +819,12 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
     launch_lane_balance(key_off, (int32_t)nkeys, perm, a->sc, hs);
     b.lane_perm = perm;
   }
-  launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
-             (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
+  if (nfa_jit_wanted(a->nfa_jit, nq))
+    launch_nfa_jit(nfa_jit_function(q.cq.blob), b, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
+                   (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
+  else
+    launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
+               (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
   SM_HIP(hipGetLastError());
   if (tm) tm->mark("nfa", hs);
   uint32_t hc = 0;
@@ -1635,6 +1642,32 @@ int sm_compile_dump(const char* siddhiql, char* buf, size_t cap, size_t* len) {
   });
 }
 
+int sm_nfa_jit_compile(const char* siddhiql, int query, char* log, size_t cap, size_t* code_size) {
+  int rc = guarded([&] {
+    const sql::App ast = sql::parse_app(siddhiql ? siddhiql : "");
+    if (query < 0 || (size_t)query >= ast.order.size()) throw std::runtime_error("no such query");
+    Dict dict;
+    auto [pi, qi] = ast.order[query];
+    const sql::Query& qd = pi < 0 ? ast.queries[qi] : ast.partitions[pi].queries[qi];
+    const CompiledQuery cq = compile_query(ast, qd, query, pi, dict);
+    const std::vector<char> code = nfa_jit_compile(cq.blob);
+    if (code_size) *code_size = code.size();
+    if (const char* path = getenv("SM_NFA_JIT_CO")) {
+      if (FILE* f = fopen(path, "wb")) {
+        fwrite(code.data(), 1, code.size(), f);
+        fclose(f);
+      }
+    }
+  });
+  if (log && cap) {
+    const std::string& m = sm::g_err;
+    const size_t n = std::min(cap - 1, m.size());
+    memcpy(log, m.data(), n);
+    log[n] = 0;
+  }
+  return rc;
+}
+
 void sm_app_destroy(sm_app* a) {
   if (!a) return;
   for (auto& q : a->queries) q->keys.release();
@@ -1814,6 +1847,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       a->fast_timing = value != 0;
     } else if (k == "lane_balance") {
       a->lane_balance = value;
+    } else if (k == "nfa_jit") {
+      a->nfa_jit = value < 0 ? -1 : (value != 0);
     } else if (k == "reset") {
       // drop every partition instance, partial match, pending timer and the playback clock, keeping the device
       // allocations: the state of a freshly created runtime of the same app (bench / test helper)

@@ -115,3 +115,16 @@ def test_device_events_rejects_filter_queries():
         a.process_device_events(torch.zeros(4, dtype=torch.int32, device=d), torch.zeros(4, dtype=torch.int64, device=d),
                                 [torch.zeros(4, dtype=torch.int32, device=d), torch.zeros(4, dtype=torch.float64, device=d)])
     a.close()
+
+
+@pytest.mark.parametrize("name", sorted(VARIANTS))
+def test_config5_variants_jit_equal_oracle(name):
+    """The query-specialised NFA kernel (option nfa_jit = 1: the interpreter compiled per plan, nfa_jit.cpp) on the
+    same streams, split in two batches: identical outputs to the oracle."""
+    sid, cols, ts = synth.gen5(0, 60_000, 2000, 1)
+    text = synth.app5(VARIANTS[name])
+    exp = oracle_out(text, sid, cols, ts)
+    got, _ = product_out(text, sid, cols, ts, splits=(33_333,), nfa_jit=1)
+    if name != "config5":
+        assert len(exp["streams"].get("Out", [])) > 50
+    assert got == exp
