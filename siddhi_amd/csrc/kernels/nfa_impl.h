@@ -87,6 +87,8 @@ struct Lane;
 #define SM_JIT_INL
 #endif
 
+constexpr int kNfaLdsMisc = 5;  // misc words in use (create, bump, space, id counter, initialised)
+
 struct StateLoader {  // OP_VAR loads for a run record
   const Lane* L;
   int rec;
@@ -97,10 +99,20 @@ struct StateLoader {  // OP_VAR loads for a run record
 // lives at base[w * lanes + k]. The 64 lanes of a wave that touch the same per-key state word (list heads,
 // flags, timer queues: fixed offsets) then share cache lines instead of each pulling its own line.
 // stride 1 = the plain key-major layout (the heap).
+#ifdef SM_COUNT_ACCESS
+extern int64_t g_access[2];
+#endif
 struct LaneWords {
   int64_t* p;      // &base[lane]
   int64_t stride;  // lanes per word row
+#ifdef SM_COUNT_ACCESS  // CPU debug build only (tests/native): per-event access mix of key-state words vs heap words
+  int64_t& operator[](int64_t w) const {
+    ++g_access[stride == 1 ? 1 : 0];
+    return p[w * stride];
+  }
+#else
   __device__ __forceinline__ int64_t& operator[](int64_t w) const { return p[w * stride]; }
+#endif
   __device__ __forceinline__ LaneWords at(int64_t w) const { return {p + w * stride, stride}; }
 };
 
@@ -118,7 +130,8 @@ struct Lane {
   const int32_t* PREFS;
 #endif
   // state
-  LaneWords ks;
+  LaneWords ks;   // per-key state words: list heads, flags, post words, misc (LDS-staged under SM_NFA_LDS)
+  LaneWords ksh;  // the same key's words in HBM (timer queues always live there)
   LaneWords heap;
   int32_t half;  // words per semispace
   // batch
@@ -132,7 +145,13 @@ struct Lane {
   int64_t clock;  // EventTimeBasedMillisTimestampGenerator.currentTime() as seen by this lane
 
   // ------------------------------------------------------------ heap
+  // misc words: create position, heap bump, semispace, state-id counter, initialised. Staged (SM_NFA_LDS), they sit
+  // right after the post words.
+#ifdef SM_NFA_LDS
+  __device__ int64_t& misc(int k) const { return ks[PQ->ks_sched + k]; }
+#else
   __device__ int64_t& misc(int k) const { return ks[PQ->ks_misc + k]; }
+#endif
   __device__ int32_t alloc(int words) {
     int64_t space = misc(2);
     int64_t end = (space + 1) * half;
@@ -312,7 +331,7 @@ struct Lane {
   __device__ int64_t& returned(int o) const { return ks[PQ->ks_post + o]; }
 
   // ------------------------------------------------------------ timers (Scheduler FIFO)
-  __device__ LaneWords sq(int s) const { return ks.at(PQ->ks_sched + s * (2 + kSchedCap)); }
+  __device__ LaneWords sq(int s) const { return ksh.at(PQ->ks_sched + s * (2 + kSchedCap)); }
   SM_JIT_INL __device__ void notifyAt(int s, int64_t t) {  // Scheduler.notifyAt :66-74
     LaneWords S = sq(s);
     if (S[1] >= kSchedCap) {
@@ -1184,6 +1203,9 @@ SM_TIMER_ATTR __device__ bool timer_fire(Lane& L, const NfaBatch& b, int64_t a1,
   return true;
 }
 
+struct Lane;
+SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key, int32_t* err_out);
+
 SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
                          int32_t heap_half, int64_t lanes, int32_t key, int32_t* err_out) {
   Lane L;
@@ -1203,6 +1225,7 @@ SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ 
   const DPre* PPRE = L.PPRE;
 #endif
   L.ks = LaneWords{ks_all + key, lanes};
+  L.ksh = L.ks;
   L.half = heap_half;
   // the heap stays key-major: a lane's run records and chain nodes are private, pointer-chased objects, so
   // keeping each object's words in one line beats sharing lines with other lanes' (unrelated) offsets
@@ -1213,6 +1236,34 @@ SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ 
   L.seq = 0;
   L.clock = b.clock_in;
 
+#ifdef SM_NFA_LDS
+  // LDS staging of the lane's per-key state words (north_star: "LDS staging of active partial matches per
+  // workgroup"): the pre / post / misc words every event reads and writes (about 40 accesses per event on
+  // config 5) live in the workgroup's LDS, lane-interleaved (word w of thread t at [w * 64 + t]), for the lane's
+  // whole event run, and go back to HBM once at its end. Timer queues stay in HBM (touched only when a timer is
+  // scheduled or fires). Needs blockDim.x == 64 and (ks_sched + kNfaLdsMisc) words x 64 x 8 B of dynamic LDS.
+  extern __shared__ int64_t sm_nfa_lds[];
+  const int nst = PQ->ks_sched;
+  LaneWords st{sm_nfa_lds + threadIdx.x, 64};
+  for (int w = 0; w < nst; ++w) st[w] = L.ksh[w];
+  for (int k = 0; k < kNfaLdsMisc; ++k) st[nst + k] = L.ksh[PQ->ks_misc + k];
+  L.ks = st;
+#endif
+  nfa_lane_run(L, b, key, err_out);
+#ifdef SM_NFA_LDS
+  for (int w = 0; w < nst; ++w) L.ksh[w] = st[w];
+  for (int k = 0; k < kNfaLdsMisc; ++k) L.ksh[PQ->ks_misc + k] = st[nst + k];
+#endif
+}
+
+// A lane's event run (after its Lane is set up): lane creation, then its events in arrival order with the timers
+// due before each.
+SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key, int32_t* err_out) {
+#ifndef SM_NFA_JIT
+  const DQuery* PQ = L.PQ;
+  const DPre* PPRE = L.PPRE;
+#endif
+  const char* blob = (const char*)PQ;
   const int64_t ebeg = b.key_off[key], eend = b.key_off[key + 1];
   const int64_t W = LaneEv::words(PQ->node_words);
   const bool has_timers = PQ->nsched > 0;

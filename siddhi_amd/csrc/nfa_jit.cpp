@@ -101,10 +101,22 @@ std::string nfa_jit_source(const std::vector<char>& blob) {
   // every member function on the event path inline (A/B: SM_NFA_JIT_INLINE_ALL=0 leaves it to the compiler)
   const char* e = getenv("SM_NFA_JIT_INLINE_ALL");
   if (!e || atoi(e)) src += "#define SM_NFA_JIT_INLINE_ALL 1\n";
+  if (nfa_jit_lds()) src += "#define SM_NFA_LDS 1\n";
   src += blob_array(blob);
   src += kNfaJitBody;
   src += kKernel;
   return src;
+}
+
+bool nfa_jit_lds() {
+  static const char* env = getenv("SM_NFA_JIT_LDS");
+  return !env || atoi(env) != 0;
+}
+
+int64_t nfa_jit_lds_bytes(const std::vector<char>& blob) {
+  if (!nfa_jit_lds()) return 0;
+  const DQuery* q = (const DQuery*)blob.data();
+  return (int64_t)(q->ks_sched + 5) * 64 * 8;  // (pre + post words + kNfaLdsMisc) x 64 lanes
 }
 
 bool nfa_jit_wanted(int option, int64_t records) {
@@ -146,7 +158,7 @@ std::vector<char> nfa_jit_compile(const std::vector<char>& blob) {
 void* nfa_jit_function(const std::vector<char>& blob) {
   int dev = 0;
   SM_HIP(hipGetDevice(&dev));
-  std::string key = std::to_string(dev) + ":" + std::string(blob.begin(), blob.end());
+  std::string key = std::to_string(dev) + ":" + nfa_jit_source(blob);  // the source carries the knobs too
   std::lock_guard<std::mutex> g(g_mu);
   auto it = cache().find(key);
   if (it != cache().end()) return (void*)it->second->fn;
@@ -159,13 +171,13 @@ void* nfa_jit_function(const std::vector<char>& blob) {
   return fn;
 }
 
-void launch_nfa_jit(void* fn, const NfaBatch& b, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
-                    int32_t nkeys, int32_t* err_dev, hipStream_t s) {
+void launch_nfa_jit(void* fn, int64_t lds_bytes, const NfaBatch& b, int64_t* ks, int64_t* heap, int32_t heap_half,
+                    int64_t lanes, int32_t nkeys, int32_t* err_dev, hipStream_t s) {
   if (nkeys <= 0) return;
   NfaBatch bb = b;
   void* args[] = {&bb, &ks, &heap, &heap_half, &lanes, &nkeys, &err_dev};
   const unsigned blocks = (unsigned)((nkeys + 63) / 64);
-  SM_HIP(hipModuleLaunchKernel((hipFunction_t)fn, blocks, 1, 1, 64, 1, 1, 0, s, args, nullptr));
+  SM_HIP(hipModuleLaunchKernel((hipFunction_t)fn, blocks, 1, 1, 64, 1, 1, (unsigned)lds_bytes, s, args, nullptr));
 }
 
 }  // namespace sm

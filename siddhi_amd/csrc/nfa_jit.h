@@ -17,7 +17,10 @@ bool nfa_jit_wanted(int option, int64_t records);
 std::vector<char> nfa_jit_compile(const std::vector<char>& blob);
 // compiled kernel for this plan on the current device (cached per device and plan; throws on compile errors)
 void* nfa_jit_function(const std::vector<char>& blob);
-void launch_nfa_jit(void* fn, const NfaBatch& b, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
-                    int32_t nkeys, int32_t* err_dev, hipStream_t s);
+// dynamic LDS of the kernel (the staged per-key state words of a 64-lane workgroup; 0 when SM_NFA_JIT_LDS=0)
+bool nfa_jit_lds();
+int64_t nfa_jit_lds_bytes(const std::vector<char>& blob);
+void launch_nfa_jit(void* fn, int64_t lds_bytes, const NfaBatch& b, int64_t* ks, int64_t* heap, int32_t heap_half,
+                    int64_t lanes, int32_t nkeys, int32_t* err_dev, hipStream_t s);
 
 }  // namespace sm

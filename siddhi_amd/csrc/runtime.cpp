@@ -820,7 +820,7 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
     b.lane_perm = perm;
   }
   if (nfa_jit_wanted(a->nfa_jit, nq))
-    launch_nfa_jit(nfa_jit_function(q.cq.blob), b, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
+    launch_nfa_jit(nfa_jit_function(q.cq.blob), nfa_jit_lds_bytes(q.cq.blob), b, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
                    (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
   else
     launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,

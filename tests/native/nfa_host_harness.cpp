@@ -326,6 +326,18 @@ void flush(HApp* a) {
 
 }  // namespace
 
+#ifdef SM_COUNT_ACCESS
+namespace sm {
+namespace {
+int64_t g_access[2];
+}
+}  // namespace sm
+extern "C" void h_access(int64_t* out) {
+  out[0] = sm::g_access[0];
+  out[1] = sm::g_access[1];
+}
+#endif
+
 extern "C" {
 
 struct hv {
