@@ -388,7 +388,18 @@ struct Lane {
 
   // ------------------------------------------------------------ selector (QuerySelector.processNoGroupBy)
   SM_JIT_INL __device__ void emit(int32_t rec) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one output-slot claim per wave: the lanes emitting together take consecutive slots (ballot + rank); the
+    // records are put in delivery order afterwards (order_outputs), so slot order carries no meaning
+    const uint64_t m = __ballot(1);
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const uint32_t rank = (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+    uint32_t first = 0;
+    if ((int)__lane_id() == leader) first = atomicAdd(b->out_count, (uint32_t)__popcll(m));
+    const uint32_t idx = (uint32_t)__shfl((int)first, leader, 64) + rank;
+#else
     uint32_t idx = atomicAdd(b->out_count, 1u);
+#endif
     if (idx >= b->out_cap) {
       err |= NFA_ERR_OUTPUT;
       return;
