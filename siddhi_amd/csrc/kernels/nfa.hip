@@ -37,6 +37,32 @@ __global__ void lane_events_kernel(NfaBatch b, int64_t n, const int32_t* __restr
   if (k >= 0) lane_event_record(b, p, k, node_words, out);
 }
 
+// The common record shape (16 words = one 128-byte line): each thread builds the record of its batch position in
+// LDS, then groups of 8 lanes store one record each (8 x 16 B), so a wave's store instruction writes 8 whole lines
+// instead of touching 64 (one 16-byte piece of each of 64 scattered records per instruction).
+constexpr int kLeBlock = 256;
+constexpr int kLeStride = 18;  // words per LDS row: 16 + 2 of padding (rows start on rotating banks)
+__global__ void __launch_bounds__(kLeBlock) lane_events16_kernel(NfaBatch b, int64_t n, const int32_t* __restrict__ inv,
+                                                               int32_t node_words, int64_t* __restrict__ out) {
+  __shared__ int64_t lrec[kLeBlock * kLeStride];
+  __shared__ int32_t lk[kLeBlock];
+  const int tid = threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * kLeBlock + tid;
+  const int32_t k = p < n ? inv[p] : -1;
+  lk[tid] = k;
+  if (k >= 0) lane_event_record(b, p, 0, node_words, lrec + tid * kLeStride);
+  __syncthreads();
+  const int piece = tid & 7;
+#pragma unroll 4
+  for (int r = tid >> 3; r < kLeBlock; r += kLeBlock / 8) {
+    const int32_t kr = lk[r];
+    if (kr >= 0) {
+      const longlong2 v = *(const longlong2*)(lrec + r * kLeStride + 2 * piece);
+      *((longlong2*)(out + (int64_t)kr * 16) + piece) = v;
+    }
+  }
+}
+
 // sort key of slot k: 65535 - min(events of k in this batch, 65535) (descending count)
 __global__ void lane_count_kernel(const int64_t* __restrict__ key_off, int32_t nkeys, uint32_t* __restrict__ ck,
                                   uint32_t* __restrict__ slot) {
@@ -70,8 +96,12 @@ void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_w
   if (nq < n) SM_HIP(hipMemsetAsync(inv_scratch, 0xff, (size_t)n * 4, s));
   hipLaunchKernelGGL(lane_index_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, b.key_pos, nq,
                      inv_scratch);
-  hipLaunchKernelGGL(lane_events_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, n,
-                     (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
+  if (LaneEv::words(node_words) == 16)
+    hipLaunchKernelGGL(lane_events16_kernel, dim3((unsigned)((n + kLeBlock - 1) / kLeBlock)), dim3(kLeBlock), 0, s, b,
+                       n, (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
+  else
+    hipLaunchKernelGGL(lane_events_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, n,
+                       (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
 }
 
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half,
