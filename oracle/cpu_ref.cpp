@@ -118,7 +118,7 @@ struct CExpr {
   AttrType type;  // result type
   Value cval;
   // VAR
-  int chain = -1;  // state slot, or -1 in a stream context
+  int chain = -1;  // state slot, -1 in a stream context, -2 an output attribute (having)
   int idx = kCurrent;
   int attr = -1;
   CmpOp cmp = CmpOp::EQ;
@@ -134,6 +134,7 @@ bool is_numeric(AttrType t) {
 struct EvalCtx {
   const StateEvent* st = nullptr;  // state query
   const Row* row = nullptr;        // single-stream context
+  const std::vector<Value>* outs = nullptr;  // the event's output data (having)
 };
 
 Value eval(const CExpr& e, const EvalCtx& c);
@@ -254,6 +255,7 @@ Value eval(const CExpr& e, const EvalCtx& c) {
     case ExprKind::VAR: {
       // VariableExpressionExecutor.execute :45 → StateEvent.getAttribute :90
       const Row* row = nullptr;
+      if (e.chain == -2) return (*c.outs)[e.attr];  // OUTPUT_DATA_INDEX of the selected event
       if (e.chain < 0) {
         row = c.row;
       } else {
@@ -286,6 +288,10 @@ Value eval(const CExpr& e, const EvalCtx& c) {
     case ExprKind::IS_NULL: {
       Value l = eval(*e.ch[0], c);
       return mkbool(l.null);
+    }
+    case ExprKind::INSTANCE_OF: {  // InstanceOf*FunctionExecutor.execute(Object) :87: data instanceof T
+      Value l = eval(*e.ch[0], c);
+      return mkbool(!l.null && e.ch[0]->type == e.cval.t);
     }
     case ExprKind::CMP: {  // CompareConditionExpressionExecutor.java:39-43; NotEqual: null → true
       Value l = eval(*e.ch[0], c);
@@ -331,6 +337,8 @@ struct ExprCompiler {
   const StreamDef* stream = nullptr;               // stream context
   int current_state = -1;
   int default_index = kCurrent;
+  // HAVING_STATE (ExpressionParser.parseVariable :1242-1275): bare names look in the output definition first
+  const std::vector<std::pair<std::string, AttrType>>* having_outs = nullptr;
 
   CExprP compile(const Expr& x) {
     auto e = std::make_unique<CExpr>();
@@ -361,6 +369,11 @@ struct ExprCompiler {
         return e;
       case ExprKind::IS_NULL:
         e->ch.push_back(compile(*x.ch[0]));
+        e->type = AttrType::BOOL;
+        return e;
+      case ExprKind::INSTANCE_OF:
+        e->ch.push_back(compile(*x.ch[0]));
+        e->cval.t = x.ctype;
         e->type = AttrType::BOOL;
         return e;
       case ExprKind::CMP: {
@@ -394,6 +407,17 @@ struct ExprCompiler {
   }
 
   void resolve_var(const Expr& x, CExpr& e) {
+    if (having_outs && x.stream_ref.empty()) {
+      for (size_t k = 0; k < having_outs->size(); ++k)
+        if ((*having_outs)[k].first == x.attr) {
+          e.chain = -2;
+          e.attr = (int)k;
+          e.type = (*having_outs)[k].second;
+          return;
+        }
+      // a MetaStreamEvent resolves HAVING_STATE names in the output definition only (:1242-1246)
+      if (!metas) throw ValidationError("attribute '" + x.attr + "' is not an output attribute of the query");
+    }
     if (!metas) {  // MetaStreamEvent branch: the stream's own attribute
       int a = stream->index_of(x.attr);
       if (a < 0) throw ValidationError("attribute '" + x.attr + "' is not defined in stream '" + stream->id + "'");
@@ -552,6 +576,7 @@ struct QueryRt {
   int64_t next_state_id = 0;
   // single-stream filter query
   std::vector<CExprP> stream_filters;
+  CExprP having;  // QuerySelector.havingConditionExecutor
   const StreamDef* single_def = nullptr;
   // selector
   std::vector<CExprP> select;
@@ -1171,7 +1196,6 @@ void selector_emit(QueryRt* q, const STP& s) {
   // QuerySelector.processNoGroupBy :124-167 → OutputRateLimiter → QueryCallback / InsertIntoStreamCallback
   OApp* a = q->app;
   const std::string& out = q->q->insert_into;
-  a->stream_count[out]++;
   Output o;
   o.ts = s->timestamp;
   EvalCtx c;
@@ -1183,6 +1207,9 @@ void selector_emit(QueryRt* q, const STP& s) {
       o.refs.push_back(se && se->row ? se->row->ordinal : -1);
     }
   }
+  c.outs = &o.vals;
+  if (q->having && !truthy(eval(*q->having, c))) return;  // :138-139 complexEventChunk.remove()
+  a->stream_count[out]++;
   if (a->collect) {
     a->stream_out[out].push_back(o);
     if (!q->partitioned) a->query_out[q->q->name].calls.push_back({o.ts, {o}});
@@ -1193,7 +1220,6 @@ void selector_emit(QueryRt* q, const STP& s) {
 void selector_emit_row(QueryRt* q, const Row& row, int64_t ts) {
   OApp* a = q->app;
   const std::string& out = q->q->insert_into;
-  a->stream_count[out]++;
   Output o;
   o.ts = ts;
   EvalCtx c;
@@ -1202,6 +1228,9 @@ void selector_emit_row(QueryRt* q, const Row& row, int64_t ts) {
     o.vals.push_back(eval(*q->select[k], c));
     for (size_t v = 0; v < q->select_vars[k].size(); ++v) o.refs.push_back(row.ordinal);
   }
+  c.outs = &o.vals;
+  if (q->having && !truthy(eval(*q->having, c))) return;  // QuerySelector.java:138-139
+  a->stream_count[out]++;
   if (a->collect) {
     a->stream_out[out].push_back(o);
     if (!q->partitioned) a->query_out[q->q->name].calls.push_back({o.ts, {o}});
@@ -1458,6 +1487,26 @@ void inner_update(Inner* in) {
   }
 }
 
+// SelectorParser.generateHavingExecutor :214-228 (parsed against the output definition, HAVING_STATE)
+void compile_having(QueryRt* q, const Query& qd, ExprCompiler& ec) {
+  if (!qd.having) return;
+  std::vector<std::pair<std::string, AttrType>> outs;
+  if (qd.select_all) {
+    if (q->single_def) {
+      for (auto& at : q->single_def->attrs) outs.push_back({at.name, at.type});
+    } else {
+      for (auto& m : q->metas)
+        for (auto& at : m.def->attrs) outs.push_back({at.name, at.type});
+    }
+  } else {
+    for (size_t k = 0; k < qd.select.size(); ++k) outs.push_back({qd.select[k].rename, q->select[k]->type});
+  }
+  ec.having_outs = &outs;
+  q->having = ec.compile(*qd.having);
+  ec.having_outs = nullptr;
+  if (q->having->type != AttrType::BOOL) throw ValidationError("having condition should be of type BOOL");
+}
+
 std::unique_ptr<QueryRt> build_query(OApp* app, const Query& qd, int order_index) {
   auto q = std::make_unique<QueryRt>();
   q->app = app;
@@ -1492,6 +1541,7 @@ std::unique_ptr<QueryRt> build_query(OApp* app, const Query& qd, int order_index
         q->select_vars.push_back(vars);
       }
     }
+    compile_having(q.get(), qd, ec);
     return q;
   }
   q->sequence = (qd.input == InputKind::SEQUENCE);
@@ -1544,6 +1594,7 @@ std::unique_ptr<QueryRt> build_query(OApp* app, const Query& qd, int order_index
     walk(q->select.back().get());
     q->select_vars.push_back(vars);
   }
+  compile_having(q.get(), qd, ec);
   // QueryRuntime constructor → init() → StateStreamRuntime.setCommonProcessor :71-75
   inner_setQuerySelector(q->inner.get());
   inner_setStartState(q->inner.get());

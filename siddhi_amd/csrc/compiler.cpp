@@ -99,6 +99,28 @@ struct Emitter {
         code.push_back(in);
         return T_BOOL;
       }
+      case ExprKind::INSTANCE_OF: {
+        // InstanceOf*FunctionExecutor.execute(Object data): `data instanceof T`. An executor's value has its
+        // static type (or is null), so the test is "not null" when the types agree and false otherwise.
+        const size_t mark = code.size();
+        if (emit(*x.ch[0]) == (int)x.ctype) {
+          in.op = OP_ISNULL;
+          code.push_back(in);
+          Instr n{};
+          n.op = OP_NOT;
+          code.push_back(n);
+        } else {
+          code.resize(mark);  // the argument's value is never read (its references still count as refs)
+          DVal v{};
+          v.i = 0;
+          in.op = OP_CONST;
+          in.a = (int)consts.size();
+          in.t0 = T_BOOL;
+          consts.push_back(v);
+          code.push_back(in);
+        }
+        return T_BOOL;
+      }
       case ExprKind::CMP: {
         int a = emit(*x.ch[0]);
         int b = emit(*x.ch[1]);
@@ -201,6 +223,34 @@ struct Emitter {
     return in.t0;
   }
 };
+
+// having (SelectorParser.generateHavingExecutor :214-228 → ExpressionParser.parseVariable with HAVING_STATE
+// :1242-1275): a bare attribute name resolves to the query's output attribute first, and only when the output
+// has no such attribute to the input events (state input) or nowhere (single-stream input: the output stream
+// definition only). The output attribute's value is its select expression's value on the same event (the
+// select is a pure function of the event), so the device program evaluates that expression in its place.
+using OutAttrs = std::vector<std::pair<std::string, const Expr*>>;
+ExprP having_subst(const Expr& x, const OutAttrs& outs, bool outputs_only) {
+  if (x.kind == ExprKind::VAR && x.stream_ref.empty()) {
+    for (auto& o : outs)
+      if (o.first == x.attr) return having_subst(*o.second, {}, false);
+    if (outputs_only) throw ValidationError("attribute '" + x.attr + "' is not an output attribute of the query");
+  }
+  auto e = std::make_unique<Expr>();
+  e->kind = x.kind;
+  e->ctype = x.ctype;
+  e->cnull = x.cnull;
+  e->ival = x.ival;
+  e->dval = x.dval;
+  e->sval = x.sval;
+  e->stream_ref = x.stream_ref;
+  e->index = x.index;
+  e->attr = x.attr;
+  e->cmp = x.cmp;
+  e->math = x.math;
+  for (auto& c : x.ch) e->ch.push_back(having_subst(*c, outs, outputs_only));
+  return e;
+}
 
 struct Lowering {
   const App& app;
@@ -425,6 +475,28 @@ CompiledQuery compile_query(const App& app, const Query& q, int order, int parti
         code.push_back(a);
       }
     }
+    if (q.having) {
+      OutAttrs outs;
+      std::vector<Expr> star;
+      if (q.select_all) {
+        star.resize(def->attrs.size());
+        for (size_t k = 0; k < def->attrs.size(); ++k) {
+          star[k].kind = ExprKind::VAR;
+          star[k].attr = def->attrs[k].name;
+          outs.push_back({def->attrs[k].name, &star[k]});
+        }
+      } else {
+        for (auto& oa : q.select) outs.push_back({oa.rename, oa.expr.get()});
+      }
+      // QuerySelector drops the event after projection; with no aggregation that is one more filter
+      if (em.emit(*having_subst(*q.having, outs, true)) != T_BOOL)
+        throw ValidationError("having condition should be of type BOOL");
+      if (!q.filters.empty()) {
+        Instr a{};
+        a.op = OP_AND;
+        code.push_back(a);
+      }
+    }
     h.filt_len = (int)code.size() - h.filt_off;
     std::vector<std::pair<int, int>> vr;
     em.var_refs = &vr;
@@ -587,6 +659,16 @@ CompiledQuery compile_query(const App& app, const Query& q, int order, int parti
       refs.push_back(r.first);
       refs.push_back(r.second);
     }
+    if (q.having) {  // evaluated on the run record before the output is written (nfa_impl.h emit)
+      OutAttrs outs;
+      if (!q.select_all)
+        for (auto& oa : q.select) outs.push_back({oa.rename, oa.expr.get()});
+      em.var_refs = nullptr;
+      h.having_off = (int)lw.code.size();
+      if (em.emit(*having_subst(*q.having, outs, false)) != T_BOOL)
+        throw ValidationError("having condition should be of type BOOL");
+      h.having_len = (int)lw.code.size() - h.having_off;
+    }
     for (auto& p : lw.pres)
       if (p.kind == PK_ABSENT_STREAM || p.kind == PK_ABSENT_LOGICAL) cq.has_absent = true;
     if (cq.has_absent && !app.playback)
@@ -614,7 +696,7 @@ CompiledQuery compile_query(const App& app, const Query& q, int order, int parti
         root_el->a->kind == StateKind::EVERY && root_el->a->a->kind == StateKind::STREAM && !root_el->a->has_within &&
         !root_el->a->a->has_within && root_el->b->kind == StateKind::STREAM &&
         root_el->a->a->stream_id == root_el->b->stream_id && h.nslots == 2) {
-      bool ok = true;
+      bool ok = !q.having;  // the closed form writes every match
       // selects may use any position; the closed form gives each output's e1/e2 single events
       for (size_t k = 0; k < refs.size(); k += 2)
         if (!(refs[k + 1] == 0 || refs[k + 1] == kCurrent)) ok = false;

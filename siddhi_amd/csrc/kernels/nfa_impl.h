@@ -388,6 +388,10 @@ struct Lane {
 
   // ------------------------------------------------------------ selector (QuerySelector.processNoGroupBy)
   SM_JIT_INL __device__ void emit(int32_t rec) {
+    if (PQ->having_len > 0) {  // QuerySelector.processNoGroupBy :138-139: the having condition drops the output
+      StateLoader hl{this, rec};
+      if (!truthy(eval_prog(PCODE + PQ->having_off, PQ->having_len, PCONSTS, hl))) return;
+    }
 #if defined(__HIP_DEVICE_COMPILE__)
     // one output-slot claim per wave: the lanes emitting together take consecutive slots (ballot + rank); the
     // records are put in delivery order afterwards (order_outputs), so slot order carries no meaning

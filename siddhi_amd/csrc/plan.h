@@ -132,6 +132,9 @@ struct DQuery {
   int32_t ks_post;      // per post: 1 word (isEventReturned)
   int32_t ks_sched;     // per scheduler: 2 + kSchedCap words (head, count, ring)
   int32_t ks_misc;      // create position, heap bump, semispace, state-id counter
+  // state query: having condition (QuerySelector.java:138-139) over the run record, output attributes
+  // substituted by their select programs; having_len 0 = none. A single-stream query ANDs it into filt.
+  int32_t having_off, having_len;
 };
 constexpr int kSchedCap = 32;
 constexpr int kPreWords = 6;

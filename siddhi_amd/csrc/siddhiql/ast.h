@@ -66,7 +66,8 @@ struct StreamDef {
   }
 };
 
-enum class ExprKind { CONST, VAR, AND, OR, NOT, CMP, MATH, IS_NULL };
+// INSTANCE_OF: instanceOf<Type>(x) (core/executor/function/InstanceOf*FunctionExecutor.java); ctype = the tested type
+enum class ExprKind { CONST, VAR, AND, OR, NOT, CMP, MATH, IS_NULL, INSTANCE_OF };
 enum class CmpOp { EQ, NE, LT, LE, GT, GE };
 enum class MathOp { ADD, SUB, MUL, DIV, MOD };
 
@@ -127,6 +128,7 @@ struct Query {
   // selection
   bool select_all = false;
   std::vector<OutputAttr> select;
+  ExprP having;  // query_section 'having' (SiddhiQL.g4 having: HAVING expression); null = none
   std::string insert_into;  // output stream
   int output_event_type = 0;  // 0 = current events (only supported type)
 };

@@ -106,6 +106,11 @@ void expr(std::ostringstream& o, const Expr* e) {
       expr(o, e->ch[0].get());
       o << "}";
       return;
+    case ExprKind::INSTANCE_OF:
+      o << "{\"instanceof\":\"" << attr_type_name(e->ctype) << "\",\"arg\":";
+      expr(o, e->ch[0].get());
+      o << "}";
+      return;
     default:
       o << "{\"isnull\":";
       expr(o, e->ch[0].get());
@@ -199,6 +204,10 @@ void query(std::ostringstream& o, const Query& q) {
       o << "}";
     }
     o << "]";
+  }
+  if (q.having) {
+    o << ",\"having\":";
+    expr(o, q.having.get());
   }
   o << ",\"insert_into\":";
   jstr(o, q.insert_into);

@@ -372,7 +372,8 @@ struct Parser {
       return e;
     }
     if (peek().t == Tk::ID) {
-      if (is_sym("(", 1) || (is_sym(":", 1) && peek(2).t == Tk::ID && is_sym("(", 3)))
+      if (is_sym("(", 1)) return function_call();
+      if (is_sym(":", 1) && peek(2).t == Tk::ID && is_sym("(", 3))
         throw UnsupportedError("function calls are outside the hot-path subset: '" + peek().s + "'");
       // attribute_reference: name1 ('[' attribute_index ']')? '.' attribute_name | attribute_name
       auto e = mk(ExprKind::VAR);
@@ -392,6 +393,34 @@ struct Parser {
       return e;
     }
     fail("expected expression");
+  }
+  // function_operation (SiddhiQL.g4 function_operation: function_id '(' attribute_list? ')'). Of the built-in
+  // functions only the instanceOf* type tests are in the subset (core/executor/function/
+  // InstanceOf{Boolean,Double,Float,Integer,Long,String}FunctionExecutor.java: exactly one argument, BOOL result).
+  ExprP function_call() {
+    static const std::pair<const char*, AttrType> kInstanceOf[] = {
+        {"instanceOfBoolean", AttrType::BOOL}, {"instanceOfDouble", AttrType::DOUBLE},
+        {"instanceOfFloat", AttrType::FLOAT},  {"instanceOfInteger", AttrType::INT},
+        {"instanceOfLong", AttrType::LONG},    {"instanceOfString", AttrType::STRING}};
+    const std::string name = tk[p].s;
+    for (auto& f : kInstanceOf) {
+      if (name != f.first) continue;
+      p += 2;  // name '('
+      std::vector<ExprP> args;
+      if (!is_sym(")")) {
+        do args.push_back(expr());
+        while (accept_sym(","));
+      }
+      expect_sym(")");
+      if (args.size() != 1)
+        throw ValidationError("Invalid no of arguments passed to " + name + "() function, required only 1, but found " +
+                              std::to_string(args.size()));
+      auto e = mk(ExprKind::INSTANCE_OF);
+      e->ctype = f.second;
+      e->ch.push_back(std::move(args[0]));
+      return e;
+    }
+    throw UnsupportedError("function calls are outside the hot-path subset: '" + name + "'");
   }
   int attribute_index() {
     // visitAttribute_index (SiddhiQLBaseVisitorImpl.java:2323-2334): LAST → -2, LAST - k → -2 - k
@@ -682,7 +711,7 @@ struct Parser {
       // left/right_absent_sequence_source (SiddhiQL.g4:312-326): absent elements need a present one
       if (all_absent(q.state.get())) fail("an absent sequence needs at least one present (non-absent) element");
     }
-    // query_section: select ... (group by / having / order by / limit are out of scope)
+    // query_section: select ... [having ...] (group by / order by / limit are out of scope)
     if (accept_kw("select")) {
       if (accept_sym("*")) {
         q.select_all = true;
@@ -696,8 +725,11 @@ struct Parser {
           q.select.push_back(std::move(oa));
         } while (accept_sym(","));
       }
-      if (is_kw("group") || is_kw("having") || is_kw("order") || is_kw("limit"))
-        throw UnsupportedError("group by / having / order by / limit are outside the hot-path subset");
+      if (is_kw("group")) throw UnsupportedError("group by is outside the hot-path subset");
+      // having: a condition over the output attributes and the input events (QuerySelector.java:138-139)
+      if (accept_kw("having")) q.having = expr();
+      if (is_kw("order") || is_kw("limit"))
+        throw UnsupportedError("order by / limit are outside the hot-path subset");
     } else {
       q.select_all = true;
     }
