@@ -353,11 +353,24 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ evaluation
-  __device__ bool filter_pass(int p, int32_t rec) const {
+  SM_JIT_INL __device__ bool filter_pass(int p, int32_t rec) const {
+#ifdef SM_NFA_JIT_INLINE_ALL
+    // plan-constant dispatch: each pre processor's program is evaluated with a constant length, so it unrolls and
+    // its operand stack lives in registers (a dynamic-length evaluation keeps the stack in scratch)
+    bool pass = true;
+#pragma unroll
+    for (int q = 0; q < PQ->npre; ++q)
+      if (q == p && PPRE[q].progLen != 0) {
+        StateLoader ld{this, rec};
+        pass = truthy(eval_prog(PCODE + PPRE[q].progOff, PPRE[q].progLen, PCONSTS, ld));
+      }
+    return pass;
+#else
     const DPre& P = PPRE[p];
     if (P.progLen == 0) return true;
     StateLoader ld{this, rec};
     return truthy(eval_prog(PCODE + P.progOff, P.progLen, PCONSTS, ld));
+#endif
   }
   __device__ bool is_absent(int p) const { return PPRE[p].kind == PK_ABSENT_STREAM || PPRE[p].kind == PK_ABSENT_LOGICAL; }
 
@@ -421,6 +434,7 @@ struct Lane {
     o->key = key;
     DVal* vals = (DVal*)(base + sizeof(OutRec));
     StateLoader ld{this, rec};
+    SM_EXPR_UNROLL
     for (int k = 0; k < PQ->nsel; ++k) {
       StackVal v = eval_prog(PCODE + PSEL[3 * k], PSEL[3 * k + 1], PCONSTS, ld);
       if (PSEL[3 * k + 2] == T_FLOAT || PSEL[3 * k + 2] == T_DOUBLE) vals[k].d = v.d;
@@ -1191,7 +1205,9 @@ __device__ __forceinline__ int64_t adv_after(const NfaBatch& b, int64_t from, in
 
 // The rare part of a lane's timer loop: find the advance point where the earliest timer falls due and fire the
 // timers there. Out of line (SM_TIMER_INLINE undoes it, A/B), so that its registers stay off the per-event path.
-#ifdef SM_TIMER_INLINE
+#if defined(SM_NFA_JIT_INLINE_ALL)
+#define SM_TIMER_ATTR SM_NFA_ALWAYS_INLINE  // JIT: the Lane must not escape into a call (it would live in scratch)
+#elif defined(SM_TIMER_INLINE)
 #define SM_TIMER_ATTR
 #else
 #define SM_TIMER_ATTR __attribute__((noinline))
