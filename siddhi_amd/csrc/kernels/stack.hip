@@ -41,7 +41,10 @@ constexpr int kSW = kSB / 64;  // budget keeps both stacks and the slice machine
 constexpr int kKeys = 1024;    // in-bucket keys
 constexpr int kSI = 8;         // records per thread per slice
 constexpr int kS = kSB * kSI;  // slice: 4096 records
-constexpr int kC = 6;          // stack entries held in registers
+#ifndef SM_STACK_KC
+#define SM_STACK_KC 6           // A/B build flag
+#endif
+constexpr int kC = SM_STACK_KC; // stack entries held in registers
 constexpr int kQ = 32;         // spilled entries per thread (HBM ring)
 constexpr int kLog = 4096;     // match log of a slice: kLog / H entries per key thread ...
 constexpr int kOvf = 1024;     // ... and a shared overflow (more: the batch takes the sort / walk kernels)

@@ -128,7 +128,7 @@ struct DQuery {
   int32_t filt_off, filt_len;
   // per-key state layout (words of int64 per key)
   int32_t ks_words;
-  int32_t ks_pre;       // per pre: 6 words (pendHead|pendTail, newHead|newTail, flags, lastArrival, spare, spare)
+  int32_t ks_pre;       // per pre: 5 words (pendHead|pendTail, newHead|newTail, flags, lastArrival, absent list)
   int32_t ks_post;      // per post: 1 word (isEventReturned)
   int32_t ks_sched;     // per scheduler: 2 + kSchedCap words (head, count, ring)
   int32_t ks_misc;      // create position, heap bump, semispace, state-id counter
@@ -137,7 +137,7 @@ struct DQuery {
   int32_t having_off, having_len;
 };
 constexpr int kSchedCap = 32;
-constexpr int kPreWords = 6;
+constexpr int kPreWords = 5;
 
 // pre flags (bit set in the flags word)
 enum : int64_t { F_STATE_CHANGED = 1, F_INITIALIZED = 2, F_SUCCESS = 4, F_START_RESET = 8, F_ACTIVE = 16 };
