@@ -724,7 +724,12 @@ CompiledQuery compile_query(const App& app, const Query& q, int order, int parti
   h.nconst = (int)consts.size();
   // per-key state layout (int64 words)
   h.ks_pre = 0;
-  h.ks_post = h.ks_pre + h.npre * kPreWords;
+  int32_t kso = h.ks_pre;
+  for (auto& p : pres) {
+    p.ksOff = kso;
+    kso += (p.kind == PK_ABSENT_STREAM || p.kind == PK_ABSENT_LOGICAL) ? kPreWordsAbsent : kPreWords;
+  }
+  h.ks_post = kso;
   h.ks_sched = h.ks_post + h.npost;
   h.ks_misc = h.ks_sched + h.nsched * (2 + kSchedCap);
   h.ks_words = h.ks_misc + 8;

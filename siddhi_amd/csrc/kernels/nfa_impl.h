@@ -87,7 +87,7 @@ struct Lane;
 #define SM_JIT_INL
 #endif
 
-constexpr int kNfaLdsMisc = 5;  // misc words in use (create, bump, space, id counter, initialised)
+constexpr int kNfaLdsMisc = 4;  // misc words staged (create, bump, space, id counter; 'initialised' stays in HBM)
 
 struct StateLoader {  // OP_VAR loads for a run record
   const Lane* L;
@@ -148,7 +148,7 @@ struct Lane {
   // misc words: create position, heap bump, semispace, state-id counter, initialised. Staged (SM_NFA_LDS), they sit
   // right after the post words.
 #ifdef SM_NFA_LDS
-  __device__ int64_t& misc(int k) const { return ks[PQ->ks_sched + k]; }
+  __device__ __forceinline__ int64_t& misc(int k) const { return k < kNfaLdsMisc ? ks[PQ->ks_sched + k] : ksh[PQ->ks_misc + k]; }
 #else
   __device__ int64_t& misc(int k) const { return ks[PQ->ks_misc + k]; }
 #endif
@@ -263,7 +263,9 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ lists (LinkedList<StateEvent>)
-  __device__ int64_t& lw(int p, int which) const { return ks[PQ->ks_pre + p * kPreWords + which]; }
+  // which: 0 pending list, 1 newAndEvery list, 2 flags, 3 the list processAndReturn returns; absent pres only:
+  // 4 lastArrival
+  __device__ int64_t& lw(int p, int which) const { return ks[PPRE[p].ksOff + which]; }
   __device__ int32_t lhead(int p, int w) const { return (int32_t)lw(p, w); }
   __device__ int32_t ltail(int p, int w) const { return (int32_t)(lw(p, w) >> 32); }
   __device__ void lset(int p, int w, int32_t h, int32_t t) const {
@@ -327,7 +329,7 @@ struct Lane {
     if (v) flags(p) |= f;
     else flags(p) &= ~f;
   }
-  __device__ int64_t& lastArrival(int p) const { return lw(p, 3); }
+  __device__ int64_t& lastArrival(int p) const { return lw(p, 4); }
   __device__ int64_t& returned(int o) const { return ks[PQ->ks_post + o]; }
 
   // ------------------------------------------------------------ timers (Scheduler FIFO)
@@ -636,11 +638,11 @@ struct Lane {
   }
 
   // processAndReturn of every pre kind; returned records are appended to the temporary list `ret`
-  // (list words kept in ks slots 4/5 of the pre: the selector runs after the loop, as in the receivers).
+  // (the pre's list word 3: the selector runs after the loop, as in the receivers).
   SM_INL_PAR __device__ void processAndReturn(int p, int32_t evnode, int64_t now) {
     const DPre& P = PPRE[p];
     const int sid = P.stateId;
-    lclear(p, 4 - 0);  // ret list lives in word 4 (head|tail); word 5 spare
+    lclear(p, 3);
     switch (P.kind) {
       case PK_STREAM:
       case PK_ABSENT_STREAM: {
@@ -658,7 +660,7 @@ struct Lane {
           int tl = P.thisLast;
           if (returned(tl)) {
             returned(tl) = 0;
-            lappend(p, 4, s);
+            lappend(p, 3, s);
           }
           if (fl(p, F_STATE_CHANGED)) {
             ln = lerase(p, 0, prev, ln);
@@ -673,7 +675,7 @@ struct Lane {
             if (cb >= 0) count_startStateReset(cb);
           }
         }
-        if (P.kind == PK_ABSENT_STREAM) lclear(p, 4);  // AbsentStreamPreStateProcessor.processAndReturn :218-231
+        if (P.kind == PK_ABSENT_STREAM) lclear(p, 3);  // AbsentStreamPreStateProcessor.processAndReturn :218-231
         return;
       }
       case PK_COUNT: {  // CountPreStateProcessor.processAndReturn :58-93
@@ -691,7 +693,7 @@ struct Lane {
           int tl = P.thisLast;
           if (returned(tl)) {
             returned(tl) = 0;
-            lappend(p, 4, s);
+            lappend(p, 3, s);
           }
           bool removed = false;
           if (fl(p, F_STATE_CHANGED)) {
@@ -735,7 +737,7 @@ struct Lane {
           int tl = P.thisLast;
           if (returned(tl)) {
             returned(tl) = 0;
-            lappend(p, 4, s);
+            lappend(p, 3, s);
           }
           if (fl(p, F_STATE_CHANGED)) {
             ln = lerase(p, 0, prev, ln);
@@ -915,7 +917,7 @@ struct Lane {
     if (!fl(p, F_ACTIVE)) return;
     bool notProcessed = true;
     const int sid = P.stateId;
-    lclear(p, 4);
+    lclear(p, 3);
     if (now >= lastArrival(p) + P.waitingTime) {
       if (P.kind == PK_ABSENT_STREAM) {
         bool initialize = P.isStart && lempty(p, 1) && lempty(p, 0);
@@ -942,7 +944,7 @@ struct Lane {
           if (now >= rts(s) + P.waitingTime) {
             ln = lerase(p, 0, prev, ln);
             rts(s) = now;
-            lappend(p, 4, s);
+            lappend(p, 3, s);
             continue;
           }
         } else {
@@ -953,9 +955,9 @@ struct Lane {
             bool partner_has = slot(s, PPRE[P.partner].stateId) >= 0;
             if (P.ltype == LT_OR && !partner_has) {
               add_event(s, sid, empty_node());
-              lappend(p, 4, s);
+              lappend(p, 3, s);
             } else if (P.ltype == LT_AND && partner_has) {
-              lappend(p, 4, s);
+              lappend(p, 3, s);
             } else if (P.ltype == LT_AND && !partner_has) {
               add_event(s, sid, empty_node());
             }
@@ -965,9 +967,9 @@ struct Lane {
         prev = ln;
         ln = ln_next(ln);
       }
-      notProcessed = lempty(p, 4);
-      for (int32_t ln = lhead(p, 4); ln >= 0; ln = ln_next(ln)) absent_sendEvent(p, ln_rec(ln));
-      lclear(p, 4);
+      notProcessed = lempty(p, 3);
+      for (int32_t ln = lhead(p, 3); ln >= 0; ln = ln_next(ln)) absent_sendEvent(p, ln_rec(ln));
+      lclear(p, 3);
       lastArrival(p) = 0;
     }
     const DPost& TP = PPOST[P.post];
@@ -1054,15 +1056,15 @@ struct Lane {
       int pp = R->procs[k];
       processAndReturn(pp, ev, now);
       if (err) return;
-      if (!lempty(pp, 4)) {
+      if (!lempty(pp, 3)) {
         if (!R->hasQuerySelector && !R->multi) {
           err |= NFA_ERR_NPE;
           return;
         }
         if (R->hasQuerySelector)
-          for (int32_t ln = lhead(pp, 4); ln >= 0; ln = ln_next(ln)) emit(ln_rec(ln));
+          for (int32_t ln = lhead(pp, 3); ln >= 0; ln = ln_next(ln)) emit(ln_rec(ln));
       }
-      lclear(pp, 4);
+      lclear(pp, 3);
     }
   }
 
@@ -1306,8 +1308,8 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
       L.lset(p, 0, -1, -1);
       L.lset(p, 1, -1, -1);
       L.flags(p) = F_ACTIVE;
-      L.lastArrival(p) = 0;
-      L.lset(p, 4, -1, -1);
+      L.lset(p, 3, -1, -1);
+      if (L.is_absent(p)) L.lastArrival(p) = 0;
     }
     for (int o = 0; o < PQ->npost; ++o) L.returned(o) = 0;
     for (int s = 0; s < PQ->nsched; ++s) {

@@ -75,7 +75,7 @@ struct DPre {
   int32_t post, thisLast, partner;
   int32_t minCount, maxCount, ltype;
   int32_t sched;             // scheduler index or -1
-  int32_t pad;
+  int32_t ksOff;             // first of its per-key state words (kPreWords, or kPreWordsAbsent for an absent pre)
   int64_t waitingTime;       // absent: 'for' time, -1 when absent (logical 'and not X' without for)
 };
 
@@ -128,7 +128,8 @@ struct DQuery {
   int32_t filt_off, filt_len;
   // per-key state layout (words of int64 per key)
   int32_t ks_words;
-  int32_t ks_pre;       // per pre: 5 words (pendHead|pendTail, newHead|newTail, flags, lastArrival, absent list)
+  int32_t ks_pre;       // per pre (DPre.ksOff): pendHead|pendTail, newHead|newTail, flags, the returned list of
+                        // processAndReturn; an absent pre also lastArrival (only absent processors read it)
   int32_t ks_post;      // per post: 1 word (isEventReturned)
   int32_t ks_sched;     // per scheduler: 2 + kSchedCap words (head, count, ring)
   int32_t ks_misc;      // create position, heap bump, semispace, state-id counter
@@ -137,7 +138,8 @@ struct DQuery {
   int32_t having_off, having_len;
 };
 constexpr int kSchedCap = 32;
-constexpr int kPreWords = 5;
+constexpr int kPreWords = 4;
+constexpr int kPreWordsAbsent = 5;
 
 // pre flags (bit set in the flags word)
 enum : int64_t { F_STATE_CHANGED = 1, F_INITIALIZED = 2, F_SUCCESS = 4, F_START_RESET = 8, F_ACTIVE = 16 };
