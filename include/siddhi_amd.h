@@ -20,6 +20,8 @@
  *                                   query callback sees (QueryCallback.receive, query/output/callback/
  *                                   QueryCallback.java:51): no Java counterpart, one JVM has one output queue
  *   sm_app_copy_device_matches      the device tuples of the last batch into a caller buffer (for collectives)
+ *   sm_app_device_project           QuerySelector.processNoGroupBy (query/selector/QuerySelector.java:124-167) for
+ *                                   those tuples, on the device: Event.data + timestamp of each output
  *   sm_compile_dump                 SiddhiCompiler.parse (siddhi-query-compiler .../SiddhiCompiler.java:56)
  *   sm_nfa_jit_compile              QueryParser.parse (core/util/parser/QueryParser.java:79) for one query, as the
  *                                   query-specialised NFA kernel (no device needed): the build check of the JIT
@@ -172,6 +174,25 @@ int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** 
  * cap_bytes on hip_stream (asynchronous); *n = tuples. Lets a caller hand them to its own collectives. */
 int sm_app_copy_device_matches(sm_app* app, const char* query_name, void* d_dst, size_t cap_bytes, size_t* n,
                                void* hip_stream);
+/* One value of a device-side output event: INT / LONG / BOOL / STRING (dictionary id) in i, FLOAT / DOUBLE (FLOAT
+ * widened) in d. */
+typedef struct sm_dval {
+  union {
+    int64_t i;
+    double d;
+  };
+  int32_t is_null;
+  int32_t pad;
+} sm_dval;
+/* QuerySelector.processNoGroupBy (query/selector/QuerySelector.java:124-167) on the device for the outputs of the
+ * last device batch of an `every e1 -> e2 within T` query that took the closed form: output k (the k-th tuple of
+ * sm_app_device_matches) gets its select list in d_values[k * nsel .. k * nsel + nsel) and its timestamp (e2's event
+ * time, StateEvent.timestamp) in d_ts[k] (d_ts may be NULL). An e1 carried from an earlier batch is read from the
+ * carried partial. With d_values == NULL only *n and *nsel are set. The batch's columns, event times and ordinals
+ * are read again: call it before freeing them. SM_E_UNSUPPORTED for filter queries and for batches the NFA kernel
+ * took (their outputs reach the callbacks as Event data). */
+int sm_app_device_project(sm_app* app, const char* query_name, sm_dval* d_values, size_t cap_values, int64_t* d_ts,
+                          size_t* n, int32_t* nsel, void* hip_stream);
 /* Diagnostics of the last device batch: "fast_path:<query>" (2 = onesweep kernels, 1 = general kernels),
  * "fast_ms:group" / "fast_ms:walk" / "fast_ms:order" (phase times in ms; needs the "fast_timing" option). */
 int sm_app_get_stat(sm_app* app, const char* key, double* out);

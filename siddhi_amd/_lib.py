@@ -21,7 +21,7 @@ EXPORTS = [
     "sm_app_add_stream_callback", "sm_app_add_query_callback", "sm_app_set_collect", "sm_app_dump_outputs",
     "sm_app_set_option", "sm_app_process_device_batch", "sm_app_process_device_events", "sm_app_device_matches",
     "sm_app_snapshot", "sm_app_restore", "sm_partition_by_owner", "sm_order_matches", "sm_app_copy_device_matches",
-    "sm_app_get_stat", "sm_compile_dump", "sm_nfa_jit_compile",
+    "sm_app_get_stat", "sm_compile_dump", "sm_nfa_jit_compile", "sm_app_device_project",
 ]
 
 
@@ -78,6 +78,7 @@ def lib():
         L.sm_app_snapshot.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.sm_app_restore.argtypes = [vp, ctypes.c_char_p, sz]
         L.sm_app_device_matches.argtypes = [vp, cp, ctypes.POINTER(vp), ctypes.POINTER(sz)]
+        L.sm_app_device_project.argtypes = [vp, cp, vp, sz, vp, ctypes.POINTER(sz), ctypes.POINTER(ctypes.c_int32), vp]
         L.sm_app_get_stat.argtypes = [vp, cp, ctypes.POINTER(ctypes.c_double)]
         L.sm_compile_dump.argtypes = [cp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.sm_nfa_jit_compile.argtypes = [cp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.POINTER(sz)]

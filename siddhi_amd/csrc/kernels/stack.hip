@@ -1032,4 +1032,106 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
   return M;
 }
 
+// ---- on-device projection of the closed form's outputs (QuerySelector.processNoGroupBy :124-167): output k is
+// the match (e1, e2) = pairs[k]; its select programs read slot 0 (e1) and slot 1 (e2) of the batch, or for an e1
+// carried from an earlier batch (negative relative ordinal) that partial's carry row (canonical attribute words)
+namespace {
+struct ProjLoader {
+  const NfaStream* st;
+  int64_t r1, r2;     // batch rows
+  const int64_t* c1;  // e1's carry row, or nullptr
+  __device__ StackVal var(const Instr& in) const {
+    if (in.a == 0 && c1) {
+      StackVal v = uncanon((uint64_t)c1[3 + in.c], in.t0);
+      if (in.t0 == T_STRING) v.null = v.i < 0;
+      return v;
+    }
+    return col_value(st, in.c, in.a == 0 ? r1 : r2);
+  }
+};
+
+__device__ __forceinline__ int64_t batch_row(const int64_t* ord, int64_t n, int64_t base, uint32_t rel) {
+  if (!ord) return (int64_t)rel;
+  const int64_t want = base + (int64_t)rel;
+  int64_t lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (ord[mid] < want) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void carry_ord_keys_kernel(const int64_t* __restrict__ rows, int64_t n, int w, int64_t base,
+                                      uint32_t* __restrict__ key, uint32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  key[i] = (uint32_t)(rows[i * w + 1] - base + 0x80000000ll);  // carried ordinals lie in [base - 2^31, base)
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void pair_project_kernel(const uint32_t* __restrict__ pairs, int64_t m, const NfaStream* __restrict__ st,
+                                    const int64_t* __restrict__ ord, int64_t n, int64_t base,
+                                    const int64_t* __restrict__ ts, const int64_t* __restrict__ crow, int cw,
+                                    const uint32_t* __restrict__ ckey, const uint32_t* __restrict__ cidx, int64_t nc,
+                                    const char* __restrict__ blob, DVal* __restrict__ out, int64_t* __restrict__ ts_out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  const DQuery* q = (const DQuery*)blob;
+  const Instr* code = (const Instr*)(blob + q->off_code);
+  const DVal* consts = (const DVal*)(blob + q->off_const);
+  const int32_t* sel = (const int32_t*)(blob + q->off_sel);
+  const uint32_t e1 = pairs[2 * k], e2 = pairs[2 * k + 1];
+  ProjLoader ld{st, 0, batch_row(ord, n, base, e2), nullptr};
+  if ((int32_t)e1 < 0) {  // carried e1: its row in the previous carry, by ordinal
+    const uint32_t want = (uint32_t)((int32_t)e1 + 0x80000000ll);
+    int64_t lo = 0, hi = nc - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ckey[mid] < want) lo = mid + 1;
+      else hi = mid;
+    }
+    ld.c1 = crow + (int64_t)cidx[lo] * cw;
+  } else {
+    ld.r1 = batch_row(ord, n, base, e1);
+  }
+  DVal* o = out + k * q->nsel;
+  for (int a = 0; a < q->nsel; ++a) {
+    const StackVal v = eval_prog(code + sel[3 * a], sel[3 * a + 1], consts, ld);
+    DVal d;
+    if (sel[3 * a + 2] == T_FLOAT || sel[3 * a + 2] == T_DOUBLE) d.d = v.d;
+    else d.i = v.i;
+    d.null = v.null;
+    d.pad = 0;
+    o[a] = d;
+  }
+  if (ts_out) ts_out[k] = ts[ld.r2];  // StateEvent.timestamp: the last event's (e2's) event time
+}
+}  // namespace
+
+void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, const int64_t* ord, int64_t n,
+                  int64_t base, const int64_t* ts, const int64_t* prev_carry, int64_t nc, int cw, const char* blob_dev,
+                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s) {
+  if (m <= 0) return;
+  const size_t mark = sc.used;
+  uint32_t *ck = nullptr, *ci = nullptr;
+  if (nc > 0) {
+    ck = (uint32_t*)sc.take((size_t)nc * 4);
+    ci = (uint32_t*)sc.take((size_t)nc * 4);
+    uint32_t* ck2 = (uint32_t*)sc.take((size_t)nc * 4);
+    uint32_t* ci2 = (uint32_t*)sc.take((size_t)nc * 4);
+    hipLaunchKernelGGL(carry_ord_keys_kernel, grid_of(nc), dim3(256), 0, s, prev_carry, nc, cw, base, ck, ci);
+    if (radix_sort_pairs<uint32_t>(ck, ck2, ci, ci2, (size_t)nc, 0, 32, sc, s)) {
+      ck = ck2;
+      ci = ci2;
+    }
+  }
+  hipLaunchKernelGGL(pair_project_kernel, grid_of(m), dim3(256), 0, s, pairs, m, st_dev, ord, n, base, ts, prev_carry,
+                     cw, ck, ci, nc, blob_dev, out, ts_out);
+  SM_HIP(hipGetLastError());
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+}
+
 }  // namespace sm
+

@@ -165,6 +165,17 @@ struct QueryRt {
   int level = 0;             // chaining depth: 0 reads input streams only, L reads a stream a level L-1 query fills
   int fast_path_used = 0;    // 5 = NFA kernel, 3 = bucket stack, 2 = onesweep form, 1 = general form (last device
                              // batch)
+  // what sm_app_device_project needs of the last closed-form batch: its stream, event times, ordinals, and the
+  // carry as it was before the batch (carried e1 rows)
+  bool proj_ok = false;
+  NfaStream proj_desc{};
+  DBuf proj_desc_dev;
+  const int64_t* proj_ts = nullptr;
+  const int64_t* proj_ord = nullptr;
+  int64_t proj_base = 0, proj_n = 0;
+  DBuf prev_carry;
+  int64_t prev_carry_n = 0;
+  int prev_carry_w = 0;
   ~QueryRt() { carry.release(); }
 };
 
@@ -1994,6 +2005,19 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
           hi.key_type = types[hi.key_col];
         }
       }
+      q.proj_ok = false;
+      q.proj_desc = d;
+      q.proj_ts = d_ts;
+      q.proj_ord = d_ordinals;
+      q.proj_base = ordinal_base;
+      q.proj_n = (int64_t)n;
+      q.prev_carry_n = q.carry.n;
+      q.prev_carry_w = q.carry.width;
+      if (q.carry.n > 0) {
+        const size_t cb = (size_t)q.carry.n * q.carry.width * 8;
+        q.prev_carry.ensure(cb);
+        SM_HIP(hipMemcpyAsync(q.prev_carry.p, q.carry.rows, cb, hipMemcpyDeviceToDevice, hs));
+      }
       int64_t m = FAST_OUTSIDE;
       if (!a->force_general_fast)
         m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
@@ -2010,6 +2034,7 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
         q.fast_path_used = 5;
       }
       q.dev_n = m;
+      q.proj_ok = q.fast_path_used != 5 && m >= 0;
     }
     } catch (const std::exception& e) {
       a->failed = true;
@@ -2412,6 +2437,36 @@ int sm_app_copy_device_matches(sm_app* a, const char* query_name, void* d_dst, s
         return;
       }
     throw sql::ValidationError(std::string("No query with name ") + query_name);
+  });
+}
+
+// QuerySelector.processNoGroupBy (core/query/selector/QuerySelector.java:124-167) for the outputs of the last
+// closed-form device batch, on the device: the select list of each (e1, e2) match, in output order.
+int sm_app_device_project(sm_app* a, const char* query_name, sm_dval* d_values, size_t cap_values, int64_t* d_ts,
+                          size_t* n, int32_t* nsel, void* hip_stream) {
+  static_assert(sizeof(sm_dval) == sizeof(DVal), "sm_dval mirrors the device value");
+  return locked(a, [&] {
+    QueryRt* q = nullptr;
+    for (auto& qp : a->queries)
+      if (qp->cq.name == query_name) q = qp.get();
+    if (!q) throw sql::ValidationError(std::string("No query with name ") + query_name);
+    if (!q->proj_ok)
+      throw sql::UnsupportedError("query '" + q->cq.name + "': no closed-form device batch to project (filter queries, "
+                                  "batches the NFA kernel took and host-API events deliver Event data to callbacks)");
+    const int64_t m = q->dev_n;
+    const int32_t ns = q->cq.hdr.nsel;
+    if (n) *n = (size_t)m;
+    if (nsel) *nsel = ns;
+    if (!d_values) return;
+    if ((size_t)m * (size_t)ns > cap_values) throw std::invalid_argument("d_values holds fewer than n * nsel values");
+    hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
+    q->proj_desc_dev.ensure(sizeof(NfaStream));
+    SM_HIP(hipMemcpyAsync(q->proj_desc_dev.p, &q->proj_desc, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
+    ensure_scratch(a, (size_t)q->prev_carry_n * 16 + ((size_t)64 << 20));
+    a->sc.used = 0;
+    pair_project((const uint32_t*)q->dev_pairs.p, m, (const NfaStream*)q->proj_desc_dev.p, q->proj_ord, q->proj_n,
+                 q->proj_base, q->proj_ts, (const int64_t*)q->prev_carry.p, q->prev_carry_n, q->prev_carry_w,
+                 (const char*)q->blob.p, (DVal*)d_values, d_ts, a->sc, hs);
   });
 }
 

@@ -151,6 +151,27 @@ class ProductApp:
         _call(lib().sm_app_get_stat(self.h, key.encode(), ctypes.byref(v)))
         return v.value
 
+    def device_project(self, query):
+        """sm_app_device_project: the last closed-form batch's outputs projected on the device. Returns (values,
+        nulls, ts) as torch tensors on the current device: values (n, nsel) int64 (the raw 64-bit word: integers,
+        dictionary ids, or double bits for FLOAT / DOUBLE), nulls (n, nsel) bool, ts (n,) int64."""
+        import torch
+        n = ctypes.c_size_t()
+        ns = ctypes.c_int32()
+        _call(lib().sm_app_device_project(self.h, query.encode(), None, 0, None, ctypes.byref(n), ctypes.byref(ns),
+                                          None))
+        dev = torch.device("cuda", torch.cuda.current_device())
+        raw = torch.empty((max(n.value, 1), max(ns.value, 1), 2), dtype=torch.int64, device=dev)  # 16-B sm_dval
+        ts = torch.empty(max(n.value, 1), dtype=torch.int64, device=dev)
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _call(lib().sm_app_device_project(self.h, query.encode(), ctypes.c_void_p(raw.data_ptr()),
+                                          n.value * ns.value, ctypes.c_void_p(ts.data_ptr()), ctypes.byref(n),
+                                          ctypes.byref(ns), s))
+        m, k = n.value, ns.value
+        vals = raw[:m, :k, 0]
+        nulls = (raw[:m, :k, 1] & 0xFFFFFFFF) != 0
+        return vals, nulls, ts[:m]
+
     def device_matches_host(self, query):
         """Copy the last device batch's match tuples to the host: numpy uint32 array of shape (n, 2) = (e1, e2)."""
         import numpy as np
