@@ -730,7 +730,8 @@ CompiledQuery compile_query(const App& app, const Query& q, int order, int parti
     kso += (p.kind == PK_ABSENT_STREAM || p.kind == PK_ABSENT_LOGICAL) ? kPreWordsAbsent : kPreWords;
   }
   h.ks_post = kso;
-  h.ks_sched = h.ks_post + h.npost;
+  if (h.npost > 62) throw UnsupportedError("more than 62 states in one query");
+  h.ks_sched = h.ks_post + 1;  // the post processors' isEventReturned bits, one word
   h.ks_misc = h.ks_sched + h.nsched * (2 + kSchedCap);
   h.ks_words = h.ks_misc + 8;
 

@@ -87,7 +87,8 @@ struct Lane;
 #define SM_JIT_INL
 #endif
 
-constexpr int kNfaLdsMisc = 4;  // misc words staged (create, bump, space, id counter; 'initialised' stays in HBM)
+constexpr int kNfaLdsMisc = 3;  // misc words staged: 1..3 (bump, space, id counter); create (0, read per output) and
+                                // initialised (4, read once) stay in HBM
 
 struct StateLoader {  // OP_VAR loads for a run record
   const Lane* L;
@@ -148,7 +149,9 @@ struct Lane {
   // misc words: create position, heap bump, semispace, state-id counter, initialised. Staged (SM_NFA_LDS), they sit
   // right after the post words.
 #ifdef SM_NFA_LDS
-  __device__ __forceinline__ int64_t& misc(int k) const { return k < kNfaLdsMisc ? ks[PQ->ks_sched + k] : ksh[PQ->ks_misc + k]; }
+  __device__ __forceinline__ int64_t& misc(int k) const {
+    return (k >= 1 && k <= kNfaLdsMisc) ? ks[PQ->ks_sched + k - 1] : ksh[PQ->ks_misc + k];
+  }
 #else
   __device__ int64_t& misc(int k) const { return ks[PQ->ks_misc + k]; }
 #endif
@@ -330,7 +333,12 @@ struct Lane {
     else flags(p) &= ~f;
   }
   __device__ int64_t& lastArrival(int p) const { return lw(p, 4); }
-  __device__ int64_t& returned(int o) const { return ks[PQ->ks_post + o]; }
+  // isEventReturned of every post processor (StreamPostStateProcessor :74-78): one bit each in one word
+  __device__ bool returned(int o) const { return (ks[PQ->ks_post] >> o) & 1; }
+  __device__ void set_returned(int o, bool v) const {
+    int64_t& w = ks[PQ->ks_post];
+    w = v ? (w | (1ll << o)) : (w & ~(1ll << o));
+  }
 
   // ------------------------------------------------------------ timers (Scheduler FIFO)
   __device__ LaneWords sq(int s) const { return ksh.at(PQ->ks_sched + s * (2 + kSchedCap)); }
@@ -484,7 +492,7 @@ struct Lane {
         const DPost& O = PPOST[p];
         if (O.hasNext) {
           setfl(O.thisPre, F_STATE_CHANGED, true);
-          returned(p) = 1;
+          set_returned(p, 1);
         }
         if (sp + 2 > 3 * kMaxSlots + 4) {
           err |= NFA_ERR_NPE;
@@ -659,7 +667,7 @@ struct Lane {
           pre_process(p, s);
           int tl = P.thisLast;
           if (returned(tl)) {
-            returned(tl) = 0;
+            set_returned(tl, 0);
             lappend(p, 3, s);
           }
           if (fl(p, F_STATE_CHANGED)) {
@@ -692,7 +700,7 @@ struct Lane {
           pre_process(p, s);
           int tl = P.thisLast;
           if (returned(tl)) {
-            returned(tl) = 0;
+            set_returned(tl, 0);
             lappend(p, 3, s);
           }
           bool removed = false;
@@ -736,7 +744,7 @@ struct Lane {
           pre_process(p, s);
           int tl = P.thisLast;
           if (returned(tl)) {
-            returned(tl) = 0;
+            set_returned(tl, 0);
             lappend(p, 3, s);
           }
           if (fl(p, F_STATE_CHANGED)) {
@@ -775,7 +783,7 @@ struct Lane {
           bool removed = false;
           int tl = P.thisLast;
           if (returned(tl)) {
-            returned(tl) = 0;
+            set_returned(tl, 0);
             int32_t nx = lerase(p, 0, prev, ln);
             removed = true;
             if (P.sequence) lremove_rec(P.partner, 0, s);
@@ -807,7 +815,7 @@ struct Lane {
     const DPost& O = PPOST[o];
     setfl(O.thisPre, F_STATE_CHANGED, true);
     rts(r) = nts(slot(r, O.stateId));
-    if (O.hasNext) returned(o) = 1;
+    if (O.hasNext) set_returned(o, 1);
     if (O.nextPre >= 0) addState(O.nextPre, r);
     if (O.nextEveryPre >= 0) addEveryState(O.nextEveryPre, r);
     if (O.callbackPre >= 0) count_startStateReset(O.callbackPre);
@@ -817,7 +825,7 @@ struct Lane {
     const DPost& O = PPOST[o];
     if (O.hasNext) {
       setfl(O.thisPre, F_STATE_CHANGED, true);
-      returned(o) = 1;
+      set_returned(o, 1);
     }
     if (O.nextPre >= 0) addState(O.nextPre, r);
     if (O.nextEveryPre >= 0) addEveryState(O.nextEveryPre, r);
@@ -871,7 +879,7 @@ struct Lane {
           else setfl(O.thisPre, F_STATE_CHANGED, true);
         } else {
           stream_post(o, r);
-          if (PPOST[O.partnerPost].hasNext && PPRE[O.thisPre].thisLast == O.partnerPost) returned(O.partnerPost) = 1;
+          if (PPOST[O.partnerPost].hasNext && PPRE[O.thisPre].thisLast == O.partnerPost) set_returned(O.partnerPost, 1);
         }
         break;
       }
@@ -879,7 +887,7 @@ struct Lane {
         setfl(O.thisPre, F_STATE_CHANGED, true);
         int32_t se = slot(r, O.stateId);
         rts(r) = nts(se);
-        returned(o) = 1;
+        set_returned(o, 1);
         if (PPRE[O.thisPre].isStart && O.nextEveryPre >= 0 && O.nextEveryPre == O.thisPre)
           addEveryState(O.nextEveryPre, r);
         lastArrival(O.thisPre) = nts(se);
@@ -887,7 +895,7 @@ struct Lane {
       }
       default: {  // AbsentLogicalPostStateProcessor.process :37-50
         setfl(O.thisPre, F_STATE_CHANGED, true);
-        returned(o) = 1;
+        set_returned(o, 1);
         lastArrival(O.thisPre) = nts(slot(r, O.stateId));
         break;
       }
@@ -1279,13 +1287,13 @@ SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ 
   const int nst = PQ->ks_sched;
   LaneWords st{sm_nfa_lds + threadIdx.x, 64};
   for (int w = 0; w < nst; ++w) st[w] = L.ksh[w];
-  for (int k = 0; k < kNfaLdsMisc; ++k) st[nst + k] = L.ksh[PQ->ks_misc + k];
+  for (int k = 0; k < kNfaLdsMisc; ++k) st[nst + k] = L.ksh[PQ->ks_misc + 1 + k];
   L.ks = st;
 #endif
   nfa_lane_run(L, b, key, err_out);
 #ifdef SM_NFA_LDS
   for (int w = 0; w < nst; ++w) L.ksh[w] = st[w];
-  for (int k = 0; k < kNfaLdsMisc; ++k) L.ksh[PQ->ks_misc + k] = st[nst + k];
+  for (int k = 0; k < kNfaLdsMisc; ++k) L.ksh[PQ->ks_misc + 1 + k] = st[nst + k];
 #endif
 }
 
@@ -1311,7 +1319,7 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
       L.lset(p, 3, -1, -1);
       if (L.is_absent(p)) L.lastArrival(p) = 0;
     }
-    for (int o = 0; o < PQ->npost; ++o) L.returned(o) = 0;
+    L.ks[PQ->ks_post] = 0;  // no post processor has returned an event
     for (int s = 0; s < PQ->nsched; ++s) {
       L.sq(s)[0] = 0;
       L.sq(s)[1] = 0;

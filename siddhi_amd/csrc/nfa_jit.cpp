@@ -116,7 +116,7 @@ bool nfa_jit_lds() {
 int64_t nfa_jit_lds_bytes(const std::vector<char>& blob) {
   if (!nfa_jit_lds()) return 0;
   const DQuery* q = (const DQuery*)blob.data();
-  return (int64_t)(q->ks_sched + 4) * 64 * 8;  // (pre + post words + kNfaLdsMisc) x 64 lanes
+  return (int64_t)(q->ks_sched + 3) * 64 * 8;  // (pre words + post bits word + kNfaLdsMisc) x 64 lanes
 }
 
 bool nfa_jit_wanted(int option, int64_t records) {

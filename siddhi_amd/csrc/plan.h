@@ -130,7 +130,7 @@ struct DQuery {
   int32_t ks_words;
   int32_t ks_pre;       // per pre (DPre.ksOff): pendHead|pendTail, newHead|newTail, flags, the returned list of
                         // processAndReturn; an absent pre also lastArrival (only absent processors read it)
-  int32_t ks_post;      // per post: 1 word (isEventReturned)
+  int32_t ks_post;      // one word: bit o = isEventReturned of post processor o
   int32_t ks_sched;     // per scheduler: 2 + kSchedCap words (head, count, ring)
   int32_t ks_misc;      // create position, heap bump, semispace, state-id counter
   // state query: having condition (QuerySelector.java:138-139) over the run record, output attributes
