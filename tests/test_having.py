@@ -166,3 +166,17 @@ def test_having_removes_some_outputs():
     with_h = drive(ProductApp, text, evs, 1000)["streams"]["O"]
     without = drive(ProductApp, no_having, evs, 1000)["streams"]["O"]
     assert 0 < len(with_h) < len(without)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pattern_having", "count_instanceof"])
+def test_having_query_specialised_kernel_equals_oracle(name):
+    """The same having programs in the query-specialised NFA kernel (option nfa_jit = 1, nfa_jit.cpp)."""
+    from siddhi_amd.testing import ProductApp
+    text = APPS[name]
+    streams = [x for x in ("S", "S2", "S3") if f"define stream {x} " in text]
+    evs = events(7, 300, streams)
+    want = drive(OracleApp, text, evs, 100)
+    got = drive(lambda t: ProductApp(t, nfa_jit=1), text, evs, 100)
+    assert sum(len(v) for v in want["streams"].values()) >= 3
+    assert got == want
