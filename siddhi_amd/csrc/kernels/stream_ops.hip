@@ -143,16 +143,36 @@ __global__ void project_kernel(const NfaStream* __restrict__ st, const int64_t* 
 }
 
 // records of the query's streams (+ START markers when `with_start`), as positions
-__global__ void select_records_kernel(const int32_t* __restrict__ ev_stream, int64_t n, uint32_t stream_mask_lo,
-                                      uint32_t stream_mask_hi, int with_start, uint8_t* __restrict__ flag) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int s = ev_stream[i];
-  bool f;
-  if (s == NFA_START) f = with_start;
-  else if (s < 0) f = false;
-  else f = (s < 32) ? ((stream_mask_lo >> s) & 1u) : ((stream_mask_hi >> (s - 32)) & 1u);
-  flag[i] = f;
+// The records a query reads, as 64-record ballot masks + per-block counts (the filter's two-pass compaction:
+// one byte-free pass instead of flag bytes, a widening pass and a full-length scan)
+__global__ __launch_bounds__(kFThreads) void select_mask_kernel(const int32_t* __restrict__ ev_stream, int64_t n,
+                                                                uint32_t stream_mask_lo, uint32_t stream_mask_hi,
+                                                                int with_start, uint64_t* __restrict__ masks,
+                                                                uint32_t* __restrict__ block_counts) {
+  __shared__ uint32_t wsum[kFThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kFThreads * kFIters;
+  uint32_t cnt = 0;
+  for (int it = 0; it < kFIters; ++it) {
+    const int64_t group = (tile >> 6) + (int64_t)it * (kFThreads / 64) + w;
+    const int64_t i = group * 64 + lane;
+    bool f = false;
+    if (i < n) {
+      const int sid = ev_stream[i];
+      if (sid == NFA_START) f = with_start;
+      else if (sid >= 0) f = (sid < 32) ? ((stream_mask_lo >> sid) & 1u) : ((stream_mask_hi >> (sid - 32)) & 1u);
+    }
+    const uint64_t m = __ballot(f);
+    if (lane == 0 && group * 64 < n) masks[group] = m;
+    cnt += (uint32_t)__popcll(m);
+  }
+  if (lane == 0) wsum[w] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < kFThreads / 64; ++k) t += wsum[k];
+    block_counts[blockIdx.x] = t;
+  }
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
@@ -602,14 +622,15 @@ int64_t select_records(const int32_t* ev_stream, int64_t n, uint64_t stream_mask
                        Scratch& sc, hipStream_t s) {
   if (n == 0) return 0;
   size_t mark = sc.used;
-  uint8_t* flag = (uint8_t*)sc.take(n);
-  uint32_t* ex = (uint32_t*)sc.take(n * 4);
+  const int64_t tile = (int64_t)kFThreads * kFIters;
+  const int64_t nblocks = (n + tile - 1) / tile;
+  uint64_t* masks = (uint64_t*)sc.take(((n + 63) / 64) * 8);
+  uint32_t* counts = (uint32_t*)sc.take((nblocks + 1) * 4);
   uint32_t* total = (uint32_t*)sc.take(4);
-  hipLaunchKernelGGL(select_records_kernel, grid_for(n), dim3(256), 0, s, ev_stream, n, (uint32_t)stream_mask,
-                     (uint32_t)(stream_mask >> 32), (int)with_start, flag);
-  hipLaunchKernelGGL(u8_to_u32_kernel, grid_for(n), dim3(256), 0, s, flag, n, ex);
-  exclusive_scan_u32(ex, n, sc, s, total);
-  hipLaunchKernelGGL(compact_flag_kernel<int64_t>, grid_for(n), dim3(256), 0, s, flag, ex, n, out_pos);
+  hipLaunchKernelGGL(select_mask_kernel, dim3((unsigned)nblocks), dim3(kFThreads), 0, s, ev_stream, n,
+                     (uint32_t)stream_mask, (uint32_t)(stream_mask >> 32), (int)with_start, masks, counts);
+  exclusive_scan_u32(counts, nblocks, sc, s, total);
+  hipLaunchKernelGGL(filter_write_kernel, dim3((unsigned)nblocks), dim3(kFThreads), 0, s, masks, n, counts, out_pos);
   uint32_t h = 0;
   SM_HIP(hipMemcpyAsync(&h, total, 4, hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));
