@@ -191,7 +191,7 @@ __global__ void key_eval_kernel(const int64_t* __restrict__ pos, int64_t n, cons
                                 uint8_t* __restrict__ valid) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  int64_t p = pos[i];
+  int64_t p = pos ? pos[i] : i;  // no pos: the query keeps every batch record
   int s = ev_stream[p];
   keys[i] = 0;
   valid[i] = 0;
@@ -648,7 +648,7 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
   int32_t* slot = (int32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
   uint32_t* nmiss = (uint32_t*)sc.take(4);
   if (n > 0)
-    hipLaunchKernelGGL(key_eval_kernel, grid_for(n), dim3(256), 0, s, pos, n, ev_stream, ev_row, streams_dev, progs_dev,
+    hipLaunchKernelGGL(key_eval_kernel, grid_for(n), dim3(256), 0, s, pos_identity ? nullptr : pos, n, ev_stream, ev_row, streams_dev, progs_dev,
                        nprogs, keys, valid);
   SM_HIP(hipMemsetAsync(nmiss, 0, 4, s));
   if (n > 0)
