@@ -175,6 +175,64 @@ __global__ __launch_bounds__(kFThreads) void select_mask_kernel(const int32_t* _
   }
 }
 
+// Run starts of a sorted key array as ballot masks + per-block counts, and the exclusive rank of every element
+// among them (= its run's index): two streaming passes instead of a flag array and a full-length scan
+template <typename K>
+__global__ __launch_bounds__(kFThreads) void run_mask_kernel(const K* __restrict__ sk, int64_t n,
+                                                             uint64_t* __restrict__ masks,
+                                                             uint32_t* __restrict__ block_counts) {
+  __shared__ uint32_t wsum[kFThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kFThreads * kFIters;
+  uint32_t cnt = 0;
+  for (int it = 0; it < kFIters; ++it) {
+    const int64_t group = (tile >> 6) + (int64_t)it * (kFThreads / 64) + w;
+    const int64_t i = group * 64 + lane;
+    const bool f = i < n && (i == 0 || sk[i] != sk[i - 1]);
+    const uint64_t m = __ballot(f);
+    if (lane == 0 && group * 64 < n) masks[group] = m;
+    cnt += (uint32_t)__popcll(m);
+  }
+  if (lane == 0) wsum[w] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < kFThreads / 64; ++k) t += wsum[k];
+    block_counts[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kFThreads) void mask_rank_kernel(const uint64_t* __restrict__ masks, int64_t n,
+                                                              const uint32_t* __restrict__ block_offsets,
+                                                              uint32_t* __restrict__ excl) {
+  __shared__ uint32_t wbase[kFThreads / 64][kFIters];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kFThreads * kFIters;
+  for (int it = 0; it < kFIters; ++it) {
+    const int64_t group = (tile >> 6) + (int64_t)it * (kFThreads / 64) + w;
+    const uint64_t m = (group * 64 < n) ? masks[group] : 0ull;
+    if (lane == 0) wbase[w][it] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = block_offsets[blockIdx.x];
+    for (int it = 0; it < kFIters; ++it)
+      for (int k = 0; k < kFThreads / 64; ++k) {
+        const uint32_t c = wbase[k][it];
+        wbase[k][it] = acc;
+        acc += c;
+      }
+  }
+  __syncthreads();
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int it = 0; it < kFIters; ++it) {
+    const int64_t group = (tile >> 6) + (int64_t)it * (kFThreads / 64) + w;
+    if (group * 64 >= n) break;
+    const int64_t i = group * 64 + lane;
+    if (i < n) excl[i] = wbase[w][it] + (uint32_t)__popcll(masks[group] & lt);
+  }
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33;
   x *= 0xff51afd7ed558ccdull;
@@ -293,13 +351,6 @@ __global__ void rebase_keys_kernel(const int64_t* __restrict__ keys, int64_t n, 
 }
 
 // after sorting (rebased key, idx): run starts get a new slot id; every entry learns its run's slot
-template <typename K>
-__global__ void run_start_kernel(const K* __restrict__ sk, int64_t n, uint32_t* __restrict__ flag) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  flag[i] = (i == 0 || sk[i] != sk[i - 1]) ? 1u : 0u;
-}
-
 template <typename K>
 __global__ void assign_new_slots_kernel(const K* __restrict__ sk, const uint32_t* __restrict__ sidx,
                                         const uint32_t* __restrict__ run_excl, int64_t n, int32_t base,
@@ -705,8 +756,15 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
       }
       uint32_t* runs = (uint32_t*)sc.take(hm * 4);
       uint32_t* nruns = (uint32_t*)sc.take(4);
-      hipLaunchKernelGGL(run_start_kernel<K>, grid_for(hm), dim3(256), 0, s, sk, (int64_t)hm, runs);
-      exclusive_scan_u32(runs, hm, sc, s, nruns);
+      {
+        const int64_t tile = (int64_t)kFThreads * kFIters;
+        const int64_t nb = ((int64_t)hm + tile - 1) / tile;
+        uint64_t* rmask = (uint64_t*)sc.take((((size_t)hm + 63) / 64) * 8);
+        uint32_t* rcnt = (uint32_t*)sc.take(((size_t)nb + 1) * 4);
+        hipLaunchKernelGGL(run_mask_kernel<K>, dim3((unsigned)nb), dim3(kFThreads), 0, s, sk, (int64_t)hm, rmask, rcnt);
+        exclusive_scan_u32(rcnt, nb, sc, s, nruns);
+        hipLaunchKernelGGL(mask_rank_kernel, dim3((unsigned)nb), dim3(kFThreads), 0, s, rmask, (int64_t)hm, rcnt, runs);
+      }
       uint32_t hr = 0;
       SM_HIP(hipMemcpyAsync(&hr, nruns, 4, hipMemcpyDeviceToHost, s));
       SM_HIP(hipStreamSynchronize(s));
