@@ -535,8 +535,11 @@ __global__ __launch_bounds__(kIxThreads) void event_index_kernel(
     const int32_t* __restrict__ sid, int32_t nstreams, const int64_t* __restrict__ ts, int64_t n,
     const int64_t* __restrict__ ord_in, int64_t ord_base, int playback, int64_t clock_in,
     const int64_t* __restrict__ tile_prefix, int64_t* __restrict__ ev_row, int64_t* __restrict__ ev_ord,
-    int64_t* __restrict__ ev_clock, uint8_t* __restrict__ adv_flag, int32_t* __restrict__ bad) {
+    int64_t* __restrict__ ev_clock, uint64_t* __restrict__ adv_mask, uint32_t* __restrict__ adv_cnt,
+    int32_t* __restrict__ bad) {
   __shared__ int64_t wmax[kIxThreads / 64];
+  __shared__ uint32_t wadv[kIxThreads / 64];
+  uint32_t nadv = 0;  // advance points of this wave (lane 0)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t base = (int64_t)blockIdx.x * kIxTile;
   int64_t carry = tile_prefix[blockIdx.x];  // clock before this tile (clock_in folded in)
@@ -560,29 +563,68 @@ __global__ __launch_bounds__(kIxThreads) void event_index_kernel(
     for (int q = 0; q < kIxThreads / 64; ++q) round_max = wmax[q] > round_max ? wmax[q] : round_max;
     __syncthreads();
     carry = round_max;
+    // advance points as one ballot mask per 64 consecutive events (rounds are 64-aligned)
+    const bool adv = in && playback && t >= before;
+    const uint64_t am = __ballot(adv);
+    if (lane == 0 && i < n) adv_mask[i >> 6] = am;
+    nadv += (uint32_t)__popcll(am);
     if (!in) continue;
     const int32_t st = sid[i];
     if (st < NFA_TICK || st >= nstreams) *bad = 1;  // plain vector store: any offender sets the flag
-    const bool adv = playback && t >= before;
     ev_row[i] = i;
     ev_ord[i] = st < 0 ? -1 : ord_in ? ord_in[i] : ord_base + i;  // heartbeats carry no event ordinal
     ev_clock[i] = playback ? (t > before ? t : before) : clock_in;
-    adv_flag[i] = adv;
+  }
+  if (lane == 0) wadv[w] = nadv;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int q = 0; q < kIxThreads / 64; ++q) c += wadv[q];
+    adv_cnt[blockIdx.x] = c;
   }
 }
 
-__global__ void advance_points_kernel(const uint8_t* __restrict__ flag, const uint32_t* __restrict__ excl, int64_t n,
-                                      const int64_t* __restrict__ ts, int64_t* __restrict__ adv_pos,
-                                      int64_t* __restrict__ adv_clock, int64_t* __restrict__ adv_wall,
-                                      int64_t* __restrict__ adv_upto) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t o = excl[i];
-  adv_upto[i] = (int64_t)o + flag[i];
-  if (!flag[i]) return;
-  adv_pos[o] = i;
-  adv_clock[o] = ts[i];
-  adv_wall[o] = -1;
+// Advance-point list and per-position counts from the masks: block offsets (exclusive scan of adv_cnt), then per
+// 64-event group its offset within the tile (round-major, wave-minor, as event_index_kernel visits them)
+__global__ __launch_bounds__(kIxThreads) void advance_rank_kernel(const uint64_t* __restrict__ adv_mask, int64_t n,
+                                                                  const uint32_t* __restrict__ tile_off,
+                                                                  const int64_t* __restrict__ ts,
+                                                                  int64_t* __restrict__ adv_pos,
+                                                                  int64_t* __restrict__ adv_clock,
+                                                                  int64_t* __restrict__ adv_wall,
+                                                                  int64_t* __restrict__ adv_upto) {
+  __shared__ uint32_t gbase[kIxItems][kIxThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kIxTile;
+  for (int k = 0; k < kIxItems; ++k) {
+    const int64_t g0 = base + (int64_t)k * kIxThreads + w * 64;
+    if (lane == 0) gbase[k][w] = g0 < n ? (uint32_t)__popcll(adv_mask[g0 >> 6]) : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = tile_off[blockIdx.x];
+    for (int k = 0; k < kIxItems; ++k)
+      for (int q = 0; q < kIxThreads / 64; ++q) {
+        const uint32_t c = gbase[k][q];
+        gbase[k][q] = acc;
+        acc += c;
+      }
+  }
+  __syncthreads();
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int k = 0; k < kIxItems; ++k) {
+    const int64_t i = base + (int64_t)k * kIxThreads + threadIdx.x;
+    if (i >= n) break;
+    const uint64_t m = adv_mask[i >> 6];
+    const uint32_t o = gbase[k][w] + (uint32_t)__popcll(m & lt);
+    const bool f = (m >> lane) & 1ull;
+    adv_upto[i] = (int64_t)o + f;
+    if (f) {
+      adv_pos[o] = i;
+      adv_clock[o] = ts[i];
+      adv_wall[o] = -1;
+    }
+  }
 }
 }  // namespace
 
@@ -919,22 +961,21 @@ int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const
   const int64_t ntiles = (n + kIxTile - 1) / kIxTile;
   int64_t* tile_max = (int64_t*)sc.take(ntiles * 8);
   int64_t* dclock = (int64_t*)sc.take(8);
-  uint8_t* flag = (uint8_t*)sc.take(n);
-  uint32_t* ex = (uint32_t*)sc.take(n * 4);
+  uint64_t* amask = (uint64_t*)sc.take(((n + 63) / 64) * 8);
+  uint32_t* acnt = (uint32_t*)sc.take((ntiles + 1) * 4);
   uint32_t* total = (uint32_t*)sc.take(4);
   int32_t* bad = (int32_t*)sc.take(4);
   SM_HIP(hipMemsetAsync(bad, 0, 4, s));
   hipLaunchKernelGGL(ts_tile_max_kernel, dim3((unsigned)ntiles), dim3(kIxThreads), 0, s, ts, n, tile_max);
   hipLaunchKernelGGL(tile_prefix_max_kernel, dim3(1), dim3(kIxThreads), 0, s, tile_max, ntiles, clock_in, dclock);
   hipLaunchKernelGGL(event_index_kernel, dim3((unsigned)ntiles), dim3(kIxThreads), 0, s, sid, nstreams, ts, n, ord_in,
-                     ord_base, (int)playback, clock_in, tile_max, ev_row, ev_ord, ev_clock, flag, bad);
+                     ord_base, (int)playback, clock_in, tile_max, ev_row, ev_ord, ev_clock, amask, acnt, bad);
   int64_t nadv = 0;
   if (!playback) SM_HIP(hipMemsetAsync(adv_upto, 0, (size_t)n * 8, s));
   if (playback) {
-    hipLaunchKernelGGL(u8_to_u32_kernel, grid_for(n), dim3(256), 0, s, flag, n, ex);
-    exclusive_scan_u32(ex, n, sc, s, total);
-    hipLaunchKernelGGL(advance_points_kernel, grid_for(n), dim3(256), 0, s, flag, ex, n, ts, adv_pos, adv_clock,
-                       adv_wall, adv_upto);
+    exclusive_scan_u32(acnt, ntiles, sc, s, total);
+    hipLaunchKernelGGL(advance_rank_kernel, dim3((unsigned)ntiles), dim3(kIxThreads), 0, s, amask, n, acnt, ts,
+                       adv_pos, adv_clock, adv_wall, adv_upto);
     uint32_t h = 0;
     SM_HIP(hipMemcpyAsync(&h, total, 4, hipMemcpyDeviceToHost, s));
     nadv = h;
