@@ -45,7 +45,7 @@ constexpr int kKeys = 1024;    // in-bucket keys
 constexpr int kSI = SM_STACK_KSI;  // records per thread per slice
 constexpr int kS = kSB * kSI;      // slice: 4608 records
 #ifndef SM_STACK_KC
-#define SM_STACK_KC 4           // A/B build flag (measured: 4 -> 33.1 ms, 6 -> 34.4, 8 -> 40.0 on config 4)
+#define SM_STACK_KC 5           // A/B build flag (config 4, slices of 4608: 3 -> 34.9 ms, 4 -> 32.1, 5 -> 31.7)
 #endif
 constexpr int kC = SM_STACK_KC; // stack entries held in registers
 constexpr int kQ = 32;         // spilled entries per thread (HBM ring)
