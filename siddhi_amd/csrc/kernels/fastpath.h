@@ -124,7 +124,7 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
 // Carry-out candidates (4 words each: key, global ordinal, event time, source = batch row >= 0 or -(old carry
 // row) - 1) → the new carry rows, sorted by (key, ordinal). `old` is read before carry.rows is replaced.
 void build_carry(const int64_t* cand, int64_t ncand, const NfaStream* st, int nattr, FastCarry& carry, Scratch& sc,
-                 hipStream_t s);
+                 hipStream_t s, int key_bits = 64, int64_t kmin = 0, bool key_runs_ordered = false);
 
 // On-device projection of m closed-form outputs (pairs = the device tuples of the last batch): the query's select
 // programs (blob_dev = its device plan) → out[k * nsel + a], and e2's event time → ts_out[k] (may be null). An e1

@@ -789,8 +789,9 @@ __global__ void __launch_bounds__(kOB) stage_base_kernel(const uint32_t* __restr
 
 // ---- carry out
 __global__ void carry_rows_kernel(const int64_t* __restrict__ cand, int64_t n, const NfaStream* __restrict__ st,
-                                  int nattr, const int64_t* __restrict__ old, int w, int64_t* __restrict__ rows,
-                                  uint64_t* __restrict__ kord, uint64_t* __restrict__ kkey, uint32_t* __restrict__ idx) {
+                                  int nattr, const int64_t* __restrict__ old, int w, int64_t kmin, int key_bits,
+                                  int64_t* __restrict__ rows, uint64_t* __restrict__ kord, uint64_t* __restrict__ kkey,
+                                  uint32_t* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t* c = cand + 4 * i;
@@ -805,7 +806,7 @@ __global__ void carry_rows_kernel(const int64_t* __restrict__ cand, int64_t n, c
     for (int k = 0; k < w; ++k) r[k] = o[k];
   }
   kord[i] = (uint64_t)c[1] ^ 0x8000000000000000ull;
-  kkey[i] = (uint64_t)c[0] ^ 0x8000000000000000ull;
+  kkey[i] = key_bits < 64 ? (uint64_t)(c[0] - kmin) : (uint64_t)c[0] ^ 0x8000000000000000ull;
   idx[i] = (uint32_t)i;
 }
 
@@ -851,7 +852,7 @@ void FastCarry::release() {
 }
 
 void build_carry(const int64_t* cand, int64_t ncand, const NfaStream* st, int nattr, FastCarry& carry, Scratch& sc,
-                 hipStream_t s) {
+                 hipStream_t s, int key_bits, int64_t kmin, bool key_runs_ordered) {
   const int w = 3 + nattr;
   if (ncand == 0) {
     carry.n = 0;
@@ -866,14 +867,21 @@ void build_carry(const int64_t* cand, int64_t ncand, const NfaStream* st, int na
   uint32_t* idx = (uint32_t*)sc.take((size_t)ncand * 4);
   uint32_t* idx2 = (uint32_t*)sc.take((size_t)ncand * 4);
   hipLaunchKernelGGL(carry_rows_kernel, grid_of(ncand), dim3(256), 0, s, cand, ncand, st, nattr,
-                     (const int64_t*)carry.rows, w, rows, kord, kkey, idx);
-  // stable sort by ordinal, then by key
-  bool alt = radix_sort_pairs<uint64_t>(kord, k2, idx, idx2, (size_t)ncand, 0, 64, sc, s);
-  uint32_t* i1 = alt ? idx2 : idx;
-  uint32_t* i1b = alt ? idx : idx2;
-  hipLaunchKernelGGL(gather_u64_kernel, grid_of(ncand), dim3(256), 0, s, kkey, i1, ncand, k2);
-  alt = radix_sort_pairs<uint64_t>(k2, kkey, i1, i1b, (size_t)ncand, 0, 64, sc, s);
-  const uint32_t* fin = alt ? i1b : i1;
+                     (const int64_t*)carry.rows, w, kmin, key_bits, rows, kord, kkey, idx);
+  const uint32_t* fin;
+  if (key_runs_ordered) {
+    // every key's candidates are one run already in ordinal order: a stable sort by key (its significant bits) only
+    const bool alt = radix_sort_pairs<uint64_t>(kkey, k2, idx, idx2, (size_t)ncand, 0, key_bits, sc, s);
+    fin = alt ? idx2 : idx;
+  } else {
+    // stable sort by ordinal, then by key
+    bool alt = radix_sort_pairs<uint64_t>(kord, k2, idx, idx2, (size_t)ncand, 0, 64, sc, s);
+    uint32_t* i1 = alt ? idx2 : idx;
+    uint32_t* i1b = alt ? idx : idx2;
+    hipLaunchKernelGGL(gather_u64_kernel, grid_of(ncand), dim3(256), 0, s, kkey, i1, ncand, k2);
+    alt = radix_sort_pairs<uint64_t>(k2, kkey, i1, i1b, (size_t)ncand, 0, key_bits, sc, s);
+    fin = alt ? i1b : i1;
+  }
   carry.reserve(ncand, w);
   hipLaunchKernelGGL(gather_rows_kernel, grid_of(ncand), dim3(256), 0, s, rows, fin, ncand, w, carry.rows);
   SM_HIP(hipStreamSynchronize(s));
@@ -955,6 +963,7 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
                              "tuples are 32-bit ordinals relative to it), or not before the batch");
   }
   const int64_t extra = hs[2];
+  const int64_t ncand_in = hs[1];  // carried partials of keys outside this batch's key range (unordered appends)
   sa.sbase = sbase;
   sa.stage = (uint64_t*)sc.take((size_t)(n + extra) * 8);
   sa.mstart = (uint32_t*)sc.take((size_t)kBins * (sa.ntiles + 1) * 4);
@@ -1028,7 +1037,12 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
   tmark("order");
   // carry out (the stack kernel left each key's open partials as candidates)
   const int64_t ncand = hs[1];
-  build_carry(sa.cand, ncand, a.st, hi.nattr, carry, sc, s);
+  // the stack kernel writes each key's pending partials as one run, oldest first (put_all): with no out-of-range
+  // carried partials appended before it, one key sort of span bits orders the carry
+  int kb = 1;
+  while (kb < 63 && ((((int64_t)p.H << kRB) - 1) >> kb) != 0) ++kb;
+  if (ncand_in == 0) build_carry(sa.cand, ncand, a.st, hi.nattr, carry, sc, s, kb, p.kmin, true);
+  else build_carry(sa.cand, ncand, a.st, hi.nattr, carry, sc, s);
   tmark("carry_out");
   SM_HIP(hipStreamSynchronize(s));
   sc.used = mark;
