@@ -162,6 +162,17 @@ class SiddhiAppRuntime:
     def start(self):
         check(lib().sm_app_start(self._h))
 
+    def sendDeviceBatch(self, stream_id, ts, cols, ordinals=None, ordinal_base=0, hip_stream=None):
+        """Bulk ingest of one stream's columns already in device memory (torch tensors: int64 event times, one
+        tensor per attribute at its native width): the device form of a sequence of InputHandler.send(ts, row)
+        calls (InputHandler.java:53 → StreamJunction.sendData :232). Filter queries and `every e1 -> e2 within T`
+        patterns on the stream run on the GPU; their outputs reach the registered callbacks in the reference's
+        order, one call per input event that produced output (sm_app_process_device_batch)."""
+        ptrs = (ctypes.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+        check(lib().sm_app_process_device_batch(self._h, stream_id.encode(), ts.numel(), ts.data_ptr(), ptrs,
+                                                ordinals.data_ptr() if ordinals is not None else None,
+                                                int(ordinal_base), hip_stream))
+
     def flush(self):
         check(lib().sm_app_flush(self._h))
 

@@ -129,9 +129,10 @@ void build_carry(const int64_t* cand, int64_t ncand, const NfaStream* st, int na
 // On-device projection of m closed-form outputs (pairs = the device tuples of the last batch): the query's select
 // programs (blob_dev = its device plan) → out[k * nsel + a], and e2's event time → ts_out[k] (may be null). An e1
 // carried from an earlier batch reads its row of prev_carry (the carry as it was before the batch: nc rows of cw
-// words). The batch's columns / ts / ordinals must still be resident.
+// words). The batch's columns / ts / ordinals must still be resident. rows = true: `pairs` are a filter query's
+// kept rows (m u32, ordinal - base), each output reading its own row.
 void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, const int64_t* ord, int64_t n,
                   int64_t base, const int64_t* ts, const int64_t* prev_carry, int64_t nc, int cw, const char* blob_dev,
-                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s);
+                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s, bool rows = false);
 
 }  // namespace sm

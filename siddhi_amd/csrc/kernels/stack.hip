@@ -1091,16 +1091,18 @@ __global__ void pair_project_kernel(const uint32_t* __restrict__ pairs, int64_t 
                                     const int64_t* __restrict__ ord, int64_t n, int64_t base,
                                     const int64_t* __restrict__ ts, const int64_t* __restrict__ crow, int cw,
                                     const uint32_t* __restrict__ ckey, const uint32_t* __restrict__ cidx, int64_t nc,
-                                    const char* __restrict__ blob, DVal* __restrict__ out, int64_t* __restrict__ ts_out) {
+                                    const char* __restrict__ blob, bool rows, DVal* __restrict__ out,
+                                    int64_t* __restrict__ ts_out) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= m) return;
   const DQuery* q = (const DQuery*)blob;
   const Instr* code = (const Instr*)(blob + q->off_code);
   const DVal* consts = (const DVal*)(blob + q->off_const);
   const int32_t* sel = (const int32_t*)(blob + q->off_sel);
-  const uint32_t e1 = pairs[2 * k], e2 = pairs[2 * k + 1];
+  // rows: a filter query's kept rows (one event per output: slot 0 is the row itself)
+  const uint32_t e1 = rows ? pairs[k] : pairs[2 * k], e2 = rows ? pairs[k] : pairs[2 * k + 1];
   ProjLoader ld{st, 0, batch_row(ord, n, base, e2), nullptr};
-  if ((int32_t)e1 < 0) {  // carried e1: its row in the previous carry, by ordinal
+  if (!rows && (int32_t)e1 < 0) {  // carried e1: its row in the previous carry, by ordinal
     const uint32_t want = (uint32_t)((int32_t)e1 + 0x80000000ll);
     int64_t lo = 0, hi = nc - 1;
     while (lo < hi) {
@@ -1128,11 +1130,11 @@ __global__ void pair_project_kernel(const uint32_t* __restrict__ pairs, int64_t 
 
 void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, const int64_t* ord, int64_t n,
                   int64_t base, const int64_t* ts, const int64_t* prev_carry, int64_t nc, int cw, const char* blob_dev,
-                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s) {
+                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s, bool rows) {
   if (m <= 0) return;
   const size_t mark = sc.used;
   uint32_t *ck = nullptr, *ci = nullptr;
-  if (nc > 0) {
+  if (nc > 0 && !rows) {
     ck = (uint32_t*)sc.take((size_t)nc * 4);
     ci = (uint32_t*)sc.take((size_t)nc * 4);
     uint32_t* ck2 = (uint32_t*)sc.take((size_t)nc * 4);
@@ -1144,7 +1146,7 @@ void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, con
     }
   }
   hipLaunchKernelGGL(pair_project_kernel, grid_of(m), dim3(256), 0, s, pairs, m, st_dev, ord, n, base, ts, prev_carry,
-                     cw, ck, ci, nc, blob_dev, out, ts_out);
+                     cw, ck, ci, nc, blob_dev, rows, out, ts_out);
   SM_HIP(hipGetLastError());
   SM_HIP(hipStreamSynchronize(s));
   sc.used = mark;

@@ -176,6 +176,10 @@ struct QueryRt {
   DBuf prev_carry;
   int64_t prev_carry_n = 0;
   int prev_carry_w = 0;
+  // a batch the NFA kernel ran (hand-over): its outputs' select values (dev_n x nsel DVal) then timestamps
+  bool proj_nfa = false;
+  DBuf nfa_proj;
+  DBuf proj_out;  // device projection of a batch for its consumers (device_outputs)
   ~QueryRt() { carry.release(); }
 };
 
@@ -884,7 +888,7 @@ size_t batch_scratch(const sm_app* a, int64_t N) {
 // emits nothing. The batch's matches go to dev_pairs as in the closed form: (e1, e2) relative to ordinal_base,
 // in reference order.
 int64_t nfa_device_batch(sm_app* a, int qi, int s, size_t n, const int64_t* d_ts, const void* const* d_cols,
-                         const int64_t* d_ordinals, int64_t ordinal_base, hipStream_t hs) {
+                         const int64_t* d_ordinals, int64_t ordinal_base, hipStream_t hs, std::vector<HostOut>* douts) {
   QueryRt& q = *a->queries[qi];
   const auto& attrs = a->streams[s].def->attrs;
   const int nattr = (int)attrs.size();
@@ -1007,9 +1011,99 @@ int64_t nfa_device_batch(sm_app* a, int qi, int s, size_t n, const int64_t* d_ts
   q.dev_pairs.ensure(std::max<size_t>(pairs.size() * 4, 16));
   if (!pairs.empty())
     SM_HIP(hipMemcpyAsync(q.dev_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, hs));
+  // the outputs' Event data for sm_app_device_project (the closed form projects on demand; here the NFA kernel
+  // already evaluated the select list)
+  const size_t ns = (size_t)q.cq.hdr.nsel, m = outs.size();
+  std::vector<DVal> pv(m * ns);
+  std::vector<int64_t> pts(m);
+  for (size_t k = 0; k < m; ++k) {
+    if (ns) memcpy(pv.data() + k * ns, outs[k].vals, ns * sizeof(DVal));
+    pts[k] = outs[k].r.ts;
+  }
+  q.nfa_proj.ensure(std::max<size_t>(m * (ns * sizeof(DVal) + 8), 16));
+  if (m) {
+    if (ns) SM_HIP(hipMemcpyAsync(q.nfa_proj.p, pv.data(), m * ns * sizeof(DVal), hipMemcpyHostToDevice, hs));
+    SM_HIP(hipMemcpyAsync((char*)q.nfa_proj.p + m * ns * sizeof(DVal), pts.data(), m * 8, hipMemcpyHostToDevice, hs));
+  }
   SM_HIP(hipStreamSynchronize(hs));
-  a->out_arena.clear();
-  return (int64_t)outs.size();
+  if (douts)  // the trigger of each output is its e2 (a data event): global ordinal as the delivery position
+    for (HostOut& h : outs) {
+      h.r.pos = h.e2;
+      douts->push_back(h);
+    }
+  return (int64_t)m;
+}
+
+// Whether anything takes query q's outputs: the collect dump, a StreamCallback on its output stream, or a
+// QueryCallback (not inherited by partition clones).
+bool outputs_consumed(const sm_app* a, const QueryRt& q) {
+  if (a->collect) return true;
+  auto it = a->stream_cbs.find(q.cq.insert_into);
+  if (it != a->stream_cbs.end() && !it->second.empty()) return true;
+  auto qt = a->query_cbs.find(q.cq.name);
+  return q.cq.partition < 0 && qt != a->query_cbs.end() && !qt->second.empty();
+}
+
+// The outputs of query qi's last device batch (closed-form matches or a filter's kept rows) as HostOut records for
+// deliver(): QuerySelector.processNoGroupBy (:124-167) on the device (pair_project), one copy to the host, then
+// OutputRateLimiter.sendToCallBacks (:61) → StreamCallback.receive (:65) / QueryCallback through deliver(). Each
+// output's trigger is its e2 (a filter: its row), so deliver() makes one chunk per input event, as a sequence of
+// InputHandler.send calls would. `keep` owns the host copies the records point into.
+void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<HostOut>& outs,
+                    std::vector<std::vector<int64_t>>& keep) {
+  QueryRt& q = *a->queries[qi];
+  const int64_t m = q.dev_n;
+  if (m <= 0 || !q.proj_ok) return;
+  const CompiledQuery& cq = q.cq;
+  const bool rows = cq.hdr.kind == 0;
+  const int ns = cq.hdr.nsel, nr = cq.hdr.nrefs_vis;
+  const int32_t* rslots = (const int32_t*)(cq.blob.data() + cq.hdr.off_refs);
+  std::vector<uint32_t> hp((size_t)m * (rows ? 1 : 2));
+  SM_HIP(hipMemcpyAsync(hp.data(), q.dev_pairs.p, hp.size() * 4, hipMemcpyDeviceToHost, hs));
+  keep.emplace_back((size_t)m * (2 * ns + 1 + nr));  // DVal = two words each, then ts, then refs
+  int64_t* hv = keep.back().data();
+  int64_t* hts = hv + (size_t)m * 2 * ns;
+  int64_t* hrf = hts + m;
+  q.proj_desc_dev.ensure(sizeof(NfaStream));
+  SM_HIP(hipMemcpyAsync(q.proj_desc_dev.p, &q.proj_desc, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
+  const int64_t chunk = std::min<int64_t>(m, (int64_t)1 << 22);
+  q.proj_out.ensure((size_t)chunk * (ns * sizeof(DVal) + 8) + 16);
+  DVal* dv = (DVal*)q.proj_out.p;
+  int64_t* dts = (int64_t*)((char*)q.proj_out.p + (size_t)chunk * ns * sizeof(DVal));
+  for (int64_t k0 = 0; k0 < m; k0 += chunk) {
+    const int64_t c = std::min(chunk, m - k0);
+    a->sc.used = 0;
+    pair_project((const uint32_t*)q.dev_pairs.p + (rows ? k0 : 2 * k0), c, (const NfaStream*)q.proj_desc_dev.p,
+                 q.proj_ord, q.proj_n, q.proj_base, q.proj_ts, (const int64_t*)q.prev_carry.p, q.prev_carry_n,
+                 q.prev_carry_w, (const char*)q.blob.p, dv, dts, a->sc, hs, rows);
+    if (ns) SM_HIP(hipMemcpyAsync(hv + (size_t)k0 * 2 * ns, dv, (size_t)c * ns * sizeof(DVal), hipMemcpyDeviceToHost, hs));
+    SM_HIP(hipMemcpyAsync(hts + k0, dts, (size_t)c * 8, hipMemcpyDeviceToHost, hs));
+  }
+  SM_HIP(hipStreamSynchronize(hs));
+  outs.reserve(outs.size() + (size_t)m);
+  for (int64_t k = 0; k < m; ++k) {
+    const int64_t e1 = q.proj_base + (int32_t)hp[rows ? k : 2 * k];
+    const int64_t e2 = q.proj_base + (int32_t)hp[rows ? k : 2 * k + 1];
+    int64_t* rf = hrf + (size_t)k * nr;
+    for (int r = 0; r < nr; ++r) rf[r] = rslots[2 * r] == 0 ? e1 : e2;
+    HostOut h;
+    memset(&h.r, 0, sizeof(h.r));
+    h.r.pos = e2;
+    h.r.create = -1;
+    h.r.ts = hts[k];
+    h.r.phase = 1;
+    h.r.query = cq.hdr.query_order;
+    h.r.seq = (int32_t)k;
+    h.vals = (const DVal*)(hv + (size_t)k * 2 * ns);
+    h.nvals = ns;
+    h.refs = rf;
+    h.nrefs = nr;
+    h.qidx = qi;
+    h.e1 = e1;
+    h.e2 = e2;
+    outs.push_back(h);
+  }
+  q.n_out += m;
 }
 
 // Host side of one batch in arrival order: the staged input (flush), or a chaining level's merged batch.
@@ -1941,6 +2035,9 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
                                                    nc * (160 + 8 * wc) + ((size_t)640 << 20));
     }
     ensure_scratch(a, need);
+    std::vector<HostOut> douts;                 // this batch's outputs for their consumers, all queries
+    std::vector<std::vector<int64_t>> dkeep;    // host copies the records point into
+    a->out_arena.clear();
     try {
     for (size_t qi = 0; qi < a->queries.size(); ++qi) {
       QueryRt& q = *a->queries[qi];
@@ -1948,6 +2045,13 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
       if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
       a->sc.used = 0;
       const char* blob = (const char*)q.blob.p;
+      const bool consumed = outputs_consumed(a, q);
+      q.proj_ok = q.proj_nfa = false;
+      q.proj_desc = d;
+      q.proj_ts = d_ts;
+      q.proj_ord = d_ordinals;
+      q.proj_base = ordinal_base;
+      q.proj_n = (int64_t)n;
       if (cq.hdr.kind == 0) {
         q.dev_pairs.ensure(std::max<size_t>(n * 4, 16));
         bool typed = false;
@@ -1958,11 +2062,16 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
                                 d_ordinals, ordinal_base, (uint32_t*)q.dev_pairs.p, a->sc, hs,
                                 a->fast_timing ? &a->fast_tm : nullptr, &typed);
         q.fast_path_used = typed ? 4 : 3;
+        q.prev_carry_n = 0;
+        q.proj_ok = true;
+        if (consumed) device_outputs(a, (int)qi, hs, douts, dkeep);
         continue;
       }
       if (q.nfa_mode || q.nfa_used) {  // matching state held by the NFA kernel
-        q.dev_n = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs);
+        q.dev_n = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs,
+                                   consumed ? &douts : nullptr);
         q.fast_path_used = 5;
+        q.proj_nfa = true;
         continue;
       }
       FastArgs fa{};
@@ -2005,12 +2114,6 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
           hi.key_type = types[hi.key_col];
         }
       }
-      q.proj_ok = false;
-      q.proj_desc = d;
-      q.proj_ts = d_ts;
-      q.proj_ord = d_ordinals;
-      q.proj_base = ordinal_base;
-      q.proj_n = (int64_t)n;
       q.prev_carry_n = q.carry.n;
       q.prev_carry_w = q.carry.width;
       if (q.carry.n > 0) {
@@ -2030,12 +2133,23 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
       } else if (m < 0) {
         // event time not monotone, or a condition outside the v2 envelope: the NFA kernel takes the query over
         // (carried partials included) and keeps it, so later batches and host events see one matching state
-        m = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs);
+        m = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs, consumed ? &douts : nullptr);
         q.fast_path_used = 5;
+        q.proj_nfa = true;
       }
       q.dev_n = m;
       q.proj_ok = q.fast_path_used != 5 && m >= 0;
+      if (q.proj_ok && consumed) device_outputs(a, (int)qi, hs, douts, dkeep);
     }
+    if (!douts.empty()) {
+      a->need_outs = true;  // deliver() hands them out even when only the collect dump takes them
+      struct Reset {
+        bool& f;
+        ~Reset() { f = false; }
+      } reset_need{a->need_outs};
+      deliver(a, douts);
+    }
+    a->out_arena.clear();
     } catch (const std::exception& e) {
       a->failed = true;
       a->failed_why = std::string("a device batch failed half-way (") + e.what() +
@@ -2450,9 +2564,9 @@ int sm_app_device_project(sm_app* a, const char* query_name, sm_dval* d_values, 
     for (auto& qp : a->queries)
       if (qp->cq.name == query_name) q = qp.get();
     if (!q) throw sql::ValidationError(std::string("No query with name ") + query_name);
-    if (!q->proj_ok)
-      throw sql::UnsupportedError("query '" + q->cq.name + "': no closed-form device batch to project (filter queries, "
-                                  "batches the NFA kernel took and host-API events deliver Event data to callbacks)");
+    if (!q->proj_ok && !q->proj_nfa)
+      throw sql::UnsupportedError("query '" + q->cq.name + "': no device batch to project (host-API events deliver "
+                                  "Event data to callbacks)");
     const int64_t m = q->dev_n;
     const int32_t ns = q->cq.hdr.nsel;
     if (n) *n = (size_t)m;
@@ -2460,13 +2574,22 @@ int sm_app_device_project(sm_app* a, const char* query_name, sm_dval* d_values, 
     if (!d_values) return;
     if ((size_t)m * (size_t)ns > cap_values) throw std::invalid_argument("d_values holds fewer than n * nsel values");
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
+    if (q->proj_nfa) {  // the NFA kernel evaluated the select list already (nfa_device_batch)
+      if (m && ns)
+        SM_HIP(hipMemcpyAsync(d_values, q->nfa_proj.p, (size_t)m * ns * sizeof(DVal), hipMemcpyDeviceToDevice, hs));
+      if (m && d_ts)
+        SM_HIP(hipMemcpyAsync(d_ts, (char*)q->nfa_proj.p + (size_t)m * ns * sizeof(DVal), (size_t)m * 8,
+                              hipMemcpyDeviceToDevice, hs));
+      SM_HIP(hipStreamSynchronize(hs));
+      return;
+    }
     q->proj_desc_dev.ensure(sizeof(NfaStream));
     SM_HIP(hipMemcpyAsync(q->proj_desc_dev.p, &q->proj_desc, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
     ensure_scratch(a, (size_t)q->prev_carry_n * 16 + ((size_t)64 << 20));
     a->sc.used = 0;
     pair_project((const uint32_t*)q->dev_pairs.p, m, (const NfaStream*)q->proj_desc_dev.p, q->proj_ord, q->proj_n,
                  q->proj_base, q->proj_ts, (const int64_t*)q->prev_carry.p, q->prev_carry_n, q->prev_carry_w,
-                 (const char*)q->blob.p, (DVal*)d_values, d_ts, a->sc, hs);
+                 (const char*)q->blob.p, (DVal*)d_values, d_ts, a->sc, hs, q->cq.hdr.kind == 0);
   });
 }
 

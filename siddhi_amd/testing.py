@@ -33,6 +33,7 @@ class ProductApp:
         for k, v in options.items():
             _call(L.sm_app_set_option(self.h, k.encode(), int(v)))
         _call(L.sm_app_set_collect(self.h, 1))
+        self._collect = True
         self._inputs = {}
 
     def close(self):
@@ -100,15 +101,26 @@ class ProductApp:
     def set_collect(self, on):
         """Keep (on) or drop (off) the JSON dump of delivered outputs; output counts are kept either way."""
         _call(lib().sm_app_set_collect(self.h, 1 if on else 0))
+        self._collect = bool(on)
 
     def set_option(self, key, value):
         _call(lib().sm_app_set_option(self.h, key.encode(), int(value)))
 
-    def process_device_batch(self, stream, ts_tensor, col_tensors, ordinals=None, ordinal_base=0, hip_stream=None):
+    def process_device_batch(self, stream, ts_tensor, col_tensors, ordinals=None, ordinal_base=0, hip_stream=None,
+                             collect=False):
+        """collect=False keeps the batch's outputs out of the JSON dump (the parity tests read the device tuples;
+        the dump would cost a host round trip per output)."""
         ptrs = (ctypes.c_void_p * len(col_tensors))(*[t.data_ptr() for t in col_tensors])
-        _call(lib().sm_app_process_device_batch(self.h, stream.encode(), ts_tensor.numel(), ts_tensor.data_ptr(), ptrs,
-                                                ordinals.data_ptr() if ordinals is not None else None,
-                                                int(ordinal_base), hip_stream))
+        quiet = self._collect and not collect
+        if quiet:
+            _call(lib().sm_app_set_collect(self.h, 0))
+        try:
+            _call(lib().sm_app_process_device_batch(self.h, stream.encode(), ts_tensor.numel(), ts_tensor.data_ptr(),
+                                                    ptrs, ordinals.data_ptr() if ordinals is not None else None,
+                                                    int(ordinal_base), hip_stream))
+        finally:
+            if quiet:
+                _call(lib().sm_app_set_collect(self.h, 1))
 
     def process_device_events(self, stream_idx, ts_tensor, col_tensors, ordinals=None, ordinal_base=0,
                               hip_stream=None):

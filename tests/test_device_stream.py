@@ -307,3 +307,147 @@ def test_snapshot_restore_keeps_carried_partials(stack):
     second = batch(b, 9000, n)
     b.close()
     np.testing.assert_array_equal(np.concatenate([first, second]), exp)
+
+
+# ---- the bucket-stack kernel's own limits (kernels/stack.hip): a batch that exceeds one of them is re-run on the
+# sort / walk kernels (fast_path 2) and must still equal the reference. The reference's pending list is an
+# unbounded LinkedList (StreamPreStateProcessor.java:58-59, processAndReturn :274-327), so none of these limits may
+# change an output.
+
+def _paths_and_pairs(text, cols, ts, ranges, stack=1):
+    import torch
+    from siddhi_amd.testing import ProductApp
+    app = ProductApp(text, fast_stack=stack)
+    dev = torch.device("cuda", 0)
+    got, paths = [], []
+    for lo, hi in ranges:
+        tcols = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
+        tts = torch.from_numpy(np.ascontiguousarray(ts[lo:hi], dtype=np.int64)).to(dev)
+        app.process_device_batch("StockStream", tts, tcols, ordinal_base=lo)
+        got.append(app.device_matches_host("q").view(np.int32).astype(np.int64) + lo)
+        paths.append(int(app.get_stat("fast_path:q")))
+    app.close()
+    return np.concatenate(got), paths
+
+
+def _overwrite(cols, ts, pos, keys, prices, t=None):
+    cols[0][pos] = keys
+    cols[1][pos] = prices
+    if t is not None:
+        ts[pos] = t
+
+
+def test_stack_overflow_long_decreasing_run():
+    """SE_OVERFLOW (stack.hip st_push): one key holds more than kC + kQ = 37 live partials (a strictly decreasing
+    price run of 60 inside the window), then one event beats them all (60 matches for one e2)."""
+    n, K, div = 30000, 100, 10
+    cols, ts = stock(n, K, div)
+    cols = [c.copy() for c in cols]
+    ts = ts.copy()
+    seg = cols[0][12000:12201]
+    seg[seg == 7] = 8  # key 7 only through the run below inside this stretch
+    run = 12000 + 3 * np.arange(60)
+    _overwrite(cols, ts, run, 7, 90.0 - 0.5 * np.arange(60))
+    _overwrite(cols, ts, np.array([12200]), 7, 99.9)
+    text = app_text()
+    exp = oracle_pairs(text, cols, ts)
+    got, paths = _paths_and_pairs(text, cols, ts, [(0, 10000), (10000, 20000), (20000, n)])
+    assert paths[0] == 3 and paths[1] == 2, paths
+    assert ((exp[:, 1] == 12200).sum()) >= 60
+    np.testing.assert_array_equal(got, exp)
+
+
+def _many_match_slice(nkeys, depth, n_tail, seed=3):
+    """Keys m * 1024 (all in bucket 0, H = 600 in-bucket keys, so 8 match-log slots per thread): the batch opens with
+    `depth` rounds of decreasing prices over `nkeys` keys, then one event per key that beats its whole stack (depth
+    matches for one e2), all in the first 4608-record slice; a random tail over 600 keys follows."""
+    rng = np.random.default_rng(seed)
+    keys = np.arange(nkeys, dtype=np.int32) * 1024
+    head_k = np.concatenate([np.tile(keys, depth), keys])
+    head_p = np.concatenate([np.repeat(80.0 - 0.5 * np.arange(depth), nkeys), np.full(nkeys, 99.5)])
+    tail_k = rng.integers(0, 600, n_tail).astype(np.int32) * 1024
+    tail_p = rng.random(n_tail) * 100.0
+    sym = np.concatenate([head_k, tail_k])
+    price = np.concatenate([head_p, tail_p])
+    n = len(sym)
+    tsa = np.arange(n, dtype=np.int64)
+    vol = rng.integers(0, 2000, n).astype(np.int64)
+    return [sym, price, vol, tsa], tsa // 20
+
+
+@pytest.mark.parametrize("nkeys,expect", [(40, 3), (200, 2)])
+def test_stack_match_log_overflow(nkeys, expect):
+    """40 keys x 20 matches spill 480 entries into the shared overflow log (kOvf = 1024): the stack kernel keeps
+    the batch. 200 keys x 20 matches exceed it (SE_LOG): the batch goes to the sort / walk kernels."""
+    depth = 20
+    cols, ts = _many_match_slice(nkeys, depth, 20000)
+    assert nkeys * (depth + 1) <= 4608
+    text = app_text()
+    exp = oracle_pairs(text, cols, ts)
+    got, paths = _paths_and_pairs(text, cols, ts, [(0, len(ts))])
+    assert paths == [expect]
+    np.testing.assert_array_equal(got, exp)
+
+
+def _pending_tail(K, depth, n_head, seed=4):
+    """A random head over K keys, then `depth` rounds of decreasing prices (all above c1's 20) over every key: each key
+    ends the batch with more than `depth` pending partials (no `within`: nothing expires)."""
+    rng = np.random.default_rng(seed)
+    keys = np.arange(K, dtype=np.int32)
+    sym = np.concatenate([rng.integers(0, K, n_head).astype(np.int32), np.tile(keys, depth)])
+    price = np.concatenate([rng.random(n_head) * 100.0, np.repeat(30.0 - 0.25 * np.arange(depth), K)])
+    n = len(sym)
+    tsa = np.arange(n, dtype=np.int64)
+    vol = rng.integers(0, 2000, n).astype(np.int64)
+    return [sym, price, vol, tsa], tsa // 10
+
+
+def test_stack_carry_candidate_overflow():
+    """SE_CAND (stack.hip put_all): 1024 keys (one in-bucket key, H = 1) end the batch with about 20 pending
+    partials each, more than the 8 * H * 1024 + 1024 carry-out candidates the stack kernel reserves: the walk
+    kernels take the batch, and the carry they leave feeds the next batch."""
+    K, depth = 1024, 20
+    cols, ts = _pending_tail(K, depth, 6000)
+    n = len(ts)
+    # a second batch: every key again, beating the carried stacks
+    rng = np.random.default_rng(9)
+    n2 = 8000
+    cols2 = [rng.integers(0, K, n2).astype(np.int32), rng.random(n2) * 100.0, rng.integers(0, 2000, n2),
+             np.arange(n, n + n2, dtype=np.int64)]
+    cols = [np.concatenate([a, b.astype(a.dtype)]) for a, b in zip(cols, cols2)]
+    ts = np.concatenate([ts, np.full(n2, ts[-1], dtype=np.int64) + np.arange(n2) // 10])
+    text = app_text(within="")
+    exp = oracle_pairs(text, cols, ts)
+    got, paths = _paths_and_pairs(text, cols, ts, [(0, n), (n, n + n2)])
+    assert paths[0] == 2, paths
+    np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("stack", [1, 2])
+def test_spilled_stacks_carried_into_key_range(stack):
+    """More than kC = 5 pending partials per key (register stack full, entries in the HBM spill ring) at a batch
+    end, no `within`, and every carried key inside the next batch's key range: the carry-out takes the one-key-sort
+    form (stack.hip build_carry, key_runs_ordered), which relies on put_all writing each key's partials as one
+    oldest-first run. Three batches, so a carry is also read back by the stack kernel."""
+    K, depth = 120, 12
+    cols, ts = _pending_tail(K, depth, 3000)
+    n = len(ts)
+    parts = [cols]
+    tss = [ts]
+    for b in range(2):
+        rng = np.random.default_rng(20 + b)
+        m = 3000
+        base = n + b * (m + K * depth)
+        k2 = np.concatenate([rng.integers(0, K, m).astype(np.int32), np.tile(np.arange(K, dtype=np.int32), depth)])
+        p2 = np.concatenate([rng.random(m) * 100.0, np.repeat(25.0 - 0.25 * np.arange(depth), K)])
+        ln = len(k2)
+        parts.append([k2, p2, rng.integers(0, 2000, ln), np.arange(base, base + ln, dtype=np.int64)])
+        tss.append(np.arange(base, base + ln, dtype=np.int64) // 10)
+    cols = [np.concatenate([p[k].astype(parts[0][k].dtype) for p in parts]) for k in range(4)]
+    ts = np.concatenate(tss)
+    bounds = np.cumsum([0] + [len(t) for t in tss])
+    text = app_text(within="")
+    exp = oracle_pairs(text, cols, ts)
+    got, paths = _paths_and_pairs(text, cols, ts, list(zip(bounds[:-1], bounds[1:])), stack=stack)
+    assert paths == [3 if stack == 1 else 2] * 3, paths
+    np.testing.assert_array_equal(got, exp)
