@@ -127,10 +127,16 @@ size_t sm_app_dump_outputs(sm_app* app, char* buf, size_t len);
  * with >= N keys by descending event count; 0 = off, the default; outputs are unchanged either way). */
 int sm_app_set_option(sm_app* app, const char* key, int64_t value);
 
-/* Device-resident batch of ONE stream (columns already in HBM, hipStream given as void*): every record is
- * processed as a fresh stream segment for the fast-path queries (every e1 -> e2 within T), producing match
- * tuples that stay on the device. `ordinals` (int64, may be NULL = base + index) gives each event's global
- * arrival ordinal (multi-GPU shards keep the ordinals of the unsharded stream). */
+/* Device-resident batch of ONE stream (columns already in HBM, hipStream given as void*): the device form of a
+ * sequence of InputHandler.send(ts, row) calls on that stream. Filter queries and `every e1 -> e2 within T` patterns
+ * run on the GPU; the pattern is a streaming receiver: each key's open partials are carried into the next batch
+ * (StreamPreStateProcessor's pending list across sends), and a batch that leaves the closed form's premise (event
+ * time going back, a condition outside its envelope) hands the query to the general NFA kernel for good. The match
+ * tuples stay on the device (sm_app_device_matches); when a StreamCallback / QueryCallback is registered for a query
+ * (or the collect dump is on), its outputs are also projected on the device and delivered as Events before the
+ * call returns, in reference order, one callback call per input event that produced output
+ * (OutputRateLimiter.sendToCallBacks :61 → StreamCallback.receive :65). `ordinals` (int64, may be NULL = base +
+ * index) gives each event's global arrival ordinal (multi-GPU shards keep the ordinals of the unsharded stream). */
 int sm_app_process_device_batch(sm_app* app, const char* stream_id, size_t n, const int64_t* d_timestamps,
                                 const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
                                 void* hip_stream);
@@ -151,7 +157,7 @@ int sm_app_process_device_events(sm_app* app, size_t n, const int32_t* d_stream_
  * events are discarded. */
 int sm_app_snapshot(sm_app* app, uint8_t* buf, size_t cap, size_t* len);
 int sm_app_restore(sm_app* app, const uint8_t* buf, size_t len);
-/* Stable partition of a device batch by owner rank (keys: 1/2/4/8-byte integers, world <= 64). The owner of key
+/* Stable partition of a device batch by owner rank (keys: 4- or 8-byte signed integers, world <= 64). The owner of key
  * k is (hi32(splitmix64_finalizer((uint64_t)(int64_t)k))) mod world, hash-by-key so that structured keys spread.
  * Column c (widths[c] bytes per element: 1, 2, 4 or 8) is copied from d_src[c] to d_dst[c] grouped by owner,
  * arrival order kept within each owner; element i of the output lands at d_dst[c] + i * strides[c] (strides
@@ -185,16 +191,19 @@ typedef struct sm_dval {
   int32_t pad;
 } sm_dval;
 /* QuerySelector.processNoGroupBy (query/selector/QuerySelector.java:124-167) on the device for the outputs of the
- * last device batch of an `every e1 -> e2 within T` query that took the closed form: output k (the k-th tuple of
- * sm_app_device_matches) gets its select list in d_values[k * nsel .. k * nsel + nsel) and its timestamp (e2's event
- * time, StateEvent.timestamp) in d_ts[k] (d_ts may be NULL). An e1 carried from an earlier batch is read from the
- * carried partial. With d_values == NULL only *n and *nsel are set. The batch's columns, event times and ordinals
- * are read again: call it before freeing them. SM_E_UNSUPPORTED for filter queries and for batches the NFA kernel
- * took (their outputs reach the callbacks as Event data). */
+ * last device batch of a query: output k (the k-th tuple of sm_app_device_matches, or a filter query's k-th kept
+ * row) gets its select list in d_values[k * nsel .. k * nsel + nsel) and its timestamp (the last event's time,
+ * StateEvent.timestamp) in d_ts[k] (d_ts may be NULL). An e1 carried from an earlier batch is read from the carried
+ * partial; a batch the NFA kernel took returns the values the kernel evaluated. With d_values == NULL only *n and
+ * *nsel are set. The batch's columns, event times and ordinals are read again: call it before freeing them.
+ * SM_E_UNSUPPORTED when the query's last outputs came from host-API events (they reach the callbacks). */
 int sm_app_device_project(sm_app* app, const char* query_name, sm_dval* d_values, size_t cap_values, int64_t* d_ts,
                           size_t* n, int32_t* nsel, void* hip_stream);
-/* Diagnostics of the last device batch: "fast_path:<query>" (2 = onesweep kernels, 1 = general kernels),
- * "fast_ms:group" / "fast_ms:walk" / "fast_ms:order" (phase times in ms; needs the "fast_timing" option). */
+/* Diagnostics of the last device batch: "fast_path:<query>" = the device path it took: patterns 3 = bucket-stack
+ * kernels, 2 = sort / walk kernels, 1 = general closed form (option fast_general), 5 = general NFA kernel (hand-over);
+ * filter queries 3 = filter interpreter, 4 = typed conjunction. "output_events:<query>" = its output count.
+ * "kernel_ms:<label>" / "kernel_calls:<label>" and "fast_ms:group" / "fast_ms:walk" / "fast_ms:order" (per-kernel
+ * and phase times in ms; need the "fast_timing" option). */
 int sm_app_get_stat(sm_app* app, const char* key, double* out);
 
 #ifdef __cplusplus

@@ -582,7 +582,10 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
         }
         ++base;
       };
-      // order does not matter: the carry is sorted
+      // Invariant the carry-out relies on (build_carry with key_runs_ordered): a key's pending partials are written
+      // as ONE contiguous run, oldest first: the spill ring from its head upward, then the registers from the bottom
+      // (kC - 1) to the top (0). One stable sort by key then orders the whole carry by (key, ordinal); reordering
+      // these loops would silently corrupt the carry order of later batches.
       for (int k = 0; k < s.hn; ++k) {
         const uint4 e = sp[(s.hb + k) & (kQ - 1)];
         put(e.x, (int32_t)e.z);

@@ -25,6 +25,10 @@
 
 #include "nfa_jit_body.inc"  // kNfaJitBody (embed_jit.py)
 
+#ifndef SM_ARCH
+#define SM_ARCH "gfx950"  // the build's --offload-arch (Makefile ARCH)
+#endif
+
 namespace sm {
 
 namespace {
@@ -87,7 +91,7 @@ std::string blob_array(const std::vector<char>& blob) {
 
 }  // namespace
 
-std::string nfa_jit_source(const std::vector<char>& blob) {
+std::string nfa_jit_source(const std::vector<char>& blob, bool lds) {
   std::string src = kPrelude;
   // Occupancy: room for 3 waves per SIMD (170 VGPRs). Measured on config 5 (N = 1e8, heap_words 1024, NFA kernel
   // ms): interpreter 74.3; JIT with the compiler's choice (268 VGPRs, 1 wave) 74.9, 2 waves 65.5, 4 waves 63.5;
@@ -101,22 +105,37 @@ std::string nfa_jit_source(const std::vector<char>& blob) {
   // every member function on the event path inline (A/B: SM_NFA_JIT_INLINE_ALL=0 leaves it to the compiler)
   const char* e = getenv("SM_NFA_JIT_INLINE_ALL");
   if (!e || atoi(e)) src += "#define SM_NFA_JIT_INLINE_ALL 1\n";
-  if (nfa_jit_lds()) src += "#define SM_NFA_LDS 1\n";
+  if (lds) src += "#define SM_NFA_LDS 1\n";
   src += blob_array(blob);
   src += kNfaJitBody;
   src += kKernel;
   return src;
 }
 
+std::string nfa_jit_source(const std::vector<char>& blob) { return nfa_jit_source(blob, nfa_jit_lds_bytes(blob) > 0); }
+
 bool nfa_jit_lds() {
   static const char* env = getenv("SM_NFA_JIT_LDS");
   return !env || atoi(env) != 0;
 }
 
+namespace {
+// LDS a workgroup may allocate on the current device (0 without a device: the build check then assumes it fits)
+int64_t device_lds_limit() {
+  int dev = 0, v = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) return 0;
+  return v;
+}
+}  // namespace
+
 int64_t nfa_jit_lds_bytes(const std::vector<char>& blob) {
   if (!nfa_jit_lds()) return 0;
   const DQuery* q = (const DQuery*)blob.data();
-  return (int64_t)(q->ks_sched + 3) * 64 * 8;  // (pre words + post bits word + kNfaLdsMisc) x 64 lanes
+  const int64_t need = (int64_t)(q->ks_sched + 3) * 64 * 8;  // (pre words + post bits word + kNfaLdsMisc) x 64 lanes
+  static const int64_t limit = device_lds_limit();
+  // a plan whose staged key state exceeds the workgroup's LDS keeps it in HBM (the interpreter's layout)
+  return limit > 0 && need > limit ? 0 : need;
 }
 
 bool nfa_jit_wanted(int option, int64_t records) {
@@ -124,6 +143,18 @@ bool nfa_jit_wanted(int option, int64_t records) {
   if (env && *env) return atoi(env) != 0;
   if (option >= 0) return option != 0;
   return records >= (int64_t)1 << 20;  // the compile (seconds) pays off on large batches only
+}
+
+std::string nfa_jit_arch() {
+  // the device's own target when one is visible (its gcnArchName without the feature suffix), else the build's
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) {
+    std::string a = prop.gcnArchName;
+    a = a.substr(0, a.find(':'));
+    if (a.rfind("gfx", 0) == 0) return a;
+  }
+  return SM_ARCH;
 }
 
 std::vector<char> nfa_jit_compile(const std::vector<char>& blob) {
@@ -137,7 +168,8 @@ std::vector<char> nfa_jit_compile(const std::vector<char>& blob) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "sm_nfa_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     throw std::runtime_error("nfa jit: hiprtcCreateProgram failed");
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pass-failed"};
+  const std::string arch = "--offload-arch=" + nfa_jit_arch();
+  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17", "-Wno-pass-failed"};
   const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
   if (rc != HIPRTC_SUCCESS) {
     size_t ls = 0;
@@ -158,14 +190,23 @@ std::vector<char> nfa_jit_compile(const std::vector<char>& blob) {
 void* nfa_jit_function(const std::vector<char>& blob) {
   int dev = 0;
   SM_HIP(hipGetDevice(&dev));
-  std::string key = std::to_string(dev) + ":" + nfa_jit_source(blob);  // the source carries the knobs too
-  std::lock_guard<std::mutex> g(g_mu);
-  auto it = cache().find(key);
-  if (it != cache().end()) return (void*)it->second->fn;
+  const std::string key = std::to_string(dev) + ":" + nfa_jit_source(blob);  // the source carries the knobs too
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = cache().find(key);
+    if (it != cache().end()) return (void*)it->second->fn;
+  }
+  // compile (seconds) without holding the cache: other apps' queries keep launching their kernels meanwhile
   const std::vector<char> code = nfa_jit_compile(blob);
   auto k = std::make_unique<JitKernel>();
   SM_HIP(hipModuleLoadData(&k->mod, code.data()));
   SM_HIP(hipModuleGetFunction(&k->fn, k->mod, "sm_nfa_jit"));
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = cache().find(key);
+  if (it != cache().end()) {  // compiled concurrently by another thread: keep the first
+    (void)hipModuleUnload(k->mod);
+    return (void*)it->second->fn;
+  }
   void* fn = (void*)k->fn;
   cache()[key] = std::move(k);
   return fn;

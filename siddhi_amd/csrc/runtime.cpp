@@ -406,12 +406,6 @@ void build_app(sm_app* a) {
     const sql::Query& qd = pi < 0 ? a->ast.queries[qi] : a->ast.partitions[pi].queries[qi];
     auto q = std::make_unique<QueryRt>();
     q->cq = compile_query(a->ast, qd, (int)o, pi, a->dict);
-    for (int s : q->cq.streams) {
-      if (!a->ast.streams[s].implicit) continue;
-      a->stream_fed[s] = 1;
-      for (int pq : producers[s]) q->level = std::max(q->level, a->queries[pq]->level + 1);
-    }
-    a->max_level = std::max(a->max_level, q->level);
     if (pi >= 0) {
       q->part = &a->parts[pi];
       q->pidx = pi;
@@ -452,14 +446,41 @@ void build_app(sm_app* a) {
       }
     }
     const int out = sm::stream_index(a->ast, qd.insert_into);
-    if (out >= 0 && a->ast.streams[out].implicit) {
-      const auto& at = a->ast.streams[out].attrs;
-      bool same = at.size() == q->cq.sel_types.size();
-      for (size_t k = 0; same && k < at.size(); ++k) same = (int)at[k].type == q->cq.sel_types[k];
-      if (!same) throw sql::ValidationError("query '" + q->cq.name + "' output does not match stream '" + qd.insert_into + "'");
-      producers[out].push_back((int)a->queries.size());
-    }
+    if (out >= 0) producers[out].push_back((int)a->queries.size());
     a->queries.push_back(std::move(q));
+  }
+  // Chaining levels by the producer / consumer relation (InsertIntoStreamCallback → StreamJunction.sendEvent →
+  // the queries reading that stream), whether the stream was declared with `define stream` or named only by
+  // `insert into`. The level merge (run_chained) places an inserted event before its root input event, which is
+  // the reference's order when every reader of the stream was defined after its producers (the producer then sits
+  // earlier on the root stream's junction); a reader defined before a producer of its stream is refused rather than
+  // given another order.
+  for (size_t qi = 0; qi < a->queries.size(); ++qi) {
+    QueryRt& q = *a->queries[qi];
+    for (int s : q.cq.streams) {
+      if (producers[s].empty()) continue;
+      a->stream_fed[s] = 1;
+      for (int pq : producers[s]) {
+        if (pq >= (int)qi)
+          throw sql::UnsupportedError("query '" + q.cq.name + "' reads stream '" + a->ast.streams[s].id +
+                                      "', which query '" + a->queries[pq]->cq.name +
+                                      "' defined at or after it inserts into");
+        q.level = std::max(q.level, a->queries[pq]->level + 1);
+      }
+    }
+    a->max_level = std::max(a->max_level, q.level);
+  }
+  // an output must fit the stream it goes into (DefinitionParserHelper.validateOutputStream): checked for the streams
+  // the parser defined from `insert into` and for every stream another query reads
+  for (size_t s = 0; s < producers.size(); ++s) {
+    if (!a->ast.streams[s].implicit && !a->stream_fed[s]) continue;
+    const auto& at = a->ast.streams[s].attrs;
+    for (int pq : producers[s]) {
+      const CompiledQuery& cq = a->queries[pq]->cq;
+      bool same = at.size() == cq.sel_types.size();
+      for (size_t k = 0; same && k < at.size(); ++k) same = (int)at[k].type == cq.sel_types[k];
+      if (!same) throw sql::ValidationError("query '" + cq.name + "' output does not match stream '" + a->ast.streams[s].id + "'");
+    }
   }
 }
 
@@ -834,9 +855,21 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
     launch_lane_balance(key_off, (int32_t)nkeys, perm, a->sc, hs);
     b.lane_perm = perm;
   }
-  if (nfa_jit_wanted(a->nfa_jit, nq))
-    launch_nfa_jit(nfa_jit_function(q.cq.blob), nfa_jit_lds_bytes(q.cq.blob), b, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
-                   (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
+  void* jit = nullptr;
+  if (nfa_jit_wanted(a->nfa_jit, nq)) {
+    try {
+      jit = nfa_jit_function(q.cq.blob);
+    } catch (const std::exception& e) {
+      // the automatic mode falls back to the interpreter (same semantics); an explicit nfa_jit = 1 reports it
+      if (a->nfa_jit == 1) throw;
+      fprintf(stderr, "[siddhi_amd] query '%s': query-specialised NFA kernel unavailable, using the interpreter (%s)\n",
+              q.cq.name.c_str(), e.what());
+      a->nfa_jit = 0;
+    }
+  }
+  if (jit)
+    launch_nfa_jit(jit, nfa_jit_lds_bytes(q.cq.blob), b, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half,
+                   q.state_slots, (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
   else
     launch_nfa(b, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
                (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
@@ -2457,8 +2490,8 @@ int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t 
                           void* const* d_dst, uint64_t* counts, void* hip_stream) {
   return guarded([&] {
     if (ncols < 0 || ncols > sm::kMaxPartCols) throw std::invalid_argument("ncols out of range");
-    if (key_width != 1 && key_width != 2 && key_width != 4 && key_width != 8)
-      throw std::invalid_argument("key width must be 1, 2, 4 or 8 bytes");
+    if (key_width != 4 && key_width != 8)
+      throw std::invalid_argument("key width must be 4 or 8 bytes (widen narrower integer keys)");
     sm::PartCols pc{};
     pc.n = ncols;
     for (int c = 0; c < ncols; ++c) {

@@ -20,7 +20,9 @@ single-process output. `concat_ordered` is the same idea for index-range shards 
 import torch
 import torch.distributed as dist
 
-_INT_DTYPES = (torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64)
+# partition keys: 32- or 64-bit integers (the owner hash reads the key's 64-bit two's complement; a narrower key
+# would need its signedness passed to the device, so it is widened by the caller instead)
+_INT_DTYPES = (torch.int32, torch.int64)
 _BY_WIDTH = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
 
 
@@ -30,8 +32,8 @@ def _i64(v):
 
 def _check_keys(keys: torch.Tensor):
     if keys.dtype not in _INT_DTYPES:
-        raise TypeError(f"partition keys must be an integer tensor, got {keys.dtype} (hash a non-integer key to an "
-                        "integer first)")
+        raise TypeError(f"partition keys must be an int32 or int64 tensor, got {keys.dtype} (widen a narrower "
+                        "integer key, hash a non-integer key to an integer first)")
     if keys.dim() != 1:
         raise ValueError("partition keys must be a 1-D tensor")
 

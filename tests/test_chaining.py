@@ -42,6 +42,13 @@ APPS = {
                                      "@info(name='q1') from every e1=S -> e2=S2[price > e1.price] "
                                      "select e1.symbol as s1, e2.price as p insert into #M; "
                                      "@info(name='q2') from #M[p > 50] select s1, p insert into O; end;",
+    # the intermediate streams declared with `define stream` (not only named by `insert into`)
+    "declared_intermediate": S + "define stream X (symbol string, price float, quantity int); "
+                                 "define stream P (a float, b float); "
+                                 "@info(name='q1') from S[price > 40] select symbol, price, quantity insert into X; "
+                                 "@info(name='q2') from every e1=X -> e2=X[price > e1.price] "
+                                 "select e1.price as a, e2.price as b insert into P; "
+                                 "@info(name='q3') from P[b - a > 5] select a, b insert into O;",
     # S2 is not keyed: each S2 event reaches every instance that exists when it arrives (A17)
     "broadcast": S + S2 + "partition with (quantity of S) begin "
                           "@info(name='q1') from every e1=S[price > 50] -> e2=S2[price < e1.price] "
@@ -101,3 +108,17 @@ def test_device_batches_refuse_chained_apps():
     with pytest.raises(EngineError):
         app.process_device_batch("S", torch.arange(n, dtype=torch.int64, device=dev), cols)
     app.close()
+
+
+def test_reader_defined_before_producer_is_refused():
+    """A query reading a declared stream that a LATER query inserts into: the reference delivers the inserted
+    events after the reader has seen their root event on the shared junction; the product's chaining levels assume
+    the other order, so the app is refused (SM_E_UNSUPPORTED) instead of answered in a different order."""
+    from siddhi_amd.testing import EngineError, ProductApp
+    text = (S + "define stream X (symbol string, price float); "
+            "@info(name='q2') from every e1=X -> e2=S[price < e1.price] select e1.price as a, e2.price as b "
+            "insert into O; "
+            "@info(name='q1') from S[price > 50] select symbol, price insert into X;")
+    with pytest.raises(EngineError) as ei:
+        ProductApp(text)
+    assert ei.value.code == 3

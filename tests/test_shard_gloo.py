@@ -282,3 +282,15 @@ def test_config5_sharded_with_heartbeats_equal_single_process(world, body, tmp_p
     for p in parts:
         idx = [pos[key(r)].pop(0) for r in p]
         assert idx == sorted(idx), "a rank's outputs are out of the global order"
+
+
+def test_narrow_keys_rejected_consistently():
+    """Partition keys are 32- or 64-bit integers on both the host (torch) and the device (sm_partition_by_owner)
+    paths: a narrower key has no signedness on the device, so it is refused on both instead of hashed two ways."""
+    import pytest as _pt
+    from siddhi_amd import shard
+    for dt in (torch.int8, torch.uint8, torch.int16):
+        with _pt.raises(TypeError):
+            shard.owner_of(torch.arange(10, dtype=dt), 3)
+        with _pt.raises(TypeError):
+            shard.partition_by_owner(torch.arange(10, dtype=dt), [torch.arange(10)], 3)
