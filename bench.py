@@ -548,7 +548,7 @@ def main():
 # ALGORITHMIC bytes per launch for a batch of n events with m matches: what each launch must read
 # and write at minimum.
 KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last",
-           "stack_prep", "stack", "order", "carry_merge", "carry_out",
+           "stack_prep", "stack_rank", "stack", "order_count", "order", "carry_merge", "carry_out",
            "filter_count", "filter_scan", "filter_write",
            "event_index", "nfa_select", "nfa_group", "nfa_setup", "nfa"]
 
@@ -565,8 +565,10 @@ def alg_bytes(label, n, m, config):
             "walk": (16 * n + 8 * m) if keyed else (16 * n + n // 8 + 8 * m),  # records (unkeyed: price + ts +
                                                                                # c1 bits) in, (j, i) pairs out
             "stack_prep": 0,                # staging bases (O(kBins))
-            "stack": 16 * n + 8 * m,        # bucket records in, staged (j, i) pairs out (bucket order)
-            "order": 8 * m + 8 * m,         # staged pairs in, output pairs out (reference order)
+            "stack_rank": 16 * n + 2 * n,   # bucket records in, key-grouped u16 in-slice positions out
+            "stack": 16 * n + 2 * n + n + 8 * m,  # positions + records in; pop counts + pops (j, i) out
+            "order_count": n,               # pop counts in
+            "order": n + 8 * m + 8 * m,     # pop counts + pops in, output pairs out (reference order)
             "carry_merge": 16 * m,
             "carry_out": 0,                 # open partials at the end of the batch (O(keys))
             "j_up": 4 * m,
