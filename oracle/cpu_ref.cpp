@@ -593,13 +593,172 @@ struct AppStream {
   std::vector<Sub> subs;
 };
 
+// java.util.concurrent.ConcurrentHashMap<String, StreamJunction> as PartitionStreamReceiver.cachedStreamJunctionMap
+// uses it (one thread, puts of new keys, values() traversal), Java 8: putVal :1011-1059, initTable :2224-2245,
+// addCount :2265-2302, treeifyBin :2615-2640, tryPresize :2319-2357, transfer :2363-2507, TreeBin.putTreeVal
+// (prepends to `first`), Traverser.advance :3315-3351.
+struct JavaJunctionMap {
+  struct Node {
+    int32_t hash;
+    int value;  // instance index
+    Node* next;
+  };
+  struct Bin {
+    Node* first = nullptr;
+    bool treebin = false;
+    int count() const {
+      int c = 0;
+      for (Node* e = first; e; e = e->next) ++c;
+      return c;
+    }
+  };
+  std::deque<Node> nodes;
+  std::vector<Bin> table;
+  int64_t sizeCtl = 0, baseCount = 0;
+
+  static int32_t string_hash(const std::string& s) {  // String.hashCode over UTF-16 units of the UTF-8 text
+    int32_t h = 0;
+    auto add = [&](uint32_t u) { h = (int32_t)(31u * (uint32_t)h + u); };
+    size_t i = 0;
+    while (i < s.size()) {
+      uint32_t c = (unsigned char)s[i], cp;
+      int extra = c >= 0xf0 ? 3 : c >= 0xe0 ? 2 : c >= 0xc0 ? 1 : 0;
+      cp = extra == 0 ? c : extra == 1 ? (c & 0x1f) : extra == 2 ? (c & 0x0f) : (c & 0x07);
+      for (int k = 1; k <= extra && i + k < s.size(); ++k) cp = (cp << 6) | ((unsigned char)s[i + k] & 0x3f);
+      i += 1 + extra;
+      if (cp > 0xffff) {
+        add(0xd800 + ((cp - 0x10000) >> 10));
+        add(0xdc00 + ((cp - 0x10000) & 0x3ff));
+      } else {
+        add(cp);
+      }
+    }
+    return h;
+  }
+  static int32_t spread(int32_t h) { return (h ^ (int32_t)((uint32_t)h >> 16)) & 0x7fffffff; }
+
+  void transfer() {
+    const int64_t n = (int64_t)table.size();
+    std::vector<Bin> nt((size_t)(n << 1));
+    for (int64_t i = n - 1; i >= 0; --i) {  // bins claimed from the top (order does not matter for the result)
+      Bin& f = table[(size_t)i];
+      if (!f.first) continue;
+      Node *ln = nullptr, *hn = nullptr;
+      if (!f.treebin) {
+        int64_t runBit = f.first->hash & n;
+        Node* lastRun = f.first;
+        for (Node* p = f.first->next; p; p = p->next) {
+          const int64_t b = p->hash & n;
+          if (b != runBit) {
+            runBit = b;
+            lastRun = p;
+          }
+        }
+        if (runBit == 0) ln = lastRun;
+        else hn = lastRun;
+        for (Node* p = f.first; p != lastRun; p = p->next) {
+          nodes.push_back(Node{p->hash, p->value, nullptr});
+          Node* q = &nodes.back();
+          if ((p->hash & n) == 0) {
+            q->next = ln;
+            ln = q;
+          } else {
+            q->next = hn;
+            hn = q;
+          }
+        }
+        nt[(size_t)i].first = ln;
+        nt[(size_t)(i + n)].first = hn;
+      } else {
+        Node *lo = nullptr, *loTail = nullptr, *hi = nullptr, *hiTail = nullptr;
+        int lc = 0, hc = 0;
+        for (Node* e = f.first; e; e = e->next) {
+          nodes.push_back(Node{e->hash, e->value, nullptr});
+          Node* p = &nodes.back();
+          if ((e->hash & n) == 0) {
+            (loTail ? loTail->next : lo) = p;
+            loTail = p;
+            ++lc;
+          } else {
+            (hiTail ? hiTail->next : hi) = p;
+            hiTail = p;
+            ++hc;
+          }
+        }
+        nt[(size_t)i].first = lo;
+        nt[(size_t)i].treebin = lc > 6;  // UNTREEIFY_THRESHOLD
+        nt[(size_t)(i + n)].first = hi;
+        nt[(size_t)(i + n)].treebin = hc > 6;
+      }
+    }
+    table.swap(nt);
+    sizeCtl = (n << 1) - (n >> 1);
+  }
+
+  void tryPresize(int64_t size) {
+    int64_t c = 1;
+    while (c < size + (size >> 1) + 1) c <<= 1;  // tableSizeFor
+    while (sizeCtl >= 0) {
+      const int64_t n = (int64_t)table.size();
+      if (c <= sizeCtl || n >= (1 << 30)) break;
+      transfer();
+    }
+  }
+
+  void put(const std::string& key, int value) {
+    const int32_t hash = spread(string_hash(key));
+    if (table.empty()) {  // initTable
+      table.resize(16);
+      sizeCtl = 16 - (16 >> 2);
+    }
+    const int64_t n = (int64_t)table.size();
+    const size_t i = (size_t)((n - 1) & hash);
+    Bin& f = table[i];
+    int binCount = 0;
+    nodes.push_back(Node{hash, value, nullptr});
+    Node* x = &nodes.back();
+    if (!f.first) {
+      f.first = x;
+    } else if (!f.treebin) {
+      binCount = 1;
+      Node* e = f.first;
+      while (e->next) {
+        e = e->next;
+        ++binCount;
+      }
+      e->next = x;
+    } else {
+      binCount = 2;
+      x->next = f.first;
+      f.first = x;
+    }
+    if (binCount >= 8) {  // treeifyBin
+      if (n < 64) tryPresize(n << 1);
+      else if (!table[i].treebin) table[i].treebin = true;
+    }
+    ++baseCount;  // addCount(1, binCount)
+    while (baseCount >= sizeCtl && (int64_t)table.size() < (1 << 30)) transfer();
+  }
+
+  std::vector<int> values() const {
+    std::vector<int> out;
+    for (const Bin& b : table)
+      for (Node* e = b.first; e; e = e->next) out.push_back(e->value);
+    return out;
+  }
+};
+
 struct PartitionRt {
   const Partition* p = nullptr;
   int partition_index = 0;
   std::map<std::string, std::vector<const CExpr*>> key_exec;  // stream id -> key executors
   std::vector<CExprP> key_owned;
   std::unordered_map<std::string, int> key_index;               // key -> instance idx
+  std::vector<std::string> inst_key;                             // key of each instance, creation order
   std::vector<std::vector<std::unique_ptr<QueryRt>>> instances;  // per key: one runtime per query
+  // per stream the partition does not key: its receiver's cachedStreamJunctionMap (streamId + key → junction)
+  std::map<std::string, JavaJunctionMap*> junction_maps;
+  std::vector<std::unique_ptr<JavaJunctionMap>> junction_owned;
 };
 
 struct QueryOutputs {
@@ -1665,6 +1824,38 @@ void deliver(QueryRt* q, const std::string& sid, const RowP& row, int64_t ts) {
   }
 }
 
+// Double.toString / Float.toString (java.lang.Double:195-280 javadoc): "NaN", "Infinity", "0.0"; for
+// 10^-3 <= |d| < 10^7 the integer part, '.', and at least one fraction digit; otherwise computerized scientific
+// notation d.ddd"E"n. Digits: as many as needed to distinguish the value (here: the shortest round-trip digits).
+template <typename F>
+std::string java_fp(F v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v < 0 ? "-Infinity" : "Infinity";
+  if (v == 0) return std::signbit(v) ? "-0.0" : "0.0";
+  char b[64];
+  auto r = std::to_chars(b, b + 64, v, std::chars_format::scientific);
+  const std::string t(b, r.ptr);
+  const bool neg = t[0] == '-';
+  const size_t epos = t.find('e');
+  std::string dig;
+  for (size_t k = neg ? 1 : 0; k < epos; ++k)
+    if (t[k] != '.') dig.push_back(t[k]);
+  const int e10 = std::stoi(t.substr(epos + 1));  // value = d.ddd x 10^e10
+  std::string o = neg ? "-" : "";
+  if (e10 >= 7 || e10 < -3) {
+    o += dig[0];
+    o += '.';
+    o += dig.size() > 1 ? dig.substr(1) : "0";
+    o += "E" + std::to_string(e10);
+  } else if (e10 < 0) {
+    o += "0." + std::string(-e10 - 1, '0') + dig;
+  } else {
+    while ((int)dig.size() < e10 + 2) dig.push_back('0');
+    o += dig.substr(0, e10 + 1) + "." + dig.substr(e10 + 1);
+  }
+  return o;
+}
+
 std::string key_string(const OApp* a, const Value& v) {
   // ValuePartitionExecutor.execute :34-40 → String.valueOf; null → event dropped
   switch (v.t) {
@@ -1672,21 +1863,12 @@ std::string key_string(const OApp* a, const Value& v) {
     case AttrType::LONG: return std::to_string(v.i);
     case AttrType::BOOL: return v.i ? "true" : "false";
     case AttrType::STRING: return a->strings.strs[v.s];
-    case AttrType::FLOAT: {
-      if (std::isnan(v.d)) return "NaN";
-      char b[64];
-      auto r = std::to_chars(b, b + 64, (float)v.d);
-      return std::string(b, r.ptr);
-    }
-    case AttrType::DOUBLE: {
-      if (std::isnan(v.d)) return "NaN";
-      char b[64];
-      auto r = std::to_chars(b, b + 64, v.d);
-      return std::string(b, r.ptr);
-    }
+    case AttrType::FLOAT: return java_fp((float)v.d);
+    case AttrType::DOUBLE: return java_fp(v.d);
   }
   return "";
 }
+
 
 // EventTimeBasedMillisTimestampGenerator.setCurrentTimestamp :99-116 → listeners → Scheduler.sendTimerEvents
 // Wall-clock emulation (SystemTimeBasedScheduler fires each timer at its scheduled time): step the clock
@@ -1727,11 +1909,20 @@ void dispatch(OApp* a, int si, const RowP& row, int64_t ts) {
       deliver(a->queries[sub.index].get(), st.def->id, row, ts);
     } else if (sub.kind == 2) {
       // PartitionStreamReceiver.send(ComplexEvent) :271-275: a stream the partition does not key is sent to every
-      // existing instance. The reference iterates a ConcurrentHashMap of the instances' junctions; instances are
-      // visited here in creation order (the same whenever one instance exists when the event arrives).
+      // existing instance, in cachedStreamJunctionMap.values() order. addStreamJunction (:284-300) put
+      // streamId + key into that map as each instance was created (PartitionRuntime.updatePartitionStreamReceivers
+      // :311-315), so the map is brought up to the instances existing now, in creation order, and traversed.
       PartitionRt* pr = a->partitions[sub.index].get();
-      for (size_t inst = 0; inst < pr->instances.size(); ++inst)
-        for (auto& qrt : pr->instances[inst])
+      auto jm = pr->junction_maps.find(st.def->id);
+      if (jm == pr->junction_maps.end()) {
+        pr->junction_owned.push_back(std::make_unique<JavaJunctionMap>());
+        jm = pr->junction_maps.emplace(st.def->id, pr->junction_owned.back().get()).first;
+      }
+      JavaJunctionMap& m = *jm->second;
+      while ((size_t)m.baseCount < pr->inst_key.size())
+        m.put(st.def->id + pr->inst_key[(size_t)m.baseCount], (int)m.baseCount);
+      for (int inst : m.values())
+        for (auto& qrt : pr->instances[(size_t)inst])
           if (reads(qrt.get(), st.def->id)) deliver(qrt.get(), st.def->id, row, ts);
     } else {
       PartitionRt* pr = a->partitions[sub.index].get();
@@ -1749,6 +1940,7 @@ void dispatch(OApp* a, int si, const RowP& row, int64_t ts) {
           // PartitionRuntime.clonePartition :262-309: one fresh QueryRuntime per partition query
           inst = (int)pr->instances.size();
           pr->key_index.emplace(key, inst);
+          pr->inst_key.push_back(key);
           pr->instances.emplace_back();
           for (size_t qi = 0; qi < pr->p->queries.size(); ++qi) {
             int order_index = 0;

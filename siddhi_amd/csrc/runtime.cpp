@@ -33,6 +33,7 @@
 #include "kernels/primitives.h"
 #include "kernels/stream_ops.h"
 #include "kernels/partition.h"
+#include "java_order.h"
 #include "nfa_jit.h"
 #include "siddhiql/ast.h"
 
@@ -230,7 +231,11 @@ struct sm_app {
   // codes of its instances in creation order (the instances a broadcast event reaches)
   std::vector<std::vector<int>> part_bcast;
   std::vector<std::vector<int64_t>> part_keys;
+  std::vector<std::vector<int32_t>> part_key_types;  // the key's attribute type per instance (its Java string form)
   std::vector<std::unordered_set<int64_t>> part_key_set;
+  // per partition and stream it broadcasts: the partition receiver's place among that stream's junction receivers
+  // (the app order of the partition's first query reading it: PartitionRuntime.addPartitionReceiver subscribes then)
+  std::vector<std::map<int, int32_t>> part_bcast_group;
   bool fast_timing = false;
   bool fast_tm_ready = false;
   sm::FastTimings fast_tm{};
@@ -400,7 +405,9 @@ void build_app(sm_app* a) {
   a->stream_fed.assign(a->ast.streams.size(), 0);
   a->part_bcast.assign(a->ast.partitions.size(), {});
   a->part_keys.assign(a->ast.partitions.size(), {});
+  a->part_key_types.assign(a->ast.partitions.size(), {});
   a->part_key_set.assign(a->ast.partitions.size(), {});
+  a->part_bcast_group.assign(a->ast.partitions.size(), {});
   for (size_t o = 0; o < a->ast.order.size(); ++o) {
     auto [pi, qi] = a->ast.order[o];
     const sql::Query& qd = pi < 0 ? a->ast.queries[qi] : a->ast.partitions[pi].queries[qi];
@@ -423,6 +430,7 @@ void build_app(sm_app* a) {
             if (cpm.key_code[k].size() != 1 || cpm.key_code[k][0].op != OP_COL)
               throw sql::UnsupportedError("a partition whose queries read an unkeyed stream needs columns as keys");
           q->bcast = true;
+          if (!a->part_bcast_group[pi].count(s)) a->part_bcast_group[pi][s] = q->cq.hdr.query_order;
           if (std::find(a->part_bcast[pi].begin(), a->part_bcast[pi].end(), s) == a->part_bcast[pi].end()) {
             Instr in{};
             in.op = OP_COL;
@@ -611,6 +619,12 @@ bool out_before(const OutRec& x, const OutRec& y) {
     if (x.query != y.query) return x.query < y.query;
     return x.sched < y.sched;
   }
+  // data phase: the trigger's junction receivers in subscription order (query order); a partition receiver hands a
+  // broadcast event to its instances one after another (time = the instance's rank in the receiver's
+  // ConcurrentHashMap iteration + 1, sched = the receiver's place), each instance's queries in query order
+  const int32_t gx = x.time ? x.sched : x.query, gy = y.time ? y.sched : y.query;
+  if (gx != gy) return gx < gy;
+  if (x.time != y.time) return x.time < y.time;
   return x.query < y.query;
 }
 
@@ -1279,7 +1293,8 @@ EvArrays upload_batch(sm_app* a, std::vector<StreamStage>& stages, const EvHost&
 // instances before the batch; each keyed event (a key column that is not null) of a new key appends one.
 // at[p] = instances existing when position p is delivered (its own instance included).
 void walk_instances(const sm_app* a, int pi, const std::vector<StreamStage>& stages, const EvHost& e,
-                    std::vector<int64_t>& keys, std::unordered_set<int64_t>& kset, std::vector<int64_t>* at) {
+                    std::vector<int64_t>& keys, std::vector<int32_t>& types, std::unordered_set<int64_t>& kset,
+                    std::vector<int64_t>* at) {
   const CompiledPartition& cp = a->parts[pi];
   const std::vector<int>& bc = a->part_bcast[pi];
   const int64_t N = (int64_t)e.stream->size();
@@ -1290,9 +1305,11 @@ void walk_instances(const sm_app* a, int pi, const std::vector<StreamStage>& sta
       const auto it = std::find(cp.streams.begin(), cp.streams.end(), s);
       if (it != cp.streams.end()) {
         int64_t code;
-        if (host_key_code(stages[s], cp.key_code[it - cp.streams.begin()][0].a, (*e.row)[p], &code) &&
-            kset.insert(code).second)
+        const int col = cp.key_code[it - cp.streams.begin()][0].a;
+        if (host_key_code(stages[s], col, (*e.row)[p], &code) && kset.insert(code).second) {
           keys.push_back(code);
+          types.push_back(col < (int)stages[s].def->attrs.size() ? (int32_t)stages[s].def->attrs[col].type : T_LONG);
+        }
       }
     }
     if (at) (*at)[p] = (int64_t)keys.size();
@@ -1300,18 +1317,42 @@ void walk_instances(const sm_app* a, int pi, const std::vector<StreamStage>& sta
 }
 
 // A query reading a stream its partition does not key, over a copy of the batch in which each such event is
-// repeated once per instance existing at that point, in creation order (the reference iterates a
-// ConcurrentHashMap of the instances' junctions; with one instance the orders agree), the copy's extra column
-// holding the instance's key code. Its outputs move back to the original event's position; an output of the
-// k-th copy ranks after those of copies < k (seq).
+// repeated once per instance existing at that point, in the order PartitionStreamReceiver.send (:271-275) visits
+// them: cachedStreamJunctionMap.values(), a ConcurrentHashMap keyed by streamId + String.valueOf(key) and filled in
+// creation order (java_order.h). The copy's extra column holds the instance's key code. Its outputs move back to
+// the original event's position, ranked by the copy's place in that iteration (OutRec.time = rank + 1) under the
+// partition receiver's place among the stream's receivers (OutRec.sched).
 void run_bcast_query(sm_app* a, int qi, std::vector<StreamStage>& stages, const EvHost& e, std::vector<HostOut>& outs) {
   QueryRt& q = *a->queries[qi];
   const int pi = q.pidx;
   const std::vector<int>& bc = a->part_bcast[pi];
   std::vector<int64_t> keys = a->part_keys[pi];
+  std::vector<int32_t> ktypes = a->part_key_types[pi];
   std::unordered_set<int64_t> kset = a->part_key_set[pi];
   std::vector<int64_t> at;
-  walk_instances(a, pi, stages, e, keys, kset, &at);
+  walk_instances(a, pi, stages, e, keys, ktypes, kset, &at);
+  // the receiver's junction map per broadcast stream, grown in creation order as the batch creates instances
+  struct Chm {
+    JavaChmOrder map;
+    std::vector<int> order;
+    size_t ordered = 0;  // map size `order` was taken at
+  };
+  std::map<int, Chm> chm;
+  auto instance_order = [&](int s, int64_t count) -> const std::vector<int>& {
+    Chm& c = chm[s];
+    while ((int64_t)c.map.size() < count) {
+      const size_t k = c.map.size();
+      const std::string ks = ktypes[k] == T_STRING
+                                 ? (keys[k] >= 0 && keys[k] < (int64_t)a->dict.strs.size() ? a->dict.strs[keys[k]] : "")
+                                 : java_value_string(ktypes[k], keys[k]);
+      c.map.put(a->ast.streams[s].id + ks);
+    }
+    if (c.ordered != c.map.size() || c.order.empty()) {
+      c.order = c.map.order();
+      c.ordered = c.map.size();
+    }
+    return c.order;
+  };
   BatchBuilder b;
   b.init(stages, bc);
   const int64_t N = (int64_t)e.stream->size();
@@ -1321,6 +1362,7 @@ void run_bcast_query(sm_app* a, int qi, std::vector<StreamStage>& stages, const 
     const int s = (*e.stream)[p];
     const bool rep = s >= 0 && std::find(bc.begin(), bc.end(), s) != bc.end();
     const int64_t copies = rep ? at[p] : 1;
+    const std::vector<int>* ord = rep && copies > 0 ? &instance_order(s, copies) : nullptr;
     newpos[p] = (int64_t)b.stream.size();
     for (int64_t k = 0; k < copies; ++k) {
       b.put(s, (*e.ts)[p], (*e.clock)[p], (*e.ord)[p]);
@@ -1328,7 +1370,7 @@ void run_bcast_query(sm_app* a, int qi, std::vector<StreamStage>& stages, const 
       rank.push_back(rep ? k : -1);
       if (s < 0) continue;
       b.copy_row(s, stages[s], (*e.row)[p]);
-      if (rep) b.put_bytes(s, stages[s].cols.size(), (const uint8_t*)&keys[k], 8, false);
+      if (rep) b.put_bytes(s, stages[s].cols.size(), (const uint8_t*)&keys[(*ord)[k]], 8, false);
     }
   }
   for (size_t k = 0; k < e.adv_pos->size(); ++k) {
@@ -1348,8 +1390,14 @@ void run_bcast_query(sm_app* a, int qi, std::vector<StreamStage>& stages, const 
     HostOut& h = outs[i];
     if (h.r.key >= 0 && h.r.key < (int32_t)slot_keys.size()) h.key_code = slot_keys[h.r.key];
     const int64_t r = rank[h.r.pos];
+    const int s = (*e.stream)[map[h.r.pos]];
     h.r.pos = map[h.r.pos];
-    if (r >= 0) h.r.seq = (int32_t)(r * (1 << 20) + h.r.seq);
+    if (r >= 0 && h.r.phase == 1) {
+      h.r.time = r + 1;
+      h.r.sched = a->part_bcast_group[pi].at(s);
+    } else if (r >= 0) {
+      h.r.seq = (int32_t)(r * (1 << 20) + h.r.seq);
+    }
   }
 }
 
@@ -1432,7 +1480,7 @@ void run_chained(sm_app* a, std::vector<HostOut>& outs) {
   };
   auto out_key = [](const Key& trig, const OutRec& r) {
     Key k = trig.size() == 2 && trig[1] == 2 ? Key{trig[0]} : trig;
-    if (r.phase == 1) k.insert(k.end(), {1, r.query, r.seq});
+    if (r.phase == 1) k.insert(k.end(), {1, r.time ? r.sched : r.query, r.time, r.query, r.seq});
     else k.insert(k.end(), {0, r.time, r.create >= 0 ? 1 : 0, r.create, r.query, r.sched, r.seq});
     return k;
   };
@@ -1611,7 +1659,8 @@ void flush(sm_app* a) {
     if (a->max_level > 0) run_chained(a, outs);
     for (size_t pi = 0; pi < a->part_bcast.size(); ++pi)  // instances this batch created, for later broadcasts
       if (!a->part_bcast[pi].empty())
-        walk_instances(a, (int)pi, a->streams, e0, a->part_keys[pi], a->part_key_set[pi], nullptr);
+        walk_instances(a, (int)pi, a->streams, e0, a->part_keys[pi], a->part_key_types[pi], a->part_key_set[pi],
+                       nullptr);
   } catch (const std::exception& e) {
     a->failed = true;
     a->failed_why = std::string("a batch failed half-way (") + e.what() +
@@ -2014,6 +2063,7 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       a->failed_why.clear();
       for (auto& q : a->queries) q->nfa_used = q->nfa_mode = false;
       for (auto& k : a->part_keys) k.clear();
+      for (auto& k : a->part_key_types) k.clear();
       for (auto& k : a->part_key_set) k.clear();
       if (value) {  // reset and start again
         a->started = true;
@@ -2304,9 +2354,11 @@ int sm_app_snapshot(sm_app* a, uint8_t* buf, size_t cap, size_t* len) {
       w.raw(str.data(), str.size());
     }
     w.put<uint32_t>((uint32_t)a->part_keys.size());  // partition instances (broadcast targets), creation order
-    for (auto& k : a->part_keys) {
+    for (size_t pi = 0; pi < a->part_keys.size(); ++pi) {
+      const auto& k = a->part_keys[pi];
       w.put<uint64_t>(k.size());
       w.raw(k.data(), k.size() * 8);
+      w.raw(a->part_key_types[pi].data(), k.size() * 4);
     }
     w.put<uint32_t>((uint32_t)a->queries.size());
     const size_t heap_words = 2 * (size_t)a->heap_half + 64;
@@ -2391,6 +2443,8 @@ int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
     for (size_t pi = 0; pi < a->part_keys.size(); ++pi) {
       a->part_keys[pi].resize(r.get<uint64_t>());
       r.raw(a->part_keys[pi].data(), a->part_keys[pi].size() * 8);
+      a->part_key_types[pi].resize(a->part_keys[pi].size());
+      r.raw(a->part_key_types[pi].data(), a->part_keys[pi].size() * 4);
       a->part_key_set[pi] = std::unordered_set<int64_t>(a->part_keys[pi].begin(), a->part_keys[pi].end());
     }
     if (r.get<uint32_t>() != a->queries.size())
