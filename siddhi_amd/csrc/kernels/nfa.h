@@ -58,6 +58,12 @@ struct NfaBatch {
   uint32_t* out_count;
   uint32_t out_cap;
   uint32_t out_stride;
+  // device-wide overflow pool of per-key arenas: a key whose live partial matches outgrow its own arena moves its
+  // heap into a larger region bump-allocated here (Lane::promote). pool_top counts the words handed out (it may
+  // pass pool_cap: that request failed and the key stayed in its arena; the host grows the pool after the batch).
+  int64_t* pool;
+  unsigned long long* pool_top;
+  int64_t pool_cap;
 };
 
 // LaneEv records for key_pos[0, nq) of a batch of n records: b.lane_ev must point at nq * LaneEv::words(node_words)

@@ -1002,6 +1002,70 @@ struct Lane {
     heap[o] = K_FWD | ((int64_t)(uint32_t)n << 32);
     return n;
   }
+  // A key's heap in the overflow pool (misc(5) = pool offset + 1, misc(6) = its words per semispace) once its live
+  // partial matches no longer fit its own arena: the reference's pending lists are unbounded LinkedLists
+  // (StreamPreStateProcessor :58-59), so a hot key keeps growing while the other keys keep their small arenas.
+  // After a collection that leaves a semispace more than a quarter full, the live objects are copied (the same
+  // Cheney copy as gc, into a region of the pool) to a region with >= 8x their size per semispace.
+  __device__ int32_t fwd_to(int32_t o, int64_t& top, const LaneWords& dst) {
+    if (o < 0) return o;
+    const int64_t h0 = heap[o];
+    const int k = (int)(h0 & 0xFF);
+    if (k == K_FWD) return (int32_t)(h0 >> 32);
+    const int words = (k == K_REC) ? PQ->rec_words : (k == K_NODE) ? PQ->node_words : 2;
+    const int32_t n = (int32_t)top;
+    for (int w = 0; w < words; ++w) dst[n + w] = heap[o + w];
+    top += words;
+    heap[o] = K_FWD | ((int64_t)(uint32_t)n << 32);
+    return n;
+  }
+  __device__ void promote(int64_t live) {
+    int64_t nh = 2 * (int64_t)half;
+    if (nh < 8 * live) nh = 8 * live;
+    nh = (nh + 63) & ~(int64_t)63;
+    if (nh > ((int64_t)1 << 30)) return;  // heap offsets are 32-bit: stay (alloc reports an arena overflow)
+    const int64_t words = 2 * nh + 64;
+    if (!b->pool) return;
+    const int64_t off = (int64_t)atomicAdd(b->pool_top, (unsigned long long)words);
+    if (off + words > b->pool_cap) return;  // pool full: the host grows it after the batch
+    const LaneWords dst{b->pool + off, 1};
+    auto hi_of = [&](int64_t w) { return (int32_t)(w >> 32); };
+    auto with_hi = [&](int64_t w, int32_t v) { return (w & 0xFFFFFFFFll) | ((int64_t)(uint32_t)v << 32); };
+    int64_t top = 0, scan = 0;
+    for (int p = 0; p < PQ->npre; ++p)
+      for (int w = 0; w < 2; ++w) {
+        const int32_t h = fwd_to(lhead(p, w), top, dst);
+        const int32_t t = ltail(p, w) >= 0 ? fwd_to(ltail(p, w), top, dst) : -1;
+        lset(p, w, h, t);
+      }
+    while (scan < top) {
+      const int32_t o = (int32_t)scan;
+      const int64_t h0 = dst[o];
+      const int k = (int)(h0 & 0xFF);
+      if (k == K_LNODE) {
+        dst[o] = with_hi(h0, fwd_to(hi_of(h0), top, dst));
+        dst[o + 1] = fwd_to((int32_t)dst[o + 1], top, dst);
+        scan += 2;
+      } else if (k == K_REC) {
+        for (int s = 0; s < PQ->nslots; ++s) {
+          int64_t& w = dst[o + 2 + (s >> 1)];
+          const int32_t v = (s & 1) ? (int32_t)(w >> 32) : (int32_t)w;
+          const int32_t nv = fwd_to(v, top, dst);
+          w = (s & 1) ? with_hi(w, nv) : ((w & ~0xFFFFFFFFll) | (int64_t)(uint32_t)nv);
+        }
+        scan += PQ->rec_words;
+      } else {
+        dst[o] = with_hi(h0, fwd_to(hi_of(h0), top, dst));
+        scan += PQ->node_words;
+      }
+    }
+    heap = dst;
+    half = (int32_t)nh;
+    misc(2) = 0;
+    misc(1) = top;
+    misc(5) = off + 1;
+    misc(6) = nh;
+  }
   __device__ void gc() {
     int64_t space = misc(2);
     int64_t to = (1 - space) * half;
@@ -1033,7 +1097,11 @@ struct Lane {
   }
   SM_JIT_INL __device__ void safe_point() {
     int64_t used = misc(1) - misc(2) * half;
-    if (used * 2 > half) gc();
+    if (used * 2 > half) {
+      gc();
+      used = misc(1) - misc(2) * half;
+      if (used * 4 > half) promote(used);
+    }
   }
 
   // ------------------------------------------------------------ event delivery
@@ -1272,6 +1340,13 @@ SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ 
   // keeping each object's words in one line beats sharing lines with other lanes' (unrelated) offsets
   L.heap = LaneWords{heap_all + (int64_t)key * (2 * (int64_t)heap_half + 64), 1};
   L.b = &b;
+  {  // a key promoted to the overflow pool by an earlier batch (Lane::promote)
+    const int64_t po = L.ksh[PQ->ks_misc + 5];
+    if (po > 0) {
+      L.heap = LaneWords{b.pool + (po - 1), 1};
+      L.half = (int32_t)L.ksh[PQ->ks_misc + 6];
+    }
+  }
   L.key = key;
   L.err = 0;
   L.seq = 0;

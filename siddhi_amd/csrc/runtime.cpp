@@ -181,6 +181,10 @@ struct QueryRt {
   bool proj_nfa = false;
   DBuf nfa_proj;
   DBuf proj_out;  // device projection of a batch for its consumers (device_outputs)
+  // overflow pool of per-key arenas (NfaBatch::pool, Lane::promote): allocated words, words handed out
+  DBuf pool, pool_top_dev;
+  int64_t pool_words = 0;
+  uint64_t pool_used = 0;
   ~QueryRt() { carry.release(); }
 };
 
@@ -261,6 +265,7 @@ struct sm_app {
   bool shut = false;
   int64_t batch_events = 1 << 20;
   int32_t heap_half = 1024;
+  int64_t pool_init = (int64_t)1 << 25;  // option "pool_words": first size of a query's overflow pool (words)
   // NFA lanes in descending event-count order for batches with at least this many keys (0 = off;
   // SM_NFA_BALANCE=<min keys> / option "lane_balance")
   int64_t lane_balance = 0;
@@ -782,6 +787,25 @@ void ensure_state(sm_app* a, QueryRt& q, int64_t nkeys) {
   q.state_slots = cap;
 }
 
+// The query's overflow pool holds at least `words` words, the first `keep` of them preserved (a promoted key's heap
+// is addressed by its pool offset, so growing copies the used prefix into the larger buffer).
+void ensure_pool(sm_app* a, QueryRt& q, int64_t words, int64_t keep) {
+  if (!q.pool_top_dev.p) {
+    q.pool_top_dev.ensure(8);
+    SM_HIP(hipMemsetAsync(q.pool_top_dev.p, 0, 8, a->stream));
+  }
+  if (words <= q.pool_words) return;
+  void* np = nullptr;
+  SM_HIP(hipMalloc(&np, (size_t)words * 8));
+  keep = std::min(keep, q.pool_words);
+  if (keep > 0) SM_HIP(hipMemcpyAsync(np, q.pool.p, (size_t)keep * 8, hipMemcpyDeviceToDevice, a->stream));
+  SM_HIP(hipStreamSynchronize(a->stream));
+  q.pool.release();
+  q.pool.p = np;
+  q.pool.cap = (size_t)words * 8;
+  q.pool_words = words;
+}
+
 template <typename T>
 void upload(sm_app* a, DBuf& d, const std::vector<T>& v) {
   d.ensure(std::max<size_t>(v.size() * sizeof(T), 16));
@@ -860,6 +884,10 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.out_count = (uint32_t*)a->d_count.p;
   b.out_cap = (uint32_t)cap;
   b.out_stride = (uint32_t)stride;
+  ensure_pool(a, q, std::max<int64_t>(q.pool_words, a->pool_init), (int64_t)q.pool_used);
+  b.pool = (int64_t*)q.pool.p;
+  b.pool_top = (unsigned long long*)q.pool_top_dev.p;
+  b.pool_cap = q.pool_words;
   SM_HIP(hipMemsetAsync(a->d_count.p, 0, 4, hs));
   SM_HIP(hipMemsetAsync(a->d_err.p, 0, 4, hs));
   launch_lane_events(b, N, nq, h.node_words, (int32_t*)a->sc.take((size_t)std::max<int64_t>(N, 1) * 4), hs);
@@ -893,10 +921,16 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   int32_t he = 0;
   SM_HIP(hipMemcpyAsync(&hc, a->d_count.p, 4, hipMemcpyDeviceToHost, hs));
   SM_HIP(hipMemcpyAsync(&he, a->d_err.p, 4, hipMemcpyDeviceToHost, hs));
+  SM_HIP(hipMemcpyAsync(&q.pool_used, q.pool_top_dev.p, 8, hipMemcpyDeviceToHost, hs));
   SM_HIP(hipStreamSynchronize(hs));
+  // keep the pool at most half full for the next batch's promotions
+  if ((int64_t)q.pool_used * 2 > q.pool_words)
+    ensure_pool(a, q, std::max<int64_t>(2 * q.pool_words, 2 * (int64_t)q.pool_used), (int64_t)q.pool_used);
   if (he) {
     std::string why;
-    if (he & NFA_ERR_ARENA) why += " per-key partial-match arena exhausted (raise option heap_words);";
+    if (he & NFA_ERR_ARENA)
+      why += " one event allocated more partial-match state than its key's arena had free, or the overflow pool is "
+             "full (raise option heap_words or pool_words);";
     if (he & NFA_ERR_TIMERS) why += " timer queue full;";
     if (he & NFA_ERR_OUTPUT) why += " output buffer full (raise option output_records);";
     if (he & NFA_ERR_NPE) why += " NullPointerException/IllegalStateException path of the reference;";
@@ -1759,7 +1793,7 @@ using namespace sm;
 
 // snapshot encoding helpers (sm_app_snapshot / sm_app_restore)
 namespace {
-constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '3'};
+constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '4'};
 
 struct SnapWriter {
   std::vector<uint8_t> b;
@@ -2021,6 +2055,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       for (auto& q : a->queries)
         if (q->state_slots) throw std::runtime_error("heap_words must be set before the first flush");
       a->heap_half = (int32_t)std::max<int64_t>(256, value);
+    } else if (k == "pool_words") {
+      a->pool_init = std::max<int64_t>(1 << 16, value);
     } else if (k == "fast_general") {
       a->force_general_fast = value != 0;
     } else if (k == "fast_stack") {
@@ -2052,6 +2088,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
         if (q->keys.tslots) SM_HIP(hipMemsetAsync(q->keys.tslots, 0, (size_t)q->keys.cap * 4, a->stream));
         q->keys.nslots = 0;
         if (q->state_slots) SM_HIP(hipMemsetAsync(q->ks.p, 0, (size_t)q->state_slots * q->cq.hdr.ks_words * 8, a->stream));
+        if (q->pool_top_dev.p) SM_HIP(hipMemsetAsync(q->pool_top_dev.p, 0, 8, a->stream));
+        q->pool_used = 0;
         q->dev_n = 0;
         q->carry.reset();
       }
@@ -2384,6 +2422,14 @@ int sm_app_snapshot(sm_app* a, uint8_t* buf, size_t cap, size_t* len) {
         SM_HIP(hipMemcpy(heap.data(), q.heap.p, heap.size() * 8, hipMemcpyDeviceToHost));
         w.raw(heap.data(), heap.size() * 8);
       }
+      // the overflow pool's used prefix (promoted keys' heaps, addressed by pool offset)
+      const uint64_t pu = std::min<uint64_t>(q.pool_used, (uint64_t)q.pool_words);
+      w.put<uint64_t>(pu);
+      if (pu) {
+        std::vector<int64_t> pool(pu);
+        SM_HIP(hipMemcpy(pool.data(), q.pool.p, pu * 8, hipMemcpyDeviceToHost));
+        w.raw(pool.data(), pu * 8);
+      }
       w.put<uint8_t>((uint8_t)(q.nfa_used | (q.nfa_mode << 1) | (q.carry.active << 2)));
       w.put<int64_t>(q.carry.ts_last);
       w.put<int64_t>(q.carry.n);
@@ -2478,6 +2524,17 @@ int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
       } else if (q.state_slots) {
         SM_HIP(hipMemset(q.ks.p, 0, (size_t)q.state_slots * kw * 8));
       }
+      const uint64_t pu = r.get<uint64_t>();
+      if (pu) {
+        std::vector<int64_t> pool(pu);
+        r.raw(pool.data(), pu * 8);
+        ensure_pool(a, q, std::max<int64_t>(a->pool_init, 2 * (int64_t)pu), 0);
+        SM_HIP(hipMemcpy(q.pool.p, pool.data(), pu * 8, hipMemcpyHostToDevice));
+      } else {
+        ensure_pool(a, q, 0, 0);
+      }
+      q.pool_used = pu;
+      SM_HIP(hipMemcpy(q.pool_top_dev.p, &q.pool_used, 8, hipMemcpyHostToDevice));
       const uint8_t fl = r.get<uint8_t>();
       q.nfa_used = fl & 1;
       q.nfa_mode = (fl >> 1) & 1;

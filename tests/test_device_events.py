@@ -100,8 +100,8 @@ def test_config5_non_partitioned_and_no_playback():
         text = synth.app5(body, partitioned=partitioned, playback=False)
         exp = oracle_out(text, sid, cols, ts)
         # non-partitioned: one lane holds every pending partial of the window (the reference's lists are
-        # unbounded), so give its arena room
-        got, _ = product_out(text, sid, cols, ts, heap_words=1 << 20)
+        # unbounded): its heap grows into the overflow pool at the default arena size
+        got, _ = product_out(text, sid, cols, ts)
         assert len(exp["streams"].get("Out", [])) > 10
         assert got == exp
 
@@ -166,3 +166,44 @@ def test_config5_bench_shape_key_subsample(name):
     else:
         assert len(want) > 100 and n_full > 100_000
     assert mine == want
+
+
+def test_hot_key_overflow_pool_default_arena():
+    """One key holding 1e5 open partial matches next to 1e5 ordinary keys, at the default per-key arena (1024 words
+    per semispace): the hot key's heap moves into the device-wide overflow pool (Lane::promote) instead of failing,
+    and the outputs equal the oracle's. Reference: the pending lists are unbounded LinkedLists
+    (StreamPreStateProcessor.java:58-59)."""
+    rng = np.random.default_rng(11)
+    n_hot, n_keys = 100_000, 100_000
+    # ordinary keys 1..n_keys: one A and one B each, at random places; the hot key 0: n_hot A events (prices
+    # below 50), three B events that beat nothing in between, one that beats every partial at the end
+    sym = np.concatenate([np.zeros(n_hot, np.int32), np.arange(1, n_keys + 1, dtype=np.int32),
+                          np.arange(1, n_keys + 1, dtype=np.int32)])
+    sid = np.concatenate([np.zeros(n_hot, np.int32), np.zeros(n_keys, np.int32), np.ones(n_keys, np.int32)])
+    price = np.concatenate([rng.random(n_hot) * 50, rng.random(n_keys) * 100, rng.random(n_keys) * 100])
+    perm = rng.permutation(len(sym))
+    sym, sid, price = sym[perm], sid[perm], price[perm]
+    sym = list(sym)
+    sid = list(sid)
+    price = list(price)
+    for q, (s_, p_) in enumerate([(0, -1.0), (0, -1.0), (0, -1.0)]):
+        at = len(sym) * (q + 1) // 4
+        sym.insert(at, s_)
+        sid.insert(at, 1)
+        price.insert(at, p_)
+    sym.append(0)
+    sid.append(1)
+    price.append(99.0)
+    n = len(sym)
+    sym = np.array(sym, np.int32)
+    sid = np.array(sid, np.int32)
+    price = np.array(price, np.float64)
+    cols = [sym, price, np.zeros(n, np.int64), np.arange(n, dtype=np.int64)]
+    ts = np.arange(n, dtype=np.int64)
+    text = synth.app5("every e1=A -> e2=B[price > e1.price]", playback=False,
+                      select="select e1.timestamp as a, e2.timestamp as b insert into Out;")
+    exp = oracle_out(text, sid, cols, ts)
+    got, _ = product_out(text, sid, cols, ts)
+    out = exp["streams"].get("Out", [])
+    assert sum(1 for r in out if r[1][1] == n - 1) >= n_hot * 0.9
+    assert got == exp

@@ -97,14 +97,35 @@ def test_projection_unpartitioned():
     assert got == exp
 
 
-def test_projection_refused_for_filter_queries():
+def test_projection_of_filter_queries():
+    """A filter query's device batch: each kept row's select list (FilterProcessor → QuerySelector on one event)."""
     import torch
-    from siddhi_amd.testing import EngineError, ProductApp
-    app = ProductApp(SCHEMA.format(kt="int") + "@info(name='q') from StockStream[price > 50] select price insert into O;")
-    cols, ts = stock(100, 5, 1)
+    from siddhi_amd.testing import ProductApp
+    t = SCHEMA.format(kt="int") + ("@info(name='q') from StockStream[price > 50] select symbol, price * 2 as p2, "
+                                   "timestamp insert into O;")
+    cols, ts = stock(5000, 5, 1)
+    app = ProductApp(t)
     dev = torch.device("cuda", 0)
     app.process_device_batch("StockStream", torch.from_numpy(ts.astype(np.int64)).to(dev),
                              [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in cols])
+    vals, nulls, ots = app.device_project("q")
+    app.close()
+    sel = np.nonzero(cols[1] > 50)[0]
+    v = vals.cpu().numpy()
+    assert v.shape[0] == len(sel) and not nulls.any()
+    np.testing.assert_array_equal(v[:, 0], cols[0][sel])
+    np.testing.assert_array_equal(v[:, 1].view(np.float64), cols[1][sel] * 2)
+    np.testing.assert_array_equal(v[:, 2], cols[3][sel])
+    np.testing.assert_array_equal(ots.cpu().numpy(), ts[sel])
+
+
+def test_projection_refused_after_host_events():
+    """Outputs of host-API events reach the callbacks as Events; there is no device batch to project."""
+    from siddhi_amd.testing import EngineError, ProductApp
+    app = ProductApp(SCHEMA.format(kt="int") + "@info(name='q') from StockStream[price > 50] select price insert into O;")
+    app.start()
+    app.send("StockStream", 1, [1, 60.0, 1, 0], ["INT", "DOUBLE", "LONG", "LONG"])
+    app.flush()
     with pytest.raises(EngineError):
         app.device_project("q")
     app.close()
