@@ -109,48 +109,6 @@ def gen_stream_idx(lo, hi, device, seed):
     return (((h3 >> 32) & 0xFFFFFFFF) % 5).to(torch.int32)
 
 
-def clock_ticks(ts, lo, world):
-    """Multi-GPU config 5: the playback clock is global (every event advances it, StreamJunction.sendData
-    :232-237) but a rank only receives its keys' events. Each rank finds the clock-advance points of its own
-    contiguous slice (first event of each new event time), all ranks all-gather them, and every rank replays
-    them as heartbeats so that its timers fire at exactly the reference's clock values."""
-    import torch
-    import torch.distributed as dist
-    first = torch.ones_like(ts, dtype=torch.bool)
-    first[1:] = ts[1:] > ts[:-1]
-    pos = torch.nonzero(first).flatten()
-    mine = torch.stack([pos + lo, ts[pos]], 1)  # (global ordinal, clock)
-    cnt = torch.tensor([mine.shape[0]], dtype=torch.int64, device=ts.device)
-    cnts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt)
-    mx = int(max(c.item() for c in cnts))
-    pad = torch.zeros((mx, 2), dtype=torch.int64, device=ts.device)
-    pad[:mine.shape[0]] = mine
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad)
-    return torch.cat([p[:int(c.item())] for p, c in zip(parts, cnts)])
-
-
-def merge_ticks(sid, ts, cols, ords, ticks):
-    """Insert heartbeat records (stream -1) before the received events, ordered by global ordinal; a tick at
-    the ordinal of an event this rank already holds is dropped (that event advances the clock itself)."""
-    import torch
-    have = torch.zeros(0, dtype=torch.bool, device=ts.device)
-    tpos = ticks[:, 0]
-    idx = torch.searchsorted(ords, tpos)
-    hit = (idx < ords.numel()) & (ords[idx.clamp(max=max(ords.numel() - 1, 0))] == tpos) if ords.numel() else have
-    keep = ~hit if ords.numel() else torch.ones_like(tpos, dtype=torch.bool)
-    tpos, tclk = tpos[keep], ticks[keep, 1]
-    key = torch.cat([ords * 2 + 1, tpos * 2])  # heartbeat first at equal ordinal (it is replayed before it)
-    order = torch.argsort(key)
-    n_t = tpos.numel()
-    sid2 = torch.cat([sid, torch.full((n_t,), -1, dtype=torch.int32, device=ts.device)])[order]
-    ts2 = torch.cat([ts, tclk])[order]
-    cols2 = [torch.cat([c, torch.zeros(n_t, dtype=c.dtype, device=c.device)])[order] for c in cols]
-    ords2 = torch.cat([ords, torch.full((n_t,), -1, dtype=torch.int64, device=ts.device)])[order]
-    return sid2, ts2, cols2, ords2
-
-
 def gen_stock_numpy(lo, hi, K, ts_div, seed):
     import numpy as np
     with np.errstate(over="ignore"):
@@ -374,7 +332,8 @@ def main():
     import torch
     import torch.distributed as dist
     from siddhi_amd.testing import ProductApp
-    from siddhi_amd.shard import concat_ordered, exchange_with_ordinals, return_matches, slice_starts
+    from siddhi_amd.shard import (clock_ticks, concat_ordered, exchange_with_ordinals, merge_heartbeats,
+                                  return_matches, slice_starts)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -397,7 +356,6 @@ def main():
         volume = price
     ordinals = torch.arange(lo, hi, dtype=torch.int64, device=dev) if args.config in (4, 5) else None
     sidx = gen_stream_idx(lo, hi, dev, seed) if args.config == 5 else None
-    ticks = clock_ticks(ts, lo, world) if args.config == 5 and world > 1 else None
     # multi-GPU constants of the exchange, made once: every slice's first ordinal, the in-slice offsets shipped in
     # the packed records, and the device buffer the per-rank match tuples are copied into for the return exchange
     starts = slice_starts(lo, world, dev) if world > 1 and cfg["shards"] else None
@@ -421,9 +379,12 @@ def main():
             # a fresh runtime of the app per step (state dropped, device allocations kept), then the batch
             app.set_option("reset", 1)
             if world > 1:
+                # the global clock-advance points (one all-gather), the key exchange, then the heartbeats merged
+                # into the received events on the device (shard.py, sm_merge_heartbeats): all inside the step
+                ticks = clock_ticks(ts, lo, world)
                 (s_sym, s_price, s_ts, s_sid), s_ord, _ = exchange_with_ordinals(
                     symbol, [symbol, price, ts, sidx], world, lo, starts=starts, offsets=offsets)
-                s_sid, s_ts, (s_sym, s_price), s_ord = merge_ticks(s_sid, s_ts, [s_sym, s_price], s_ord, ticks)
+                s_sid, s_ts, (s_sym, s_price), s_ord = merge_heartbeats(s_sid, s_ts, [s_sym, s_price], s_ord, ticks)
             else:
                 s_sym, s_price, s_ts, s_ord, s_sid = symbol, price, ts, ordinals, sidx
             n_local[0] = s_ts.numel()

@@ -16,6 +16,8 @@
  *   sm_app_snapshot / sm_app_restore  SiddhiAppRuntime.snapshot() / restore(byte[])  :548 / :560
  *   sm_partition_by_owner           multi-GPU form of PartitionStreamReceiver.receive (partition/
  *                                   PartitionStreamReceiver.java:156): route each event to its key's owner rank
+ *   sm_merge_heartbeats             multi-GPU playback: the global clock advances (StreamJunction.sendData :232)
+ *                                   replayed as heartbeats among a rank's received events
  *   sm_order_matches                multi-GPU merge of the per-rank outputs back into the single output order a
  *                                   query callback sees (QueryCallback.receive, query/output/callback/
  *                                   QueryCallback.java:51): no Java counterpart, one JVM has one output queue
@@ -173,6 +175,16 @@ int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t 
  * global output order for that slice. Concatenating the ranks' outputs in rank order gives the single-process
  * output order. */
 int sm_order_matches(const uint64_t* d_pairs, size_t n, int64_t lo, int64_t hi, uint64_t* d_out, void* hip_stream);
+/* Multi-GPU playback (@app:playback partitioned apps, siddhi_amd/shard.py merge_heartbeats): a rank's received
+ * events (n; global ordinals d_ord ascending; stream index, event time and ncols columns of 4 or 8 bytes) merged
+ * in ordinal order with the global clock-advance points (m; ordinals d_tick_ord ascending, clock d_tick_ts), a point
+ * at an ordinal this rank holds dropped: the playback clock is global (StreamJunction.sendData :232-237) while a rank
+ * holds only its keys' events, so it replays the other ranks' clock advances as heartbeats (stream index -1,
+ * ordinal -1, zero attributes). Outputs hold n + m entries; *n_out = merged length. */
+int sm_merge_heartbeats(size_t n, const int64_t* d_ord, const int32_t* d_sid, const int64_t* d_ts, int ncols,
+                        const int32_t* widths, const void* const* d_src, size_t m, const int64_t* d_tick_ord,
+                        const int64_t* d_tick_ts, int32_t* d_sid_out, int64_t* d_ts_out, int64_t* d_ord_out,
+                        void* const* d_dst, size_t* n_out, void* hip_stream);
 /* Match tuples of the last device batch for a query: n pairs (e1, e2) of ordinals relative to the batch's
  * ordinal_base, uint32[2*n] in device memory, in reference output order (e2 ordinal, then e1 ordinal). */
 int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** d_pairs, size_t* n);

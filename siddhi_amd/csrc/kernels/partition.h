@@ -38,4 +38,23 @@ void order_matches(const uint64_t* pairs, int64_t n, int64_t lo, int64_t hi, uin
 void partition_by_owner(const void* keys, int key_width, int64_t n, uint32_t world, const PartCols& cols,
                         uint64_t* counts_host, Scratch& sc, hipStream_t s);
 
+// Output of merge_heartbeats: the merged sequence's stream index (-1 = heartbeat), event time, global ordinal (-1 for
+// a heartbeat) and every column (src[c] of the events -> dst[c]; a heartbeat's attribute words are zero).
+struct MergeOut {
+  int32_t ncols;
+  int32_t width[kMaxPartCols];  // 4 or 8
+  const void* src[kMaxPartCols];
+  void* dst[kMaxPartCols];
+  int32_t* sid;
+  int64_t* ts;
+  int64_t* ord;
+};
+
+// Multi-GPU playback (@app:playback partitioned apps): a rank's received events (n, global ordinals `ord`
+// ascending) merged with the global clock-advance points (m, ordinals `tord` ascending, clock `tts`) in ordinal
+// order; a point at an ordinal this rank holds is dropped (that event advances the clock itself,
+// StreamJunction.sendData :232-237). Returns the merged length (n + points kept); outputs need n + m entries.
+int64_t merge_heartbeats(const int64_t* ord, const int32_t* sid, const int64_t* ts, int64_t n, const int64_t* tord,
+                         const int64_t* tts, int64_t m, const MergeOut& o, Scratch& sc, hipStream_t s);
+
 }  // namespace sm

@@ -123,7 +123,87 @@ __global__ void e2_place_kernel(const uint64_t* __restrict__ p, int64_t n, int64
   out[off[(int64_t)j - lo] + r] = v;
 }
 
+// Playback heartbeats of a rank (multi-GPU config 5): the received events (global ordinals ascending) merged with
+// the global clock-advance points (ascending ordinals), a point at an ordinal this rank holds dropped (that event
+// advances the clock itself). Merge path by binary search: a kept point's place = kept points before it + events
+// with smaller ordinals; an event's place = its index + kept points with smaller ordinals.
+__device__ __forceinline__ int64_t lower_bound_i64(const int64_t* __restrict__ a, int64_t n, int64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void tick_keep_kernel(const int64_t* __restrict__ ord, int64_t n, const int64_t* __restrict__ tord,
+                                 int64_t m, uint32_t* __restrict__ keep) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const int64_t lb = lower_bound_i64(ord, n, tord[j]);
+  keep[j] = (lb < n && ord[lb] == tord[j]) ? 0u : 1u;
+}
+
+__global__ void tick_place_kernel(const int64_t* __restrict__ ord, int64_t n, const int64_t* __restrict__ tord,
+                                  const int64_t* __restrict__ tts, int64_t m, const uint32_t* __restrict__ kpos,
+                                  MergeOut o) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m || kpos[j + 1] == kpos[j]) return;  // dropped
+  const int64_t p = (int64_t)kpos[j] + lower_bound_i64(ord, n, tord[j]);
+  o.sid[p] = -1;
+  o.ts[p] = tts[j];
+  o.ord[p] = -1;
+  for (int c = 0; c < o.ncols; ++c) {
+    char* d = (char*)o.dst[c];
+    if (o.width[c] == 4) ((uint32_t*)d)[p] = 0u;
+    else ((uint64_t*)d)[p] = 0ull;
+  }
+}
+
+__global__ void event_place_kernel(const int64_t* __restrict__ ord, const int32_t* __restrict__ sid,
+                                   const int64_t* __restrict__ ts, int64_t n, const int64_t* __restrict__ tord,
+                                   int64_t m, const uint32_t* __restrict__ kpos, MergeOut o) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = i + (int64_t)kpos[lower_bound_i64(tord, m, ord[i])];
+  o.sid[p] = sid[i];
+  o.ts[p] = ts[i];
+  o.ord[p] = ord[i];
+  for (int c = 0; c < o.ncols; ++c) {
+    const char* sc = (const char*)o.src[c];
+    char* d = (char*)o.dst[c];
+    if (o.width[c] == 4) ((uint32_t*)d)[p] = ((const uint32_t*)sc)[i];
+    else ((uint64_t*)d)[p] = ((const uint64_t*)sc)[i];
+  }
+}
+
 }  // namespace
+
+int64_t merge_heartbeats(const int64_t* ord, const int32_t* sid, const int64_t* ts, int64_t n, const int64_t* tord,
+                         const int64_t* tts, int64_t m, const MergeOut& o, Scratch& sc, hipStream_t s) {
+  for (int c = 0; c < o.ncols; ++c)
+    if (o.width[c] != 4 && o.width[c] != 8) throw std::invalid_argument("heartbeat merge: columns of 4 or 8 bytes");
+  if (o.ncols > kMaxPartCols) throw std::invalid_argument("too many columns");
+  const size_t mark = sc.used;
+  uint32_t* kpos = (uint32_t*)sc.take((size_t)(m + 1) * 4);
+  uint32_t kept = 0;
+  if (m > 0) {
+    hipLaunchKernelGGL(tick_keep_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, ord, n, tord, m, kpos);
+    exclusive_scan_u32(kpos, (size_t)m, sc, s, kpos + m);
+    SM_HIP(hipMemcpyAsync(&kept, kpos + m, 4, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(tick_place_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, ord, n, tord, tts, m,
+                       (const uint32_t*)kpos, o);
+  } else {
+    SM_HIP(hipMemsetAsync(kpos, 0, 4, s));
+  }
+  if (n > 0)
+    hipLaunchKernelGGL(event_place_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ord, sid, ts, n, tord,
+                       m, (const uint32_t*)kpos, o);
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+  return n + (int64_t)kept;
+}
 
 void order_matches(const uint64_t* pairs, int64_t n, int64_t lo, int64_t hi, uint64_t* out, Scratch& sc,
                    hipStream_t s) {

@@ -2623,6 +2623,29 @@ int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t 
   });
 }
 
+int sm_merge_heartbeats(size_t n, const int64_t* d_ord, const int32_t* d_sid, const int64_t* d_ts, int ncols,
+                        const int32_t* widths, const void* const* d_src, size_t m, const int64_t* d_tick_ord,
+                        const int64_t* d_tick_ts, int32_t* d_sid_out, int64_t* d_ts_out, int64_t* d_ord_out,
+                        void* const* d_dst, size_t* n_out, void* hip_stream) {
+  return guarded([&] {
+    if (ncols < 0 || ncols > sm::kMaxPartCols) throw std::invalid_argument("ncols out of range");
+    sm::MergeOut o{};
+    o.ncols = ncols;
+    for (int c = 0; c < ncols; ++c) {
+      o.width[c] = widths[c];
+      o.src[c] = d_src[c];
+      o.dst[c] = d_dst[c];
+    }
+    o.sid = d_sid_out;
+    o.ts = d_ts_out;
+    o.ord = d_ord_out;
+    HelperScratch& h = helper_scratch((size_t)m * 4 + (16 << 20));
+    HelperLock lk{h};
+    *n_out = (size_t)sm::merge_heartbeats(d_ord, d_sid, d_ts, (int64_t)n, d_tick_ord, d_tick_ts, (int64_t)m, o, h.sc,
+                                          (hipStream_t)hip_stream);
+  });
+}
+
 int sm_order_matches(const uint64_t* d_pairs, size_t n, int64_t lo, int64_t hi, uint64_t* d_out, void* hip_stream) {
   return guarded([&] {
     if (n == 0) return;

@@ -256,6 +256,87 @@ def concat_ordered(rows: torch.Tensor, world: int, group=None) -> torch.Tensor:
     return torch.cat([p[:c] for p, c in zip(parts, cs)])
 
 
+def clock_ticks(ts: torch.Tensor, lo: int, world: int, group=None) -> torch.Tensor:
+    """Multi-GPU playback (@app:playback partitioned apps, config 5): the clock is global (every event advances it,
+    StreamJunction.sendData :232-237) but a rank receives only its keys' events. Each rank finds the clock-advance
+    points of its own contiguous ingest slice (the first event of each new event time: global ordinal lo + i), and
+    one all-gather (counts, then the padded points) gives every rank all of them, in global ordinal order (the
+    slices are contiguous and ranked). Returns an int64 (m, 2) tensor of (global ordinal, clock)."""
+    first = torch.ones_like(ts, dtype=torch.bool)
+    if ts.numel() > 1:
+        first[1:] = ts[1:] > ts[:-1]
+    pos = torch.nonzero(first).flatten()
+    mine = torch.stack([pos + lo, ts[pos]], 1)
+    if world == 1:
+        return mine
+    cnt = torch.tensor([mine.shape[0]], dtype=torch.int64, device=ts.device)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    cs = [int(c.item()) for c in cnts]
+    pad = torch.zeros((max(cs), 2), dtype=torch.int64, device=ts.device)
+    pad[:mine.shape[0]] = mine
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, cs)])
+
+
+def merge_heartbeats(sid: torch.Tensor, ts: torch.Tensor, columns, ords: torch.Tensor, ticks: torch.Tensor):
+    """A rank's received events (global ordinals `ords` ascending) merged with the global clock-advance points
+    (`ticks` from clock_ticks) in ordinal order, as heartbeats (stream index -1, ordinal -1, zero attributes) for
+    sm_app_process_device_events; a point at an ordinal this rank holds is dropped (that event advances the clock
+    itself). GPU tensors: the HIP merge of the native library (sm_merge_heartbeats: binary-search merge path, no
+    sort); host tensors (gloo tests): the same merge with torch.searchsorted. Returns (sid, ts, columns, ords)."""
+    tord = ticks[:, 0].contiguous()
+    tts = ticks[:, 1].contiguous()
+    n, m = ords.numel(), tord.numel()
+    for c in columns:
+        if c.element_size() not in (4, 8) or c.numel() != n:
+            raise ValueError("merge_heartbeats: columns of 4- or 8-byte elements aligned with the events")
+    if ords.is_cuda:
+        import ctypes
+        from siddhi_amd import _lib
+        cap = n + m
+        o_sid = torch.empty(cap, dtype=torch.int32, device=ords.device)
+        o_ts = torch.empty(cap, dtype=torch.int64, device=ords.device)
+        o_ord = torch.empty(cap, dtype=torch.int64, device=ords.device)
+        cols = [c.contiguous() for c in columns]
+        outs = [torch.empty(cap, dtype=c.dtype, device=c.device) for c in cols]
+        k = len(cols)
+        widths = (ctypes.c_int32 * max(k, 1))(*[c.element_size() for c in cols])
+        src = (ctypes.c_void_p * max(k, 1))(*[c.data_ptr() for c in cols])
+        dst = (ctypes.c_void_p * max(k, 1))(*[o.data_ptr() for o in outs])
+        n_out = ctypes.c_size_t()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(ords.device).cuda_stream)
+        rc = _lib.lib().sm_merge_heartbeats(n, ords.data_ptr(), sid.contiguous().data_ptr(), ts.contiguous().data_ptr(),
+                                            k, widths, src, m, tord.data_ptr(), tts.data_ptr(), o_sid.data_ptr(),
+                                            o_ts.data_ptr(), o_ord.data_ptr(), dst, ctypes.byref(n_out), stream)
+        if rc != _lib.SM_OK:
+            raise RuntimeError(_lib.lib().sm_last_error().decode(errors="replace"))
+        L = n_out.value
+        return o_sid[:L], o_ts[:L], [o[:L] for o in outs], o_ord[:L]
+    lb = torch.searchsorted(ords, tord)
+    held = (lb < n) & (ords[lb.clamp(max=max(n - 1, 0))] == tord) if n else torch.zeros(m, dtype=torch.bool)
+    keep = ~held
+    kt, kts, klb = tord[keep], tts[keep], lb[keep]
+    K = kt.numel()
+    tick_at = torch.arange(K, dtype=torch.int64) + klb
+    ev_at = torch.arange(n, dtype=torch.int64) + torch.searchsorted(kt, ords)
+    L = n + K
+    o_sid = torch.full((L,), -1, dtype=torch.int32)
+    o_ts = torch.empty(L, dtype=torch.int64)
+    o_ord = torch.full((L,), -1, dtype=torch.int64)
+    o_sid[ev_at] = sid.to(torch.int32)
+    o_ts[ev_at] = ts
+    o_ts[tick_at] = kts
+    o_ord[ev_at] = ords
+    outs = []
+    for c in columns:
+        o = torch.zeros(L, dtype=c.dtype)
+        o[ev_at] = c
+        outs.append(o)
+    return o_sid, o_ts, outs, o_ord
+
+
 def merge_matches(parts):
     """Merge per-rank match tuples (each an (n, 2) int array of global (e1, e2) ordinals in reference order for
     that rank's keys) into the reference's global order: by e2 ordinal; ties (same e2) come from one rank and

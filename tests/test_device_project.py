@@ -106,8 +106,9 @@ def test_projection_of_filter_queries():
     cols, ts = stock(5000, 5, 1)
     app = ProductApp(t)
     dev = torch.device("cuda", 0)
-    app.process_device_batch("StockStream", torch.from_numpy(ts.astype(np.int64)).to(dev),
-                             [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in cols])
+    tts = torch.from_numpy(ts.astype(np.int64)).to(dev)
+    tcols = [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in cols]  # read again by the projection
+    app.process_device_batch("StockStream", tts, tcols)
     vals, nulls, ots = app.device_project("q")
     app.close()
     sel = np.nonzero(cols[1] > 50)[0]

@@ -61,3 +61,26 @@ def test_order_matches_kernel_equals_stable_sort(n_src, per):
     exp = pairs[torch.argsort(pairs >> 32, stable=True)]
     got = order_matches(pairs.to(torch.device("cuda", 0)), lo, hi)
     assert torch.equal(got.cpu(), exp)
+
+
+@pytest.mark.parametrize("n,m,overlap", [(0, 5, 0.0), (7, 0, 0.0), (1000, 300, 0.3), (200_000, 50_000, 0.5)])
+def test_merge_heartbeats_hip_equals_torch(n, m, overlap):
+    """sm_merge_heartbeats (HIP merge path) = the torch form of shard.merge_heartbeats: a rank's events (ascending
+    global ordinals) with the global clock-advance points, a point at an ordinal the rank holds dropped."""
+    from siddhi_amd.shard import merge_heartbeats
+    g = torch.Generator().manual_seed(n + m)
+    ords = torch.sort(torch.randperm(4 * (n + m) + 8, generator=g)[:n].to(torch.int64)).values
+    held = ords[torch.randperm(n, generator=g)[:int(overlap * min(n, m))]] if n else torch.zeros(0, dtype=torch.int64)
+    others = torch.randperm(4 * (n + m) + 8, generator=g)[:m - held.numel()].to(torch.int64)
+    tord = torch.unique(torch.cat([held, others]))
+    ticks = torch.stack([tord, tord // 3 + 7], 1)
+    sid = torch.randint(0, 5, (n,), generator=g, dtype=torch.int32)
+    ts = ords // 3
+    cols = [torch.randint(-100, 100, (n,), generator=g, dtype=torch.int32), torch.rand(n, generator=g,
+                                                                                      dtype=torch.float64)]
+    want = merge_heartbeats(sid, ts, cols, ords, ticks)
+    dev = torch.device("cuda", 0)
+    got = merge_heartbeats(sid.to(dev), ts.to(dev), [c.to(dev) for c in cols], ords.to(dev), ticks.to(dev))
+    for a, b in zip([got[0], got[1], got[3]] + got[2], [want[0], want[1], want[3]] + want[2]):
+        assert torch.equal(a.cpu(), b)
+    assert got[0].numel() == n + tord.numel() - torch.isin(tord, ords).sum().item()

@@ -207,8 +207,8 @@ def test_merge_keeps_same_trigger_order():
     np.testing.assert_array_equal(merge_matches([a, b]), [[3, 4], [1, 5], [0, 5], [4, 7], [2, 9]])
 
 
-# ---- config 5 (five streams, playback timers): key exchange + global clock-advance heartbeats (bench.py
-# clock_ticks / merge_ticks) must reproduce every output of the single-process run, with the same timestamps,
+# ---- config 5 (five streams, playback timers): key exchange + global clock-advance heartbeats (shard.py
+# clock_ticks / merge_heartbeats) must reproduce every output of the single-process run, with the same timestamps,
 # and each rank's outputs in the global relative order.
 N5, K5 = 20000, 400
 BODIES5 = ["every e1=A -> e2=B[price>e1.price]<2:5> -> (e3=C or e4=D) -> not E for 1 sec",
@@ -237,8 +237,7 @@ def replay5(text, sid, ts, cols):
 
 
 def _worker5(rank, world, port, outfile, body):
-    from bench import clock_ticks, merge_ticks
-    from siddhi_amd.shard import exchange_by_key
+    from siddhi_amd.shard import clock_ticks, exchange_by_key, merge_heartbeats
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -251,7 +250,7 @@ def _worker5(rank, world, port, outfile, body):
         ords = torch.arange(lo, hi, dtype=torch.int64)
         ticks = clock_ticks(tts, lo, world)
         (r_sym, r_price, r_vol, r_tsa, r_ts, r_ord, r_sid), _ = exchange_by_key(t[0], t + [tts, ords, tsid], world)
-        m_sid, m_ts, m_cols, m_ord = merge_ticks(r_sid, r_ts, [r_sym, r_price, r_vol, r_tsa], r_ord, ticks)
+        m_sid, m_ts, m_cols, m_ord = merge_heartbeats(r_sid, r_ts, [r_sym, r_price, r_vol, r_tsa], r_ord, ticks)
         assert (np.diff(m_ts.numpy()) >= 0).all()
         local = replay5(synth.app5(body), m_sid.numpy(), m_ts.numpy(), [c.numpy() for c in m_cols])
         parts = [None] * world
