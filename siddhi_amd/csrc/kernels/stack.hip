@@ -36,11 +36,15 @@ namespace sm {
 
 namespace {
 
-constexpr int kSB = 512;       // threads per bucket workgroup: thread t owns in-bucket keys t and t + kSB (a 256-VGPR
-constexpr int kSW = kSB / 64;  // budget keeps both stacks and the slice machinery in registers)
 constexpr int kKeys = 1024;    // in-bucket keys
+#ifndef SM_STACK_KPT
+#define SM_STACK_KPT 2          // A/B build flag: in-bucket keys per thread (2: 512 threads and a 256-VGPR budget for
+#endif                          // both stacks; 1: 1024 threads, 4 waves per SIMD)
+constexpr int kKPT = SM_STACK_KPT;
+constexpr int kSB = kKeys / kKPT;  // threads per bucket workgroup: thread t owns in-bucket keys t (and t + kSB)
+constexpr int kSW = kSB / 64;
 #ifndef SM_STACK_KSI
-#define SM_STACK_KSI 9          // A/B build flag (config 4 stack kernel: 8 -> 33.2 ms, 9 -> 32.2 ms)
+#define SM_STACK_KSI (SM_STACK_KPT == 2 ? 9 : 4)  // A/B build flag (config 4 stack kernel: 8 -> 33.2 ms, 9 -> 32.2 ms)
 #endif
 constexpr int kSI = SM_STACK_KSI;  // records per thread per slice
 constexpr int kS = kSB * kSI;      // slice: 4608 records
@@ -57,10 +61,15 @@ constexpr int kOT = 1 << kTB;
 constexpr int kOCap = 12288;   // matches of a tile staged in LDS before one coalesced write
 constexpr int kGT = 16;        // consecutive tiles per order workgroup
 
-static_assert(kBins == kKeys && kKeys == 2 * kSB && kBins == kOB, "two in-bucket keys per thread, one bucket per "
-              "order thread");
+static_assert(kBins == kKeys && kKeys == kKPT * kSB && kBins == kOB && (kKPT == 1 || kKPT == 2),
+              "one or two in-bucket keys per thread, one bucket per order thread");
+static_assert(kSW * kKeys * 2 <= kLog * 8, "the per-wave key counts of the ranking fit the match log area");
 
 enum : uint32_t { SE_OVERFLOW = 1, SE_LOG = 2, SE_NAN = 4, SE_CAND = 8, SE_ORD = 16 };
+#ifndef SM_STACK_STAMPS_BUILD
+#define SM_STACK_STAMPS_BUILD 0  // build flag: phase clock + counters of the stack kernel (env SM_STACK_STAMPS=1 reads them)
+#endif
+constexpr bool kStamps = SM_STACK_STAMPS_BUILD != 0;
 
 struct StackArgs {
   const uint4* rec;
@@ -144,11 +153,19 @@ struct ExactSrc {
 };
 
 // equal inexact codes (or NaN): the exact values decide. Out of line: rare, and its binary searches must not
-// hold registers in the event loop.
+// hold registers in the event loop; the source is passed by value (a reference would put it in scratch).
 template <int OP, bool FP>
-__device__ __noinline__ bool c2_exact(const ExactSrc& ex, uint32_t oi, uint32_t oj) {
+__device__ __noinline__ bool c2_exact_v(bool exact_codes, int vtype, int vattr, int cwidth, const void* vcol,
+                                        const int64_t* ord, int64_t obase, int64_t n, const int64_t* crow, int32_t o0,
+                                        uint32_t cs, uint32_t ce, uint32_t oi, uint32_t oj) {
+  const ExactSrc ex{exact_codes, vtype, vattr, cwidth, vcol, ord, obase, n, crow, o0, cs, ce};
   if constexpr (FP) return cmp_fixed<OP>(ex.fval(oj), ex.fval(oi));
   else return cmp_fixed<OP>(ex.ival(oj), ex.ival(oi));
+}
+template <int OP, bool FP>
+__device__ __forceinline__ bool c2_exact(const ExactSrc& ex, uint32_t oi, uint32_t oj) {
+  return c2_exact_v<OP, FP>(ex.exact_codes, ex.vtype, ex.vattr, ex.cwidth, ex.vcol, ex.ord, ex.obase, ex.n, ex.crow,
+                            ex.o0, ex.cs, ex.ce, oi, oj);
 }
 
 // c2 = `e2.x OP e1.x` for partial i (code ci, ordinal oi) and event j
@@ -261,10 +278,10 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
   const int32_t within32 = (int32_t)a.within;
   // phase clock (diagnostic): 0 slice setup, 1 ranking, 2 placement, 3 stacks, 4 scan + tiles, 5 match writes,
   // 6 bucket tail + carry out
-  unsigned long long st_acc[7] = {0, 0, 0, 0, 0, 0, 0}, st_last = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  unsigned long long st_acc[7] = {0, 0, 0, 0, 0, 0, 0}, st_last = kStamps && a.stamps ? __builtin_amdgcn_s_memtime() : 0;
 #define SM_PHASE(i)                                               \
   do {                                                            \
-    if (a.stamps) {                                               \
+    if (kStamps && a.stamps) {                                    \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
       st_acc[i] += t_ - st_last;                                  \
       st_last = t_;                                               \
@@ -272,10 +289,13 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
   } while (0)
   const uint64_t lt = lanemask_lt();
   // the two keys of this thread: h = tid (A) and h = tid + kSB (B)
-  const bool hasA = tid < a.H, hasB = tid + kSB < a.H;
+  const bool hasA = tid < a.H, hasB = kKPT == 2 && tid + kSB < a.H;
   uint4* spA = a.spill + ((int64_t)blockIdx.x * kKeys + tid) * kQ;
   uint4* spB = spA + (int64_t)kSB * kQ;
-  const uint32_t kSlots = kLog / (uint32_t)(a.H < kSB ? a.H : kSB);
+  // match log: slot k of thread t at area[k * kLStride + t] (slot-major: the lanes of a wave write consecutive words;
+  // thread-major t * kSlots + k put every lane of a wave on the same two banks)
+  const uint32_t kLStride = (uint32_t)(a.H < kSB ? a.H : kSB);
+  const uint32_t kSlots = kLog / kLStride;
   unsigned long long cn[2] = {0, 0};
 
   for (int d = blockIdx.x; d < kBins; d += gridDim.x) {
@@ -347,11 +367,11 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
       }
       lds_barrier();
       {
-        // keys 2 * tid and 2 * tid + 1: exclusive over waves in place, totals, block scan over keys
-        uint32_t r2[2];
+        // keys kKPT * tid + u: exclusive over waves in place, totals, block scan over keys
+        uint32_t r2[kKPT];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int h = 2 * tid + u;
+        for (int u = 0; u < kKPT; ++u) {
+          const int h = kKPT * tid + u;
           uint32_t r = 0;
           for (int qq = 0; qq < kSW; ++qq) {
             const uint32_t c = wcnt[qq][h];
@@ -362,9 +382,13 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
           r2[u] = r;
         }
         uint32_t tot;
-        const uint32_t st0 = block_excl<kSB>(r2[0] + r2[1], lw, &tot);
-        hst[2 * tid] = (uint16_t)st0;
-        hst[2 * tid + 1] = (uint16_t)(st0 + r2[0]);
+        if constexpr (kKPT == 2) {
+          const uint32_t st0 = block_excl<kSB>(r2[0] + r2[1], lw, &tot);
+          hst[2 * tid] = (uint16_t)st0;
+          hst[2 * tid + 1] = (uint16_t)(st0 + r2[0]);
+        } else {
+          hst[tid] = (uint16_t)block_excl<kSB>(r2[0], lw, &tot);
+        }
       }
       lds_barrier();
       SM_PHASE(1);
@@ -388,7 +412,7 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
       // register entries with spilled ones behind them goes on entry by entry (rare).
       auto log_put = [&](uint32_t& nlog, uint64_t ent) {
         if (nlog < kSlots) {
-          area[tid * kSlots + nlog] = ent;
+          area[nlog * kLStride + tid] = ent;
         } else {
           const uint32_t o = atomicAdd(&s_ovf, 1u);
           if (o < kOvf) ovf[o] = ent;
@@ -460,7 +484,7 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
         }
         jcnt[e] = (uint16_t)npop;
         if (r.x >> 31) st_push(s, sp, oj, cj, jt, jt, a.within, a.err);
-        if (a.counts) {
+        if (kStamps && a.counts) {
           cn[0] += 1;
           cn[1] += npop;
         }
@@ -469,8 +493,8 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
       if (a.dbg == 1)
         for (int k = tid; k < sn; k += kSB) jcnt[k] = 0;
       if (a.dbg != 1) {
-        const int cA = hasA ? hcn[tid] : 0, cB = hasB ? hcn[tid + kSB] : 0;
-        const int sA0 = hst[tid], sB0 = hst[tid + kSB];
+        const int cA = hasA ? hcn[tid] : 0, cB = hasB ? hcn[(tid + kSB) & (kKeys - 1)] : 0;
+        const int sA0 = hst[tid], sB0 = hst[(tid + kSB) & (kKeys - 1)];
         const int cmax = cA > cB ? cA : cB;
         if (cA) {
           tlA = (int32_t)rec[sA0 + cA - 1].w;
@@ -528,7 +552,7 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
         const uint32_t pos = mrun + joff[e] + (jcnt[e] - 1u - pop);
         a.stage[sb + pos] = ((uint64_t)ordt[e] << 32) | io;
       };
-      for (uint32_t k = 0; k < nlog && k < kSlots; ++k) emit(area[tid * kSlots + k]);
+      for (uint32_t k = 0; k < nlog && k < kSlots; ++k) emit(area[k * kLStride + tid]);
       for (uint32_t k = tid; k < no; k += kSB) emit(ovf[k]);
       mrun += stot;
       SM_PHASE(5);
@@ -599,9 +623,9 @@ __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
     __syncthreads();  // LDS of this bucket is free for the next one
     SM_PHASE(6);
   }
-  if (a.stamps && lane == 0)
+  if (kStamps && a.stamps && lane == 0)
     for (int i = 0; i < 7; ++i) atomicAdd(&a.stamps[i], st_acc[i]);
-  if (a.counts) {
+  if (kStamps && a.counts) {
     atomicAdd(&a.counts[0], cn[0]);
     atomicAdd(&a.counts[1], cn[1]);
   }
@@ -919,14 +943,11 @@ struct Walk3Args {
   uint32_t* err;
 };
 
-// equal inexact codes (or NaN): the exact values decide (rare; out of line, scalar arguments)
 template <int OP, bool FP>
-__device__ __noinline__ bool c2_exact3(bool exact_codes, int vtype, int vattr, int cwidth, const void* vcol,
-                                       const int64_t* ord, int64_t obase, int64_t n, const int64_t* crow, int32_t o0,
-                                       uint32_t cs, uint32_t ce, uint32_t oi, uint32_t oj) {
-  const ExactSrc ex{exact_codes, vtype, vattr, cwidth, vcol, ord, obase, n, crow, o0, cs, ce};
-  if constexpr (FP) return cmp_fixed<OP>(ex.fval(oj), ex.fval(oi));
-  else return cmp_fixed<OP>(ex.ival(oj), ex.ival(oi));
+__device__ __forceinline__ bool c2_exact3(bool exact_codes, int vtype, int vattr, int cwidth, const void* vcol,
+                                          const int64_t* ord, int64_t obase, int64_t n, const int64_t* crow, int32_t o0,
+                                          uint32_t cs, uint32_t ce, uint32_t oi, uint32_t oj) {
+  return c2_exact_v<OP, FP>(exact_codes, vtype, vattr, cwidth, vcol, ord, obase, n, crow, o0, cs, ce, oi, oj);
 }
 
 template <int OP, bool FP>
@@ -1485,8 +1506,9 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
     SM_HIP(hipGetDevice(&dev));
     SM_HIP(hipDeviceGetAttribute(&fs.cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  // v3 (rank / walk / count / place) by default; SM_STACK_V2=1 runs the slice-synchronous kernel (A/B)
-  static const bool v2 = getenv("SM_STACK_V2") && atoi(getenv("SM_STACK_V2")) != 0;
+  // the slice-synchronous kernel by default; SM_STACK_V3=1 runs the barrier-free v3 kernels (A/B: exact, but their
+  // drifting lanes gather records and scatter pop slots with little locality: 54.6 + 35 ms against 31.7 + 6.7 ms)
+  static const bool v2 = !(getenv("SM_STACK_V3") && atoi(getenv("SM_STACK_V3")) != 0);
   const int64_t ntiles = (p.omax >> kTB) + 1;
   int64_t M = 0;
   if (!v2) {
