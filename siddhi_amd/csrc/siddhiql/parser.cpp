@@ -695,6 +695,9 @@ struct Parser {
     }
     if (q.name.empty()) q.name = "query_" + std::to_string(++anon_query);
     expect_kw("from");
+    // anonymous_stream (SiddhiQL.g4: `from from ... return` / `from (from ... return)`): a nested query
+    if (is_kw("from") || (is_sym("(") && is_kw("from", 1)))
+      throw UnsupportedError("anonymous (nested) query streams are outside the hot-path subset");
     q.input = classify_input();
     if (q.input == InputKind::SINGLE) {
       StateElem tmp;

@@ -6,6 +6,15 @@ Sources (read here, in the build container; only the extracted data is committed
     SiddhiQL. Input = the comment's `from ...` clause, expected = the builder tree.
   * siddhi-query-compiler .../query/test/AbsentPatternTestCase.java: parseQuery(text) must raise
     SiddhiParserException (test1-3) or equal the builder tree (test4).
+  * siddhi-query-compiler .../query/test/SimpleQueryTestCase.java (filter queries): parseQuery(text) must equal the
+    builder's Query. Every one of them also uses a window, a stream function, an aggregation, group by, order by,
+    limit, update or a nested query, which this engine rejects (OperationNotSupportedException, SURVEY.md §2 out of
+    scope). So each test yields two checks: the full text must be rejected as unsupported (not mis-parsed), and
+    its `from S[f1][f2]...` head up to the first `#` handler must parse into the builder's filter list up to its
+    first window / function call (the FilterProcessor trees of SURVEY.md §8(a) A3-A4).
+  * siddhi-query-compiler .../query/test/DefinePartitionTestCase.java: parsePartition(text) must equal the
+    builder's partition type (the tests compare toString() up to "queryList", so the inner query is not part of
+    the expectation and is replaced by a supported one). test1 (range partitions) is rejected as unsupported.
 The builder expressions are evaluated by a small interpreter of the builder API below (State.java,
 InputStream.java, Expression.java semantics), independent of the product's parser, into the JSON shapes of
 siddhi_amd/csrc/siddhiql/dump.cpp. Next chains are compared flattened (the builders nest `->` to the right,
@@ -26,6 +35,7 @@ TIME_MS = {"milliSec": 1, "millisec": 1, "sec": 1000, "minute": 60_000, "hour": 
 OPS = {"GREATER_THAN": ">", "GREATER_THAN_EQUAL": ">=", "LESS_THAN": "<", "LESS_THAN_EQUAL": "<=", "EQUAL": "==",
        "NOT_EQUAL": "!="}
 LAST, ANY = -2, -1
+MATH = {"add": "+", "subtract": "-", "multiply": "*", "divide": "/", "mod": "%"}
 # tests whose comment and builder disagree: the builder is the reference's pinned tree, so either the comment
 # loses the clause the builder omits, or the test is excluded
 TEXT_FIX = {"PatternQueryTestCase.testPatternQuery6": ("e4=Stream3[price>74] within 2 min", "e4=Stream3[price>74]")}
@@ -135,7 +145,11 @@ def call(name, a):
 
 def method(v, meth, a):
     if v[0] == "bsis" and meth == "filter":
-        v[1]["filters"].append(a[0][1])
+        if not v[1].get("handler"):
+            v[1]["filters"].append(a[0][1])
+        return v
+    if v[0] == "bsis" and meth in ("window", "function"):
+        v[1]["handler"] = True  # `#window...` / `#fn(...)`: the filters after it are outside the checked head
         return v
     if v[0] == "expr" and meth == "ofStream":
         e = dict(v[1])
@@ -171,6 +185,12 @@ def expr_call(fn, a):
         return ("expr", {fn: [a[0][1], a[1][1]]})
     if fn == "not":
         return ("expr", {"not": a[0][1]})
+    if fn in MATH:
+        return ("expr", {"math": MATH[fn], "l": a[0][1], "r": a[1][1]})
+    if fn == "isNull":
+        return ("expr", {"isnull": a[0][1]})
+    if fn == "function":
+        return ("expr", {"function": True})  # aggregations / functions: only inside the rejected full texts
     raise Unsupported("Expression." + fn)
 
 
@@ -283,6 +303,50 @@ def main():
                 k["input"], k["tree"] = builder_tree(body)
             except Unsupported as e:
                 k["skip"] = str(e)
+        kats.append(k)
+    src = open(COMP + "SimpleQueryTestCase.java").read()
+    for name, ann, comment, body, line in methods(src):
+        base = {"source": f"modules/siddhi-query-compiler/src/test/java/org/wso2/siddhi/query/test/"
+                          f"SimpleQueryTestCase.java:{line}"}
+        texts = ["".join(json.loads(x) for x in re.findall(r'"(?:[^"\\]|\\.)*"', q))
+                 for q in re.findall(r"parseQuery\((.*?)\);", body, re.S)]
+        if not texts:
+            continue  # builder-only tests: no text to parse
+        for qi, text in enumerate(texts):
+            text = " ".join(text.split())
+            sfx = f"#{qi + 1}" if len(texts) > 1 else ""
+            kats.append(dict(base, name=f"compiler.SimpleQueryTestCase.{name}{sfx}.full", text=text,
+                             expect="unsupported"))
+            k = dict(base, name=f"compiler.SimpleQueryTestCase.{name}{sfx}.filters")
+            m = re.match(r"from\s+(\w+)\s*((?:\[[^#]*?\]\s*)*)", text)
+            try:
+                if not m or not m.group(2).strip():
+                    raise Unsupported("no `S[filter]` head (nested query or no filter)")
+                k["text"] = "from " + m.group(1) + m.group(2).strip()
+                if "DuplicateAttributeException" in ann:
+                    raise Unsupported("no builder tree (expects DuplicateAttributeException)")
+                b = re.search(r"InputStream\.stream\(", body)
+                v = P(tokenize(body[b.start():])).expr()
+                if v[0] != "bsis":
+                    raise Unsupported("no stream builder")
+                k["input"], k["stream"], k["filters"] = "single", v[1]["stream"], v[1]["filters"]
+            except (Unsupported, IndexError, KeyError) as e:
+                k["skip"] = str(e)
+            kats.append(k)
+    src = open(COMP + "DefinePartitionTestCase.java").read()
+    for name, ann, comment, body, line in methods(src):
+        k = {"name": f"compiler.DefinePartitionTestCase.{name}",
+             "source": f"modules/siddhi-query-compiler/src/test/java/org/wso2/siddhi/query/test/"
+                       f"DefinePartitionTestCase.java:{line}"}
+        q = re.search(r"parsePartition\((.*?)\);", body, re.S)
+        text = " ".join("".join(json.loads(x) for x in re.findall(r'"(?:[^"\\]|\\.)*"', q.group(1))).split())
+        head = re.match(r"(partition with \(.*?\)) begin", text)
+        k["text"] = head.group(1)
+        if "Partition.range" in body:
+            k["expect"] = "unsupported"
+        else:
+            w = re.search(r'with\("(\w+)",\s*(Expression\.variable\("\w+"\))\)', body)
+            k["with"] = [{"stream": w.group(1), "key": P(tokenize(w.group(2))).expr()[1]}]
         kats.append(k)
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "ast_kats.json")
     with open(out, "w") as f:

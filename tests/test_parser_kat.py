@@ -2,7 +2,10 @@
 reference's own query-tree tests must parse into the trees the reference's builders construct
 (tests/golden/ast_kats.json, transcribed by tests/golden/make_ast_kats.py from siddhi-query-api
 PatternQueryTestCase / SequenceQueryTestCase and siddhi-query-compiler AbsentPatternTestCase), or fail with
-SiddhiParserException where the reference's compiler does. The oracle and the product share the parser, so these
+SiddhiParserException where the reference's compiler does. The compiler's SimpleQueryTestCase (filter queries) and
+DefinePartitionTestCase pin the filter-expression trees (FilterProcessor) and the value
+partition type; the parts of those texts outside the hot-path subset (windows, aggregations, group by, update,
+range partitions) must be refused with OperationNotSupportedException, never mis-parsed. The oracle and the product share the parser, so these
 are the checks a parse/binding bug (e.g. `within` attached to the wrong element) cannot pass on both sides.
 CPU only: sm_compile_dump parses without a device."""
 import json
@@ -15,6 +18,8 @@ import siddhi_amd
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ast_kats.json")
 KATS = json.load(open(GOLDEN))
 DEFS = " ".join(f"define stream Stream{k} (symbol string, price float, volume int);" for k in range(1, 5)) + " "
+SIMPLE_DEFS = " ".join(f"define stream {s} (symbol string, price float, volume int);"
+                       for s in ("StockStream", "AllStockQuotes", "cseEventStream")) + " "
 
 
 def norm(s):
@@ -53,6 +58,8 @@ def norm(s):
 def test_parse_kat(kat):
     if "skip" in kat:
         pytest.skip(kat["skip"])
+    if kat["name"].startswith(("compiler.SimpleQueryTestCase", "compiler.DefinePartitionTestCase")):
+        return check_filter_or_partition_kat(kat)
     text = DEFS + kat["text"] + " select * insert into OutputStream;"
     if kat.get("expect") == "parse_error":
         with pytest.raises(siddhi_amd.SiddhiParserException):
@@ -73,3 +80,23 @@ def test_within_binds_to_the_element_it_follows():
     q = siddhi_amd.compile_dump(DEFS + "from (every e1=Stream1 -> e2=Stream2) within 1 sec select * insert into O;")
     st = q["queries"][0]["state"]
     assert st["within"] == 1000 and "within" not in st["next"][1]
+
+
+def check_filter_or_partition_kat(kat):
+    partition = "DefinePartitionTestCase" in kat["name"]
+    if partition:  # the reference compares the partition type only (toString() up to "queryList")
+        text = SIMPLE_DEFS + kat["text"] + " begin from cseEventStream select symbol insert into PartOut; end;"
+    elif kat.get("expect") == "unsupported":
+        text = SIMPLE_DEFS + kat["text"]
+    else:
+        text = SIMPLE_DEFS + kat["text"] + " select symbol insert into OutStockStream;"
+    if kat.get("expect") == "unsupported":
+        with pytest.raises(siddhi_amd.OperationNotSupportedException):
+            siddhi_amd.compile_dump(text)
+        return
+    d = siddhi_amd.compile_dump(text)
+    if partition:
+        assert [p["with"] for p in d["partitions"]] == [kat["with"]]
+        return
+    q = d["queries"][0]
+    assert (q["input"], q["stream"], q["filters"]) == (kat["input"], kat["stream"], kat["filters"])
