@@ -4,7 +4,7 @@
 #include <type_traits>
 
 #include "expr.h"
-#include "fastpath.h"
+#include "nfa.h"
 
 namespace sm {
 namespace {
@@ -34,9 +34,47 @@ struct Ctrl {
 // (__syncthreads() may also drain vmcnt, which exposes every round of scattered stores). No kernel here exchanges
 // global data between the waves of a workgroup.
 __device__ __forceinline__ void lds_barrier() {
+#if defined(__HIP_DEVICE_COMPILE__)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+#else  // host wave emulator (hd.h SM_HOST_EMU): a workgroup barrier
+  __syncthreads();
+#endif
+}
+
+// Lockstep point of a wave: a no-op on the GPU (the lanes of a wave execute each instruction together), a wave
+// barrier under the host wave emulator, where the lanes are threads: placed between an LDS read every lane makes
+// and a write one lane makes to the same word (the rank-counting idiom), which SIMD order serialises on the GPU.
+__device__ __forceinline__ void wave_lockstep() {
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(SM_HOST_EMU)
+  (void)__ballot(1);
+#endif
+}
+
+// gfx950 bit / dot instructions, with plain restatements for the host wave emulator
+__device__ __forceinline__ uint32_t sm_sbfe1(uint32_t d, int b) {  // bit b of d as 0 or ~0
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);
+#else
+  return ((d >> b) & 1u) ? 0xffffffffu : 0u;
+#endif
+}
+__device__ __forceinline__ uint32_t sm_and_not_xor(uint32_t a, uint32_t b, uint32_t c) {  // a & ~(b ^ c)
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x90);  // a = 0xF0, b = 0xCC, c = 0xAA
+#else
+  return a & ~(b ^ c);
+#endif
+}
+__device__ __forceinline__ uint32_t sm_udot4(uint32_t a, uint32_t b, uint32_t c) {  // sum of byte products + c
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_udot4(a, b, c, false);
+#else
+  uint32_t s = c;
+  for (int k = 0; k < 4; ++k) s += ((a >> (8 * k)) & 255u) * ((b >> (8 * k)) & 255u);
+  return s;
+#endif
 }
 
 // Lanes of this wave whose kRB-bit digit equals this lane's (valid lanes only): one ballot per bit, and per
@@ -46,10 +84,10 @@ __device__ __forceinline__ uint64_t peer_mask(uint32_t d, bool valid) {
   uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
 #pragma unroll
   for (int bb = 0; bb < kRB; ++bb) {
-    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)d, bb, 1);  // 0 or ~0
+    const uint32_t m = sm_sbfe1(d, bb);  // 0 or ~0
     const uint64_t bal = __ballot(m != 0u);
-    lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)bal, m, 0x90);  // a & ~(b ^ c), a = 0xF0, b = 0xCC, c = 0xAA
-    hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(bal >> 32), m, 0x90);
+    lo = sm_and_not_xor(lo, (uint32_t)bal, m);
+    hi = sm_and_not_xor(hi, (uint32_t)(bal >> 32), m);
   }
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }

@@ -30,13 +30,13 @@
 #include <cstdlib>
 #include <vector>
 
-#include "fastpath_dev.h"
+#include "fastpath.h"
+#include "stack_dev.h"
 
 namespace sm {
 
 namespace {
 
-constexpr int kKeys = 1024;    // in-bucket keys
 #ifndef SM_STACK_KPT
 #define SM_STACK_KPT 2          // A/B build flag: in-bucket keys per thread (2: 512 threads and a 256-VGPR budget for
 #endif                          // both stacks; 1: 1024 threads, 4 waves per SIMD)
@@ -48,16 +48,8 @@ constexpr int kSW = kSB / 64;
 #endif
 constexpr int kSI = SM_STACK_KSI;  // records per thread per slice
 constexpr int kS = kSB * kSI;      // slice: 4608 records
-#ifndef SM_STACK_KC
-#define SM_STACK_KC 5           // A/B build flag (config 4, slices of 4608: 3 -> 34.9 ms, 4 -> 32.1, 5 -> 31.7)
-#endif
-constexpr int kC = SM_STACK_KC; // stack entries held in registers
-constexpr int kQ = 32;         // spilled entries per thread (HBM ring)
 constexpr int kLog = 4096;     // match log of a slice: kLog / H entries per key thread ...
 constexpr int kOvf = 1024;     // ... and a shared overflow (more: the batch takes the sort / walk kernels)
-constexpr int kOB = 1024;      // order workgroup: thread d owns bucket d
-constexpr int kTB = 13;        // order tile: 2^kTB consecutive relative ordinals
-constexpr int kOT = 1 << kTB;
 constexpr int kOCap = 12288;   // matches of a tile staged in LDS before one coalesced write
 constexpr int kGT = 16;        // consecutive tiles per order workgroup
 
@@ -65,7 +57,6 @@ static_assert(kBins == kKeys && kKeys == kKPT * kSB && kBins == kOB && (kKPT == 
               "one or two in-bucket keys per thread, one bucket per order thread");
 static_assert(kSW * kKeys * 2 <= kLog * 8, "the per-wave key counts of the ranking fit the match log area");
 
-enum : uint32_t { SE_OVERFLOW = 1, SE_LOG = 2, SE_NAN = 4, SE_CAND = 8, SE_ORD = 16 };
 #ifndef SM_STACK_STAMPS_BUILD
 #define SM_STACK_STAMPS_BUILD 0  // build flag: phase clock + counters of the stack kernel (env SM_STACK_STAMPS=1 reads them)
 #endif
@@ -107,159 +98,6 @@ struct StackArgs {
   int dbg;                     // diagnostic mode (SM_STACK_DEBUG): 1 = skip the stacks (wrong results; timing only)
   unsigned long long* counts;  // with stamps: events, pops, refills, spills, exact compares, log overflows
 };
-
-// Exact value of a compared attribute: a batch row's column, or a carried partial's stored value.
-struct ExactSrc {
-  bool exact_codes;
-  int vtype, vattr, cwidth;
-  const void* vcol;
-  const int64_t* ord;
-  int64_t obase, n;
-  const int64_t* crow;
-  int32_t o0;
-  uint32_t cs, ce;  // this key's carried rows
-  __device__ bool carried(uint32_t o) const { return (int32_t)o < o0; }
-  __device__ int64_t row_of(uint32_t o) const {
-    if (!ord) return o;
-    const int64_t want = (int64_t)o + obase;
-    int64_t lo = 0, hi = n - 1;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (ord[mid] < want) lo = mid + 1;
-      else hi = mid;
-    }
-    return lo;
-  }
-  __device__ int64_t carry_row(uint32_t o) const {
-    const int64_t want = (int64_t)(int32_t)o + obase;
-    uint32_t lo = cs, hi = ce;
-    while (lo + 1 < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (crow[(int64_t)mid * cwidth + 1] <= want) lo = mid;
-      else hi = mid;
-    }
-    return lo;
-  }
-  __device__ double fval(uint32_t o) const {
-    if (carried(o)) return __longlong_as_double((long long)crow[carry_row(o) * cwidth + 3 + vattr]);
-    const int64_t r = row_of(o);
-    return vtype == T_FLOAT ? (double)((const float*)vcol)[r] : ((const double*)vcol)[r];
-  }
-  __device__ int64_t ival(uint32_t o) const {
-    if (carried(o)) return crow[carry_row(o) * cwidth + 3 + vattr];
-    const int64_t r = row_of(o);
-    return vtype == T_INT ? (int64_t)((const int32_t*)vcol)[r] : ((const int64_t*)vcol)[r];
-  }
-};
-
-// equal inexact codes (or NaN): the exact values decide. Out of line: rare, and its binary searches must not
-// hold registers in the event loop; the source is passed by value (a reference would put it in scratch).
-template <int OP, bool FP>
-__device__ __noinline__ bool c2_exact_v(bool exact_codes, int vtype, int vattr, int cwidth, const void* vcol,
-                                        const int64_t* ord, int64_t obase, int64_t n, const int64_t* crow, int32_t o0,
-                                        uint32_t cs, uint32_t ce, uint32_t oi, uint32_t oj) {
-  const ExactSrc ex{exact_codes, vtype, vattr, cwidth, vcol, ord, obase, n, crow, o0, cs, ce};
-  if constexpr (FP) return cmp_fixed<OP>(ex.fval(oj), ex.fval(oi));
-  else return cmp_fixed<OP>(ex.ival(oj), ex.ival(oi));
-}
-template <int OP, bool FP>
-__device__ __forceinline__ bool c2_exact(const ExactSrc& ex, uint32_t oi, uint32_t oj) {
-  return c2_exact_v<OP, FP>(ex.exact_codes, ex.vtype, ex.vattr, ex.cwidth, ex.vcol, ex.ord, ex.obase, ex.n, ex.crow,
-                            ex.o0, ex.cs, ex.ce, oi, oj);
-}
-
-// c2 = `e2.x OP e1.x` for partial i (code ci, ordinal oi) and event j
-template <int OP, bool FP>
-__device__ __forceinline__ bool c2_hit(const ExactSrc& ex, uint32_t ci, uint32_t oi, uint32_t cj, uint32_t oj) {
-  const bool nan = FP & ((ci == kNanCode) | (cj == kNanCode));
-  if (!nan & (ex.exact_codes | (ci != cj))) return cmp_fixed<OP>(cj, ci);
-  return c2_exact<OP, FP>(ex, oi, oj);
-}
-
-struct Stack {
-  uint32_t o[kC], c[kC];
-  int32_t t[kC];
-  int n;       // entries in registers
-  int hb, hn;  // spill ring: head, count
-};
-
-__device__ __forceinline__ void st_pop(Stack& s) {
-#pragma unroll
-  for (int k = 0; k + 1 < kC; ++k) {
-    s.o[k] = s.o[k + 1];
-    s.c[k] = s.c[k + 1];
-    s.t[k] = s.t[k + 1];
-  }
-  --s.n;
-}
-
-// the registers ran empty: bring back the youngest spilled entry (one at a time; spills are rare)
-__device__ __forceinline__ void st_refill(Stack& s, const uint4* sp) {
-  const uint4 e = sp[(s.hb + s.hn - 1) & (kQ - 1)];
-  s.o[0] = e.x;
-  s.c[0] = e.y;
-  s.t[0] = (int32_t)e.z;
-  s.hn -= 1;
-  s.n = 1;
-}
-
-// push (o, c, t) on top; `now` = event time of the pushing event (entries older than now - within are dead)
-__device__ __forceinline__ void st_push(Stack& s, uint4* sp, uint32_t o, uint32_t c, int32_t t, int32_t now,
-                                        int64_t within, uint32_t* err) {
-  if (s.n == kC) {
-    if (within >= 0 && now - s.t[kC - 1] > (int32_t)within) {  // the register bottom and all spilled are dead
-      s.hn = 0;
-      s.n = kC - 1;
-    } else {
-      if (s.hn == kQ) {  // free the ring's dead head first
-        while (s.hn > 0 && within >= 0 && now - (int32_t)sp[s.hb & (kQ - 1)].z > (int32_t)within) {
-          s.hb = (s.hb + 1) & (kQ - 1);
-          --s.hn;
-        }
-        if (s.hn == kQ) {  // more than kC + kQ live partials on one key: the walk pipeline takes the batch
-          atomicOr(err, SE_OVERFLOW);
-          s.hb = (s.hb + 1) & (kQ - 1);
-          --s.hn;
-        }
-      }
-      sp[(s.hb + s.hn) & (kQ - 1)] = make_uint4(s.o[kC - 1], s.c[kC - 1], (uint32_t)s.t[kC - 1], 0u);
-      ++s.hn;
-      s.n = kC - 1;
-    }
-  }
-#pragma unroll
-  for (int k = kC - 1; k > 0; --k) {
-    s.o[k] = s.o[k - 1];
-    s.c[k] = s.c[k - 1];
-    s.t[k] = s.t[k - 1];
-  }
-  s.o[0] = o;
-  s.c[0] = c;
-  s.t[0] = t;
-  ++s.n;
-}
-
-// block-wide exclusive scan of one value per thread (NT threads); returns the total through *tot
-template <int NT = kOB>
-__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* lw, uint32_t* tot) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t u = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += u;
-  }
-  if (lane == 63) lw[w] = inc;
-  lds_barrier();
-  uint32_t r = inc - v, t = 0;
-  for (int q = 0; q < NT / 64; ++q) {
-    const uint32_t x = lw[q];
-    if (q < w) r += x;
-    t += x;
-  }
-  *tot = t;
-  return r;
-}
 
 template <int OP, bool FP>
 __global__ void __launch_bounds__(kSB) stack_kernel(StackArgs a) {
@@ -763,514 +601,9 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
   }
 }
 
-// ============================================================================================================
-// v3: the same closed form without slice barriers.
-//   rank3_kernel   per bucket, slice by slice (kSL records in arrival order): rank the slice by in-bucket key in
-//                  LDS (wave64 ballot peer masks, as stack_kernel) and write the grouping to HBM: perm (in-slice
-//                  positions grouped by key, arrival order within a key; u16) and kst (each key's run of it).
-//                  Also the first bucket position of every ordinal tile (pst).
-//   walk3_kernel   one lane per in-bucket key, one workgroup per bucket: each lane walks ALL of its key's events
-//                  of the bucket in one flat loop (slice after slice through perm / kst) against its register
-//                  stack. No barrier: a wave's time is its busiest lane's event count over the whole bucket
-//                  (about 977 +- 31 at config 4), not the sum of per-slice maxima of about 4.5 events each, so the
-//                  lanes stay ~93 % busy. Each event's pops go to its slot (bucket position): none, one inline, or
-//                  two or more as a run [count, i_0, ..., i_c-1] in the bucket's overflow region (youngest first).
-//   count3_kernel  matches per ordinal tile (the u8 pop counts of every bucket's positions in the tile).
-//   place3_kernel  per tile: count per ordinal (each j is one event: a store), block scan, placement of every pop
-//                  at (offset of j) + (its rank counted from the oldest) in an LDS image, one coalesced write at
-//                  the tile's exclusive prefix. Reference order: j, then the pending list's order (oldest e1 first).
-constexpr int kRA = 512;
-constexpr int kRW = kRA / 64;
-constexpr int kRI = 9;
-constexpr int kSL = kRA * kRI;  // records per slice (in-slice positions and run lengths fit 16 bits)
-constexpr int kWB = kKeys;      // walk workgroup: thread h = in-bucket key h
-constexpr uint32_t kSlotEmpty = 0xffffffffu;
-static_assert(kSL < 65536, "in-slice positions are u16");
-
-struct RankArgs {
-  const uint4* rec;
-  const uint32_t* dbase;
-  int64_t n;
-  const uint32_t* sfirst;  // [kBins + 1] first global slice of each bucket
-  uint16_t* perm;          // [slice][kSL]
-  uint32_t* kst;           // [slice][kKeys]: run start | run length << 16
-  uint32_t* pst;           // [kBins][ntiles + 1]: first bucket position of each ordinal tile
-  int64_t ntiles;
-};
-
-__global__ void __launch_bounds__(kRA) rank3_kernel(RankArgs a) {
-  __shared__ uint16_t wcnt[kRW][kKeys];
-  __shared__ uint16_t hst[kKeys];
-  __shared__ uint32_t ordt[kSL];
-  __shared__ uint32_t lw[kRW];
-  __shared__ uint32_t s_lastj;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint64_t lt = lanemask_lt();
-  for (int d = blockIdx.x; d < kBins; d += gridDim.x) {
-    const int64_t b0 = a.dbase[d];
-    const int64_t b1 = d + 1 < kBins ? (int64_t)a.dbase[d + 1] : a.n;
-    const int64_t blen = b1 - b0;
-    const int64_t g0 = a.sfirst[d];
-    uint32_t* pst = a.pst + (int64_t)d * (a.ntiles + 1);
-    if (tid == 0) s_lastj = 0xffffffffu;
-    int64_t s = 0;
-    for (int64_t q = 0; q < blen; q += kSL, ++s) {
-      const int sn = (int)(blen - q < kSL ? blen - q : kSL);
-      uint2 xy[kRI];
-#pragma unroll
-      for (int k = 0; k < kRI; ++k) {
-        const int e = w * 64 * kRI + k * 64 + lane;
-        if (e < sn) {
-          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-          const u32x2 v = __builtin_nontemporal_load((const u32x2*)(a.rec + b0 + q + e));
-          xy[k] = make_uint2(v.x, v.y);
-        }
-      }
-      lds_barrier();  // the previous slice's readers of wcnt / hst / ordt are done
-      for (int k = tid; k < kRW * kKeys / 2; k += kRA) ((uint32_t*)wcnt)[k] = 0;
-      lds_barrier();
-      uint32_t hk[kRI], lp[kRI];
-#pragma unroll
-      for (int k = 0; k < kRI; ++k) {
-        const int e = w * 64 * kRI + k * 64 + lane;
-        const bool valid = e < sn;
-        hk[k] = valid ? (xy[k].x & kKeyMask) >> kRB : 0u;
-        const uint64_t peers = peer_mask(hk[k], valid);
-        uint32_t old = 0;
-        if (valid) old = wcnt[w][hk[k]];
-        const uint32_t below = (uint32_t)__popcll(peers & lt);
-        if (valid && below == 0) wcnt[w][hk[k]] = (uint16_t)(old + (uint32_t)__popcll(peers));
-        lp[k] = old + below;
-      }
-      lds_barrier();
-      {
-        uint32_t r2[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int h = 2 * tid + u;
-          uint32_t r = 0;
-          for (int qq = 0; qq < kRW; ++qq) {
-            const uint32_t c = wcnt[qq][h];
-            wcnt[qq][h] = (uint16_t)r;
-            r += c;
-          }
-          r2[u] = r;
-        }
-        uint32_t tot;
-        const uint32_t st0 = block_excl<kRA>(r2[0] + r2[1], lw, &tot);
-        hst[2 * tid] = (uint16_t)st0;
-        hst[2 * tid + 1] = (uint16_t)(st0 + r2[0]);
-        uint2 kv = make_uint2(st0 | (r2[0] << 16), (st0 + r2[0]) | (r2[1] << 16));
-        *(uint2*)(a.kst + (g0 + s) * kKeys + 2 * tid) = kv;
-      }
-      lds_barrier();
-      uint16_t* pm = a.perm + (g0 + s) * kSL;
-#pragma unroll
-      for (int k = 0; k < kRI; ++k) {
-        const int e = w * 64 * kRI + k * 64 + lane;
-        if (e < sn) {
-          pm[hst[hk[k]] + wcnt[w][hk[k]] + lp[k]] = (uint16_t)e;
-          ordt[e] = xy[k].y;
-        }
-      }
-      lds_barrier();
-      // ordinal tiles whose first ordinal falls in (previous record's ordinal, this record's] start here
-      const uint32_t jprev = s_lastj;
-#pragma unroll
-      for (int k = 0; k < kRI; ++k) {
-        const int e = tid * kRI + k;
-        if (e < sn) {
-          const uint32_t j = ordt[e];
-          const uint32_t jp = e == 0 ? jprev : ordt[e - 1];
-          const uint32_t t0 = jp == 0xffffffffu ? 0u : (jp >> kTB) + 1u;
-          for (uint32_t t = t0; t <= (j >> kTB); ++t) pst[t] = (uint32_t)(q + e);
-        }
-      }
-      lds_barrier();
-      if (tid == 0) s_lastj = ordt[sn - 1];
-    }
-    __syncthreads();
-    {
-      const uint32_t jl = s_lastj;
-      const uint32_t t0 = jl == 0xffffffffu ? 0u : (jl >> kTB) + 1u;
-      for (uint32_t t = t0 + tid; t <= (uint32_t)a.ntiles; t += kRA) pst[t] = (uint32_t)blen;
-    }
-    __syncthreads();
-  }
-}
-
-// first global slice of each bucket (kBins + 1 entries; the last = slices in all)
-__global__ void __launch_bounds__(kOB) slice_base_kernel(const uint32_t* __restrict__ dbase, int64_t n,
-                                                         uint32_t* __restrict__ sfirst) {
-  __shared__ uint32_t lw[kOB / 64];
-  const int d = threadIdx.x;
-  const int64_t b1 = d + 1 < kBins ? (int64_t)dbase[d + 1] : n;
-  const uint32_t c = (uint32_t)((b1 - (int64_t)dbase[d] + kSL - 1) / kSL);
-  uint32_t tot;
-  const uint32_t r = block_excl(c, lw, &tot);
-  sfirst[d] = r;
-  if (d == 0) sfirst[kBins] = tot;
-}
-
-struct Walk3Args {
-  const uint4* rec;
-  const uint32_t* dbase;
-  int64_t n;
-  int H;
-  const uint32_t* sfirst;
-  const uint16_t* perm;
-  const uint32_t* kst;
-  int64_t kmin, within, ts0;
-  bool exact_codes;
-  int vtype, vattr, cwidth;
-  const void* vcol;
-  const int64_t* ord;
-  int64_t obase;
-  int32_t o0;
-  const uint4* cin;
-  const uint32_t* cstart;
-  const uint32_t* cend;
-  const int64_t* crow;
-  // outputs
-  uint2* slot;      // per bucket position: {j | multi << 31 (kSlotEmpty: no pop), i or overflow index}
-  uint8_t* cnt8;    // per bucket position: pops
-  uint32_t* ovf;    // bucket d's overflow region: [3 * sbase[d] + 64 * d, + 3 * (sbase[d + 1] - sbase[d]) + 64)
-  const uint32_t* sbase;
-  uint4* spill;
-  int64_t* cand;
-  uint32_t* cand_n;
-  uint32_t cand_cap;
-  uint32_t* err;
-};
-
 template <int OP, bool FP>
-__device__ __forceinline__ bool c2_exact3(bool exact_codes, int vtype, int vattr, int cwidth, const void* vcol,
-                                          const int64_t* ord, int64_t obase, int64_t n, const int64_t* crow, int32_t o0,
-                                          uint32_t cs, uint32_t ce, uint32_t oi, uint32_t oj) {
-  return c2_exact_v<OP, FP>(exact_codes, vtype, vattr, cwidth, vcol, ord, obase, n, crow, o0, cs, ce, oi, oj);
-}
-
-template <int OP, bool FP>
-__global__ void __launch_bounds__(kWB) walk3_kernel(Walk3Args a) {
-  __shared__ uint32_t s_ovf;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int h = tid;
-  const bool has = h < a.H;
-  const int32_t within32 = (int32_t)a.within;
-  uint4* sp = a.spill + ((int64_t)blockIdx.x * kKeys + h) * kQ;
-  for (int d = blockIdx.x; d < kBins; d += gridDim.x) {
-    __syncthreads();  // the previous bucket's overflow allocations are done
-    if (tid == 0) s_ovf = 0;
-    __syncthreads();
-    const int64_t b0 = a.dbase[d];
-    const int64_t g0 = a.sfirst[d];
-    const int S = (int)(a.sfirst[d + 1] - g0);
-    uint32_t* ovf = a.ovf + 3 * (int64_t)a.sbase[d] + 64 * (int64_t)d;
-    const uint32_t ocap = 3 * (a.sbase[d + 1] - a.sbase[d]) + 64;
-    const uint32_t kr = ((uint32_t)h << kRB) | (uint32_t)d;
-    Stack st;
-    st.n = st.hb = st.hn = 0;
-    uint32_t cs = 0, ce = 0;
-    if (has && a.cin) {  // carried partials first (oldest first)
-      cs = a.cstart[kr];
-      ce = a.cend[kr];
-      for (uint32_t q = cs; q < ce; ++q) {
-        const uint4 e = a.cin[q];
-        st_push(st, sp, e.x, e.y, (int32_t)e.z, (int32_t)e.z, a.within, a.err);
-      }
-    }
-    int32_t tl = 0;
-    bool seen = false;
-    int s = -1;
-    uint32_t x = 0, cnt = 0;
-    const uint16_t* pp = nullptr;
-    int64_t sq = 0;
-    bool live = has;
-    while (__any(live)) {
-      if (live && x == cnt) {  // the key's next slice with events
-        for (;;) {
-          if (++s >= S) {
-            live = false;
-            break;
-          }
-          const uint32_t v = a.kst[(g0 + s) * kKeys + h];
-          cnt = v >> 16;
-          x = 0;
-          if (cnt) {
-            pp = a.perm + (g0 + s) * kSL + (v & 0xffffu);
-            sq = (int64_t)s * kSL;
-            break;
-          }
-        }
-      }
-      // ---- one event against the stack: the register part of the pops first (nothing changes yet)
-      uint32_t e = 0, cj = 0, oj = 0, npop = 0, need = 0, hit = 0, exp = 0;
-      uint4 r = make_uint4(0, 0, 0, 0);
-      bool cont = false, stop_expired = false;
-      int32_t jt = 0;
-      if (live) {
-        e = pp[x];
-        ++x;
-        r = a.rec[b0 + sq + e];
-        jt = (int32_t)r.w;
-        cj = r.z;
-        oj = r.y;
-        tl = jt;
-        seen = true;
-        if (FP && cj == kNanCode) atomicOr(a.err, SE_NAN);
-        uint32_t tie = 0;
-#pragma unroll
-        for (int k = 0; k < kC; ++k) {
-          const bool lv = k < st.n;
-          const bool xx = within32 >= 0 && jt - st.t[k] > within32;
-          const bool t = !a.exact_codes && st.c[k] == cj;
-          const bool nan = FP && ((st.c[k] == kNanCode) | (cj == kNanCode));
-          hit |= (lv && cmp_fixed<OP>(cj, st.c[k])) ? (1u << k) : 0u;
-          exp |= (lv && xx) ? (1u << k) : 0u;
-          tie |= (lv && (t || nan)) ? (1u << k) : 0u;
-        }
-        if (tie) {
-#pragma unroll
-          for (int k = 0; k < kC; ++k)
-            if ((tie >> k) & 1u) {
-              const bool hh = c2_exact3<OP, FP>(a.exact_codes, a.vtype, a.vattr, a.cwidth, a.vcol, a.ord, a.obase,
-                                                a.n, a.crow, a.o0, cs, ce, st.o[k], oj);
-              hit = hh ? (hit | (1u << k)) : (hit & ~(1u << k));
-            }
-        }
-        const uint32_t ok = hit & ~exp;
-        npop = (uint32_t)__builtin_ctz(~ok);
-        if (npop > (uint32_t)st.n) npop = st.n;
-        stop_expired = npop < (uint32_t)st.n && ((exp >> npop) & 1u);
-        cont = !stop_expired && npop == (uint32_t)st.n && st.hn > 0;
-        const uint32_t most = npop + (cont ? (uint32_t)st.hn : 0u);
-        need = most >= 2 ? 1 + most : 0;
-      }
-      // ---- overflow runs of this round: one LDS allocation per wave
-      uint32_t inc = need;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += u;
-      }
-      uint32_t wbase = 0;
-      const uint32_t wtot = __shfl(inc, 63, 64);
-      if (lane == 63 && wtot) wbase = atomicAdd(&s_ovf, wtot);
-      const uint32_t obi = __shfl(wbase, 63, 64) + inc - need;
-      if (live) {
-        const bool multi = need != 0;
-        if (multi && obi + need > ocap) {
-          atomicOr(a.err, SE_LOG);
-        } else {
-          uint32_t* run = ovf + obi;
-          uint32_t first = 0;
-#pragma unroll
-          for (int k = 0; k < kC; ++k)
-            if ((uint32_t)k < npop) {
-              if (multi) run[1 + k] = st.o[k];
-              else first = st.o[k];
-            }
-          // shift the register part down by npop
-#pragma unroll
-          for (int b = 1; b < kC; b <<= 1)
-            if (npop & b) {
-#pragma unroll
-              for (int k = 0; k < kC; ++k)
-                if (k + b < kC) {
-                  st.o[k] = st.o[k + b];
-                  st.c[k] = st.c[k + b];
-                  st.t[k] = st.t[k + b];
-                }
-            }
-          st.n -= (int)npop;
-          if (stop_expired) {  // the entry that stopped the run has expired: so has every older one
-            st.n = 0;
-            st.hn = 0;
-          } else if (cont) {  // ran through the registers: continue into the spill
-            for (;;) {
-              st_refill(st, sp);
-              if (within32 >= 0 && jt - st.t[0] > within32) {
-                st.n = 0;
-                st.hn = 0;
-                break;
-              }
-              const bool nan = FP & ((st.c[0] == kNanCode) | (cj == kNanCode));
-              const bool hh = (!nan & (a.exact_codes | (st.c[0] != cj)))
-                                  ? cmp_fixed<OP>(cj, st.c[0])
-                                  : c2_exact3<OP, FP>(a.exact_codes, a.vtype, a.vattr, a.cwidth, a.vcol, a.ord,
-                                                      a.obase, a.n, a.crow, a.o0, cs, ce, st.o[0], oj);
-              if (!hh) break;
-              run[1 + npop] = st.o[0];
-              ++npop;
-              st_pop(st);
-              if (st.hn == 0) break;
-            }
-          }
-          const int64_t p = b0 + sq + e;
-          a.cnt8[p] = (uint8_t)npop;
-          if (multi) {
-            run[0] = npop;
-            a.slot[p] = make_uint2(oj | 0x80000000u, obi);
-          } else if (npop) {
-            a.slot[p] = make_uint2(oj, first);
-          }
-          if (r.x >> 31) st_push(st, sp, oj, cj, jt, jt, a.within, a.err);
-        }
-      }
-    }
-    // ---- carry out: the partials still pending in the reference (not matched, not found expired by the key's
-    // last event; a key without events in this batch keeps all of its carried partials)
-    auto pending = [&](int32_t t) { return !seen || a.within < 0 || (int64_t)tl - t <= a.within; };
-    uint32_t keep = 0;
-    if (has) {
-#pragma unroll
-      for (int k = 0; k < kC; ++k)
-        if (k < st.n && pending(st.t[k])) ++keep;
-      for (int k = 0; k < st.hn; ++k)
-        if (pending((int32_t)sp[(st.hb + k) & (kQ - 1)].z)) ++keep;
-    }
-    uint32_t inc = keep;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += u;
-    }
-    uint32_t base = 0;
-    if (lane == 63 && inc) base = atomicAdd(a.cand_n, inc);
-    base = __shfl(base, 63, 64) + inc - keep;
-    if (keep) {
-      const ExactSrc ex{a.exact_codes, a.vtype, a.vattr, a.cwidth, a.vcol, a.ord, a.obase, a.n, a.crow, a.o0, cs, ce};
-      const int64_t key = a.kmin + (int64_t)kr;
-      auto put = [&](uint32_t o, int32_t t) {
-        if (!pending(t)) return;
-        if (base < a.cand_cap) {
-          int64_t* c = a.cand + 4 * (int64_t)base;
-          c[0] = key;
-          c[1] = (int64_t)(int32_t)o + a.obase;
-          c[2] = (int64_t)t + a.ts0;
-          c[3] = ex.carried(o) ? -(int64_t)ex.carry_row(o) - 1 : ex.row_of(o);
-        } else {
-          atomicOr(a.err, SE_CAND);
-        }
-        ++base;
-      };
-      // one run per key, oldest first (build_carry's key_runs_ordered relies on it): spill ring, then registers
-      for (int k = 0; k < st.hn; ++k) {
-        const uint4 q = sp[(st.hb + k) & (kQ - 1)];
-        put(q.x, (int32_t)q.z);
-      }
-#pragma unroll
-      for (int k = kC - 1; k >= 0; --k)
-        if (k < st.n) put(st.o[k], st.t[k]);
-    }
-  }
-}
-
-// matches of every ordinal tile: the pops of each bucket's positions in it
-__global__ void __launch_bounds__(kOB) count3_kernel(const uint8_t* __restrict__ cnt8, const uint32_t* __restrict__ dbase,
-                                                     const uint32_t* __restrict__ pt, int64_t ntiles,
-                                                     uint32_t* __restrict__ ttot) {
-  __shared__ uint32_t lw[kOB / 64];
-  const int d = threadIdx.x;
-  const int64_t tb = (int64_t)blockIdx.x * kGT;
-  const int64_t te = tb + kGT < ntiles ? tb + kGT : ntiles;
-  const uint8_t* c = cnt8 + dbase[d];
-  uint32_t ps = pt[tb * kBins + d];
-  for (int64_t t = tb; t < te; ++t) {
-    const uint32_t pe = pt[(t + 1) * kBins + d];
-    uint32_t sum = 0;
-    for (uint32_t p = ps; p < pe; ++p) sum += c[p];
-    ps = pe;
-    uint32_t tot;
-    (void)block_excl(sum, lw, &tot);
-    if (d == 0) ttot[t] = tot;
-    lds_barrier();  // lw is reused by the next tile's scan
-  }
-}
-
-struct Place3Args {
-  const uint2* slot;
-  const uint8_t* cnt8;
-  const uint32_t* ovf;
-  const uint32_t* sbase;
-  const uint32_t* dbase;
-  const uint32_t* pt;    // [t][d] first bucket position of tile t
-  const uint32_t* toff;  // exclusive prefix of the tiles' matches
-  int64_t ntiles;
-  uint64_t* out;
-};
-
-__global__ void __launch_bounds__(kOB) place3_kernel(Place3Args a) {
-  __shared__ uint32_t cnt[kOT];
-  __shared__ uint64_t obuf[kOCap];
-  __shared__ uint32_t lw[kOB / 64];
-  const int tid = threadIdx.x, d = tid;
-  const int64_t tb = (int64_t)blockIdx.x * kGT;
-  const int64_t te = tb + kGT < a.ntiles ? tb + kGT : a.ntiles;
-  const int64_t b0 = a.dbase[d];
-  const uint2* slot = a.slot + b0;
-  const uint8_t* c8 = a.cnt8 + b0;
-  const uint32_t* ovf = a.ovf + 3 * (int64_t)a.sbase[d] + 64 * (int64_t)d;
-  uint32_t ps = a.pt[tb * kBins + d];
-  for (int64_t t = tb; t < te; ++t) {
-    const uint32_t pe = a.pt[(t + 1) * kBins + d];
-    const uint32_t j0 = (uint32_t)(t << kTB);
-    lds_barrier();  // previous tile's readers are done
-    for (int k = tid; k < kOT; k += kOB) cnt[k] = 0;
-    lds_barrier();
-    for (uint32_t p = ps; p < pe; ++p) {  // each j is one event: its pop count is a plain store
-      const uint32_t c = c8[p];
-      if (c) cnt[(slot[p].x & 0x7fffffffu) - j0] = c;
-    }
-    lds_barrier();
-    uint32_t tot;
-    {
-      constexpr int kPer = kOT / kOB;
-      uint32_t v[kPer], sum = 0;
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        v[k] = cnt[tid * kPer + k];
-        sum += v[k];
-      }
-      uint32_t r = block_excl(sum, lw, &tot);
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        cnt[tid * kPer + k] = r;
-        r += v[k];
-      }
-    }
-    lds_barrier();
-    const bool staged = tot <= (uint32_t)kOCap;
-    uint64_t* out = a.out + a.toff[t];
-    for (uint32_t p = ps; p < pe; ++p) {
-      const uint32_t c = c8[p];
-      if (!c) continue;
-      const uint2 v = slot[p];
-      const uint32_t j = v.x & 0x7fffffffu;
-      const uint32_t o = cnt[j - j0];
-      const uint64_t jhi = (uint64_t)j << 32;
-      if (!(v.x >> 31)) {
-        if (staged) obuf[o] = jhi | v.y;
-        else out[o] = jhi | v.y;
-      } else {
-        const uint32_t* run = ovf + v.y + 1;  // youngest first: the oldest e1 is output first
-        for (uint32_t k = 0; k < c; ++k) {
-          const uint64_t m = jhi | run[k];
-          if (staged) obuf[o + c - 1 - k] = m;
-          else out[o + c - 1 - k] = m;
-        }
-      }
-    }
-    ps = pe;
-    lds_barrier();
-    if (staged)
-      for (uint32_t k = tid; k < tot; k += kOB) out[k] = obuf[k];
-  }
-}
-
-template <int OP, bool FP>
-void launch_walk3_t(const Walk3Args& wa, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((walk3_kernel<OP, FP>), dim3(grid), dim3(kWB), 0, s, wa);
+void launch_stack4_t(const Stack4Args& a4, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((stack4_kernel<OP, FP>), dim3(grid), dim3(kT4), 0, s, a4);
 }
 
 // Carried partials for this batch: codes of the compared value and each key's row range. Keys outside the
@@ -1506,108 +839,12 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
     SM_HIP(hipGetDevice(&dev));
     SM_HIP(hipDeviceGetAttribute(&fs.cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  // the slice-synchronous kernel by default; SM_STACK_V3=1 runs the barrier-free v3 kernels (A/B: exact, but their
-  // drifting lanes gather records and scatter pop slots with little locality: 54.6 + 35 ms against 31.7 + 6.7 ms)
-  static const bool v2 = !(getenv("SM_STACK_V3") && atoi(getenv("SM_STACK_V3")) != 0);
-  const int64_t ntiles = (p.omax >> kTB) + 1;
+  // the ring kernel (v4) by default; SM_STACK_V2=1 runs the slice-synchronous kernel (A/B). (A barrier-free v3,
+  // whose lanes walked their key's events through an HBM permutation, was exact but slower: its drifting lanes
+  // gathered records and scattered pop slots with little locality, 54.6 + 35 ms against 31.7 + 6.7 ms.)
+  static const bool v2 = getenv("SM_STACK_V2") && atoi(getenv("SM_STACK_V2")) != 0;
   int64_t M = 0;
-  if (!v2) {
-    uint32_t* sfirst = (uint32_t*)sc.take((kBins + 1) * 4);
-    hipLaunchKernelGGL(slice_base_kernel, dim3(1), dim3(kOB), 0, s, p.dbase, n, sfirst);
-    const int64_t nsl = n / kSL + kBins + 1;  // slices in all (bound)
-    RankArgs ra{};
-    ra.rec = (const uint4*)p.rec;
-    ra.dbase = p.dbase;
-    ra.n = n;
-    ra.sfirst = sfirst;
-    ra.perm = (uint16_t*)sc.take((size_t)nsl * kSL * 2);
-    ra.kst = (uint32_t*)sc.take((size_t)nsl * kKeys * 4);
-    ra.pst = (uint32_t*)sc.take((size_t)kBins * (ntiles + 1) * 4);
-    ra.ntiles = ntiles;
-    tmark("stack_prep");
-    hipLaunchKernelGGL(rank3_kernel, dim3(kBins), dim3(kRA), 0, s, ra);
-    uint32_t* pt = (uint32_t*)sc.take((size_t)kBins * (ntiles + 1) * 4);
-    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((ntiles + 1 + 31) / 32), kBins / 32), dim3(256), 0, s, ra.pst,
-                       ntiles + 1, pt);
-    tmark("stack_rank");
-    Walk3Args wa{};
-    wa.rec = (const uint4*)p.rec;
-    wa.dbase = p.dbase;
-    wa.n = n;
-    wa.H = p.H;
-    wa.sfirst = sfirst;
-    wa.perm = ra.perm;
-    wa.kst = ra.kst;
-    wa.kmin = p.kmin;
-    wa.within = p.within;
-    wa.ts0 = p.ts0;
-    wa.exact_codes = p.exact_codes;
-    wa.vtype = p.vtype;
-    wa.vattr = p.vattr;
-    wa.cwidth = sa.cwidth;
-    wa.vcol = p.vcol;
-    wa.ord = a.ordinals;
-    wa.obase = a.ordinal_base;
-    wa.o0 = p.o0;
-    wa.cin = sa.cin;
-    wa.cstart = sa.cstart;
-    wa.cend = sa.cend;
-    wa.crow = sa.crow;
-    wa.slot = (uint2*)sc.take((size_t)n * 8);
-    wa.cnt8 = (uint8_t*)sc.take((size_t)n);
-    wa.ovf = (uint32_t*)sc.take(((size_t)3 * (n + extra) + 64 * kBins) * 4);
-    wa.sbase = sbase;
-    const int gw = std::min(kBins, 2 * fs.cus);
-    wa.spill = (uint4*)sc.take((size_t)gw * kKeys * kQ * 16);
-    wa.cand = sa.cand;
-    wa.cand_n = cand_n;
-    wa.cand_cap = sa.cand_cap;
-    wa.err = err;
-    switch (p.op * 2 + (p.fp ? 1 : 0)) {
-      case CMP_GT * 2: launch_walk3_t<CMP_GT, false>(wa, gw, s); break;
-      case CMP_GT * 2 + 1: launch_walk3_t<CMP_GT, true>(wa, gw, s); break;
-      case CMP_GE * 2: launch_walk3_t<CMP_GE, false>(wa, gw, s); break;
-      case CMP_GE * 2 + 1: launch_walk3_t<CMP_GE, true>(wa, gw, s); break;
-      case CMP_LT * 2: launch_walk3_t<CMP_LT, false>(wa, gw, s); break;
-      case CMP_LT * 2 + 1: launch_walk3_t<CMP_LT, true>(wa, gw, s); break;
-      case CMP_LE * 2: launch_walk3_t<CMP_LE, false>(wa, gw, s); break;
-      case CMP_LE * 2 + 1: launch_walk3_t<CMP_LE, true>(wa, gw, s); break;
-      default: sc.used = mark; return -1;
-    }
-    tmark("stack");
-    SM_HIP(hipMemcpyAsync(hs, err, 12, hipMemcpyDeviceToHost, s));
-    SM_HIP(hipStreamSynchronize(s));
-    if (hs[0]) {
-      sc.used = mark;
-      return -1;
-    }
-    uint32_t* ttot = (uint32_t*)sc.take((size_t)(ntiles + 1) * 4);
-    const unsigned gt = (unsigned)((ntiles + kGT - 1) / kGT);
-    hipLaunchKernelGGL(count3_kernel, dim3(gt), dim3(kOB), 0, s, wa.cnt8, p.dbase, pt, ntiles, ttot);
-    exclusive_scan_u32(ttot, (size_t)ntiles, sc, s, ttot + ntiles);
-    uint32_t hm = 0;
-    SM_HIP(hipMemcpyAsync(&hm, ttot + ntiles, 4, hipMemcpyDeviceToHost, s));
-    SM_HIP(hipStreamSynchronize(s));
-    tmark("order_count");
-    M = hm;
-    if (M > pairs_cap) {
-      sc.used = mark;
-      throw std::runtime_error("match buffer too small");
-    }
-    if (M > 0) {
-      Place3Args pa{};
-      pa.slot = wa.slot;
-      pa.cnt8 = wa.cnt8;
-      pa.ovf = wa.ovf;
-      pa.sbase = sbase;
-      pa.dbase = p.dbase;
-      pa.pt = pt;
-      pa.toff = ttot;
-      pa.ntiles = ntiles;
-      pa.out = (uint64_t*)pairs_out;
-      hipLaunchKernelGGL(place3_kernel, dim3(gt), dim3(kOB), 0, s, pa);
-    }
-  } else {
+  {
     sa.sbase = sbase;
     sa.stage = (uint64_t*)sc.take((size_t)(n + extra) * 8);
     sa.mstart = (uint32_t*)sc.take((size_t)kBins * (sa.ntiles + 1) * 4);
@@ -1620,7 +857,7 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
     }
     const int grid = std::min(kBins, fs.cus);
     sa.spill = (uint4*)sc.take((size_t)grid * kKeys * kQ * 16);
-    static const bool want_stamps = getenv("SM_STACK_STAMPS") != nullptr;
+    static const bool want_stamps = v2 && getenv("SM_STACK_STAMPS") != nullptr;
     static const int dbg = getenv("SM_STACK_DEBUG") ? atoi(getenv("SM_STACK_DEBUG")) : 0;
     sa.dbg = dbg;
     if (want_stamps) {
@@ -1629,16 +866,68 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
       SM_HIP(hipMemsetAsync(sa.stamps, 0, 128, s));
     }
     tmark("stack_prep");
-    switch (p.op * 2 + (p.fp ? 1 : 0)) {
-      case CMP_GT * 2: launch_stack_t<CMP_GT, false>(sa, grid, s); break;
-      case CMP_GT * 2 + 1: launch_stack_t<CMP_GT, true>(sa, grid, s); break;
-      case CMP_GE * 2: launch_stack_t<CMP_GE, false>(sa, grid, s); break;
-      case CMP_GE * 2 + 1: launch_stack_t<CMP_GE, true>(sa, grid, s); break;
-      case CMP_LT * 2: launch_stack_t<CMP_LT, false>(sa, grid, s); break;
-      case CMP_LT * 2 + 1: launch_stack_t<CMP_LT, true>(sa, grid, s); break;
-      case CMP_LE * 2: launch_stack_t<CMP_LE, false>(sa, grid, s); break;
-      case CMP_LE * 2 + 1: launch_stack_t<CMP_LE, true>(sa, grid, s); break;
-      default: sc.used = mark; return -1;
+    if (v2) {
+      switch (p.op * 2 + (p.fp ? 1 : 0)) {
+        case CMP_GT * 2: launch_stack_t<CMP_GT, false>(sa, grid, s); break;
+        case CMP_GT * 2 + 1: launch_stack_t<CMP_GT, true>(sa, grid, s); break;
+        case CMP_GE * 2: launch_stack_t<CMP_GE, false>(sa, grid, s); break;
+        case CMP_GE * 2 + 1: launch_stack_t<CMP_GE, true>(sa, grid, s); break;
+        case CMP_LT * 2: launch_stack_t<CMP_LT, false>(sa, grid, s); break;
+        case CMP_LT * 2 + 1: launch_stack_t<CMP_LT, true>(sa, grid, s); break;
+        case CMP_LE * 2: launch_stack_t<CMP_LE, false>(sa, grid, s); break;
+        case CMP_LE * 2 + 1: launch_stack_t<CMP_LE, true>(sa, grid, s); break;
+        default: sc.used = mark; return -1;
+      }
+    } else {
+      Stack4Cold c4{};
+      c4.kmin = sa.kmin;
+      c4.ts0 = sa.ts0;
+      c4.within = sa.within;
+      c4.obase = sa.obase;
+      c4.n = n;
+      c4.vtype = sa.vtype;
+      c4.vattr = sa.vattr;
+      c4.cwidth = sa.cwidth;
+      c4.o0 = sa.o0;
+      c4.exact_codes = sa.exact_codes;
+      c4.vcol = sa.vcol;
+      c4.ord = sa.ord;
+      c4.cin = sa.cin;
+      c4.cstart = sa.cstart;
+      c4.cend = sa.cend;
+      c4.crow = sa.crow;
+      c4.cand = sa.cand;
+      c4.cand_n = sa.cand_n;
+      c4.cand_cap = sa.cand_cap;
+      Stack4Cold* c4d = (Stack4Cold*)sc.take(sizeof(Stack4Cold));
+      SM_HIP(hipMemcpyAsync(c4d, &c4, sizeof(c4), hipMemcpyHostToDevice, s));
+      SM_HIP(hipStreamSynchronize(s));  // c4 is a local of this block
+      Stack4Args a4{};
+      a4.rec = sa.rec;
+      a4.dbase = sa.dbase;
+      a4.n = (uint32_t)n;
+      a4.H = sa.H;
+      a4.within = sa.within < 0 ? -1 : (int32_t)sa.within;
+      a4.exact_codes = sa.exact_codes;
+      a4.ntiles = (uint32_t)sa.ntiles;
+      a4.sbase = sa.sbase;
+      a4.stage = sa.stage;
+      a4.mstart = sa.mstart;
+      a4.mtot = sa.mtot;
+      a4.spill = sa.spill;
+      a4.err = sa.err;
+      a4.cold = c4d;
+      switch (p.op * 2 + (p.fp ? 1 : 0)) {
+        case CMP_GT * 2: launch_stack4_t<CMP_GT, false>(a4, grid, s); break;
+        case CMP_GT * 2 + 1: launch_stack4_t<CMP_GT, true>(a4, grid, s); break;
+        case CMP_GE * 2: launch_stack4_t<CMP_GE, false>(a4, grid, s); break;
+        case CMP_GE * 2 + 1: launch_stack4_t<CMP_GE, true>(a4, grid, s); break;
+        case CMP_LT * 2: launch_stack4_t<CMP_LT, false>(a4, grid, s); break;
+        case CMP_LT * 2 + 1: launch_stack4_t<CMP_LT, true>(a4, grid, s); break;
+        case CMP_LE * 2: launch_stack4_t<CMP_LE, false>(a4, grid, s); break;
+        case CMP_LE * 2 + 1: launch_stack4_t<CMP_LE, true>(a4, grid, s); break;
+        default: sc.used = mark; return -1;
+      }
     }
     tmark("stack");
     if (sa.stamps) {
