@@ -312,6 +312,7 @@ def main():
     ap.add_argument("--ts-div", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="config 4: skip the end-to-end (H2D-inclusive) variant")
     ap.add_argument("--stack", type=int, default=0, choices=(0, 1, 2),
                     help="device-batch pipeline for configs 3/4: 0 automatic, 1 bucket stack, 2 sort / walk")
     ap.add_argument("--variant", default=None, choices=sorted(VARIANTS5),
@@ -460,6 +461,32 @@ def main():
     value = units / (dt / args.steps)
 
     roof = roofline(ktot, n_local[0], nm, args.steps, args.config)
+    e2e = None
+    if args.config == 4 and world == 1 and not args.no_e2e:
+        # SURVEY.md §8(d) end-to-end variant: the same step with the three columns the plan reads (symbol i32,
+        # price f64, event time i64: 20 B/event) copied host -> device first, from pinned host buffers, timed together
+        log("e2e variant: pinning the host columns")
+        host = [x.cpu().pin_memory() for x in (symbol, price, ts)]
+        best = None
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for d, h in zip((symbol, price, ts), host):
+                d.copy_(h, non_blocking=True)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            m_e2e = step()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            if m_e2e != nm:
+                raise RuntimeError(f"e2e step found {m_e2e} matches, the device-resident steps {nm}")
+            if best is None or t3 - t1 < best[1]:
+                best = (t2 - t1, t3 - t1)
+        del host
+        e2e = {"ms_per_step": best[1] * 1e3, "value": N / best[1], "unit": "events/s", "h2d_ms": best[0] * 1e3,
+               "h2d_GBps": 20 * N / best[0] / 1e9,
+               "note": "H2D of symbol + price + event time from pinned host memory over PCIe, then the step; "
+                       "not overlapped (best of 2)"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         sample = args.cpu_sample or cfg["cpu_sample"]
@@ -500,6 +527,8 @@ def main():
             "dtype": "f64", "data": "synthetic (counter-based splitmix64 StockStream, device-resident)",
             "config": conf, "roofline": roof, "cpu_baseline": cpu,
         }
+        if e2e:
+            line["e2e_with_h2d"] = e2e
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -509,16 +538,16 @@ def main():
 # ALGORITHMIC bytes per launch for a batch of n events with m matches: what each launch must read
 # and write at minimum.
 KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last",
-           "stack_prep", "stack_rank", "stack", "order_count", "order", "carry_merge", "carry_out",
+           "stack_prep", "stack", "order", "carry_merge", "carry_out",
            "filter_count", "filter_scan", "filter_write",
            "event_index", "nfa_select", "nfa_group", "nfa_setup", "nfa"]
 
 
 def alg_bytes(label, n, m, config):
     keyed = config == 4
-    return {"prep": (12 * n) if keyed else (16 * n + n // 8),  # keyed: key i32 + ts i64 (c1 = price > 20 is
-                                                              # evaluated in pass 0); unkeyed: ts + price in,
-                                                              # c1 bit out
+    return {"prep": (4 * n) if keyed else (16 * n + n // 8),  # keyed: key i32 (c1 = price > 20 and the event-time
+                                                             # order are evaluated in pass 0); unkeyed: ts +
+                                                             # price in, c1 bit out
             "key_up": 16 * n,               # pass-1 digits: one 16-B record per event (the key word of each)
             "scan": 0,                      # per-chunk digit counts (O(chunks x 1024), not per event)
             "key_pass0": 20 * n + 16 * n,   # key i32 + price f64 + ts i64 in, 16-B keyed record out
@@ -526,10 +555,8 @@ def alg_bytes(label, n, m, config):
             "walk": (16 * n + 8 * m) if keyed else (16 * n + n // 8 + 8 * m),  # records (unkeyed: price + ts +
                                                                                # c1 bits) in, (j, i) pairs out
             "stack_prep": 0,                # staging bases (O(kBins))
-            "stack_rank": 16 * n + 2 * n,   # bucket records in, key-grouped u16 in-slice positions out
-            "stack": 16 * n + 2 * n + n + 8 * m,  # positions + records in; pop counts + pops (j, i) out
-            "order_count": n,               # pop counts in
-            "order": n + 8 * m + 8 * m,     # pop counts + pops in, output pairs out (reference order)
+            "stack": 16 * n + 8 * m,        # bucket records in, staged (j, i) pairs out (bucket order)
+            "order": 8 * m + 8 * m,         # staged pairs in, output pairs out (reference order)
             "carry_merge": 16 * m,
             "carry_out": 0,                 # open partials at the end of the batch (O(keys))
             "j_up": 4 * m,

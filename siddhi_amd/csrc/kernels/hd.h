@@ -20,6 +20,11 @@ inline unsigned atomicAdd(unsigned* p, unsigned v) {
   *p += v;
   return o;
 }
+inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
+  unsigned long long o = *p;
+  *p += v;
+  return o;
+}
 inline int atomicOr(int* p, int v) {
   int o = *p;
   *p |= v;

@@ -215,9 +215,10 @@ struct Lane {
     for (int k = 4; k < PQ->node_words; ++k) heap[n + k] = 0;
     return n;
   }
-  // the incoming event, materialised as a chain node once per delivery: a copy of the node image the
-  // lane-events pass already built (LaneEv, nfa.h)
-  SM_JIT_INL __device__ int32_t event_node(const int64_t* __restrict__ r) {
+  // StreamEventCloner.copyStreamEvent of the incoming event: the copy is made straight from the node image the
+  // lane-events pass built (LaneEv, nfa.h). The event itself is never materialised in the heap: every use of it
+  // in processAndReturn is such a copy, so an event no pending partial takes allocates nothing.
+  SM_INL_SMALL __device__ int32_t copy_event(const int64_t* __restrict__ r) {
     int32_t n = alloc(PQ->node_words);
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
     for (int w = 1; w < PQ->node_words; ++w) heap[n + w] = r[LaneEv::kNode + w];
@@ -647,7 +648,7 @@ struct Lane {
 
   // processAndReturn of every pre kind; returned records are appended to the temporary list `ret`
   // (the pre's list word 3: the selector runs after the loop, as in the receivers).
-  SM_INL_PAR __device__ void processAndReturn(int p, int32_t evnode, int64_t now) {
+  SM_INL_PAR __device__ void processAndReturn(int p, const int64_t* __restrict__ evr, int64_t now) {
     const DPre& P = PPRE[p];
     const int sid = P.stateId;
     lclear(p, 3);
@@ -663,7 +664,7 @@ struct Lane {
             ln = lerase(p, 0, prev, ln);
             continue;
           }
-          set_slot(s, sid, copy_node(evnode));
+          set_slot(s, sid, copy_event(evr));
           pre_process(p, s);
           int tl = P.thisLast;
           if (returned(tl)) {
@@ -695,7 +696,7 @@ struct Lane {
             ln = lerase(p, 0, prev, ln);
             continue;
           }
-          add_event(s, sid, copy_node(evnode));
+          add_event(s, sid, copy_event(evr));
           setfl(p, F_SUCCESS, false);
           pre_process(p, s);
           int tl = P.thisLast;
@@ -740,7 +741,7 @@ struct Lane {
             ln = lerase(p, 0, prev, ln);
             continue;
           }
-          set_slot(s, sid, copy_node(evnode));
+          set_slot(s, sid, copy_event(evr));
           pre_process(p, s);
           int tl = P.thisLast;
           if (returned(tl)) {
@@ -776,7 +777,7 @@ struct Lane {
             continue;
           }
           int32_t current = slot(s, sid);
-          set_slot(s, sid, copy_node(evnode));
+          set_slot(s, sid, copy_event(evr));
           pre_process(p, s);
           if (P.waitingTime != -1 || (P.sequence && P.ltype == LT_AND && PPOST[P.post].nextEveryPre >= 0))
             set_slot(s, sid, current);
@@ -1117,7 +1118,6 @@ struct Lane {
     time = 0;
     phase = 1;
     sched = -1;
-    int32_t ev = event_node(r);
     int64_t now = r[LaneEv::kNode + 1];
     // stabilizeStates
     if (PQ->kind == 2) {
@@ -1130,7 +1130,7 @@ struct Lane {
     }
     for (int k = 0; k < R->nproc && !err; ++k) {
       int pp = R->procs[k];
-      processAndReturn(pp, ev, now);
+      processAndReturn(pp, r, now);
       if (err) return;
       if (!lempty(pp, 3)) {
         if (!R->hasQuerySelector && !R->multi) {

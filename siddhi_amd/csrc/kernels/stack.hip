@@ -50,8 +50,10 @@ constexpr int kSI = SM_STACK_KSI;  // records per thread per slice
 constexpr int kS = kSB * kSI;      // slice: 4608 records
 constexpr int kLog = 4096;     // match log of a slice: kLog / H entries per key thread ...
 constexpr int kOvf = 1024;     // ... and a shared overflow (more: the batch takes the sort / walk kernels)
-constexpr int kOCap = 12288;   // matches of a tile staged in LDS before one coalesced write
-constexpr int kGT = 16;        // consecutive tiles per order workgroup
+// matches of a tile staged in LDS before one coalesced write (what the tile counts leave of the LDS; none for tiles of
+// 2^15 ordinals, whose direct writes land in a ~190 KB window that the L2 combines)
+constexpr int kOCap = kOT * 4 + 12288 * 8 <= 160 * 1024 ? 12288 : 0;
+constexpr int kGT = kTB >= 15 ? 4 : 16;  // consecutive tiles per order workgroup
 
 static_assert(kBins == kKeys && kKeys == kKPT * kSB && kBins == kOB && (kKPT == 1 || kKPT == 2),
               "one or two in-bucket keys per thread, one bucket per order thread");
@@ -504,7 +506,7 @@ struct OrderArgs {
 // output exceeds the LDS image writes its matches to their places directly.
 __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
   __shared__ uint32_t cnt[kOT];
-  __shared__ uint64_t obuf[kOCap];
+  __shared__ uint64_t obuf[kOCap > 0 ? kOCap : 1];
   __shared__ uint32_t sst[kBins], slen[kBins];
   __shared__ uint32_t lw[kOB / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -563,7 +565,7 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
       }
     }
     lds_barrier();
-    const bool staged = tot <= (uint32_t)kOCap;
+    const bool staged = kOCap > 0 && tot <= (uint32_t)kOCap;
     // pass B: rank of each match among its j's matches = its segment position - the position where its j's run
     // starts (runs may continue from the previous 16-match chunk of the segment)
     auto place = [&](uint64_t v, bool valid, uint32_t c, uint32_t& cj, uint32_t& cstart) {
@@ -857,7 +859,7 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
     }
     const int grid = std::min(kBins, fs.cus);
     sa.spill = (uint4*)sc.take((size_t)grid * kKeys * kQ * 16);
-    static const bool want_stamps = v2 && getenv("SM_STACK_STAMPS") != nullptr;
+    static const bool want_stamps = getenv("SM_STACK_STAMPS") != nullptr;
     static const int dbg = getenv("SM_STACK_DEBUG") ? atoi(getenv("SM_STACK_DEBUG")) : 0;
     sa.dbg = dbg;
     if (want_stamps) {
@@ -917,6 +919,7 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
       a4.spill = sa.spill;
       a4.err = sa.err;
       a4.cold = c4d;
+      a4.stamps = sa.stamps;
       switch (p.op * 2 + (p.fp ? 1 : 0)) {
         case CMP_GT * 2: launch_stack4_t<CMP_GT, false>(a4, grid, s); break;
         case CMP_GT * 2 + 1: launch_stack4_t<CMP_GT, true>(a4, grid, s); break;
@@ -930,7 +933,16 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
       }
     }
     tmark("stack");
-    if (sa.stamps) {
+    if (sa.stamps && !v2) {
+      unsigned long long hst[5];
+      SM_HIP(hipMemcpyAsync(hst, sa.stamps, sizeof(hst), hipMemcpyDeviceToHost, s));
+      SM_HIP(hipStreamSynchronize(s));
+      double tot = 0;
+      for (double v : hst) tot += v;
+      if (tot > 0)
+        fprintf(stderr, "[stack4 phases] rank %.3f stacks %.3f wait %.3f emit %.3f rest %.3f; wave-clocks %.3g\n",
+                hst[0] / tot, hst[1] / tot, hst[2] / tot, hst[3] / tot, hst[4] / tot, tot);
+    } else if (sa.stamps) {
       unsigned long long hst[7], hcn[2];
       SM_HIP(hipMemcpyAsync(hst, sa.stamps, sizeof(hst), hipMemcpyDeviceToHost, s));
       SM_HIP(hipMemcpyAsync(hcn, sa.counts, sizeof(hcn), hipMemcpyDeviceToHost, s));

@@ -15,7 +15,10 @@ constexpr int kKeys = 1024;  // in-bucket keys
 constexpr int kC = SM_STACK_KC;  // stack entries held in registers
 constexpr int kQ = 32;           // spilled entries per thread (HBM ring)
 constexpr int kOB = 1024;        // order workgroup: thread d owns bucket d
-constexpr int kTB = 13;          // order tile: 2^kTB consecutive relative ordinals
+#ifndef SM_ORDER_TB
+#define SM_ORDER_TB 15  // A/B build flag (config 4 order kernel: 13 -> 6.6 ms)
+#endif
+constexpr int kTB = SM_ORDER_TB;  // order tile: 2^kTB consecutive relative ordinals
 constexpr int kOT = 1 << kTB;
 
 enum : uint32_t { SE_OVERFLOW = 1, SE_LOG = 2, SE_NAN = 4, SE_CAND = 8, SE_ORD = 16 };
@@ -127,6 +130,7 @@ __device__ __forceinline__ void st_push(Stack& s, uint4* sp, uint32_t o, uint32_
       s.n = kC - 1;
     } else {
       if (s.hn == kQ) {  // free the ring's dead head first
+#pragma unroll 1
         while (s.hn > 0 && within >= 0 && now - (int32_t)sp[s.hb & (kQ - 1)].z > (int32_t)within) {
           s.hb = (s.hb + 1) & (kQ - 1);
           --s.hn;
@@ -191,10 +195,10 @@ __device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* lw, uint32_
 //   Per event the lane records its pops in the slot: the youngest popped e1 inline (pk, by arrival position), the
 //   count (jc), and further pops in the slot's pool {i, position | k << 16}.
 #ifndef SM_STACK_R
-#define SM_STACK_R 3
+#define SM_STACK_R 2
 #endif
 #ifndef SM_STACK_SS
-#define SM_STACK_SS 2048
+#define SM_STACK_SS 3072
 #endif
 constexpr int kR = SM_STACK_R;    // slices held in LDS
 constexpr int kSS = SM_STACK_SS;  // records per slice
@@ -252,7 +256,25 @@ struct Stack4Args {
   uint4* spill;
   uint32_t* err;
   const Stack4Cold* cold;
+  unsigned long long* stamps;  // SM_STACK4_STAMPS builds: shader clocks per phase, summed over waves
 };
+
+#ifndef SM_STACK4_STAMPS
+#define SM_STACK4_STAMPS 0  // diagnostic build flag: phase clock of stack4_kernel (0 rank, 1 stacks, 2 wait, 3 emit, 4 rest)
+#endif
+#if SM_STACK4_STAMPS && defined(__HIP_DEVICE_COMPILE__)
+#define SM4_CLOCK() __builtin_amdgcn_s_memtime()
+#else
+#define SM4_CLOCK() 0ull
+#endif
+#define SM4_PHASE(i)                              \
+  do {                                            \
+    if (SM_STACK4_STAMPS) {                       \
+      const unsigned long long t_ = SM4_CLOCK();  \
+      st_acc[i] += t_ - st_last;                  \
+      st_last = t_;                               \
+    }                                             \
+  } while (0)
 
 template <int OP, bool FP>
 __device__ SM_EXACT4_INLINE bool c2_exact4(const Stack4Cold* c, uint32_t cs, uint32_t ce, uint32_t oi, uint32_t oj) {
@@ -260,9 +282,12 @@ __device__ SM_EXACT4_INLINE bool c2_exact4(const Stack4Cold* c, uint32_t cs, uin
                             c->o0, cs, ce, oi, oj);
 }
 
+#ifndef SM_RANK4_INLINE
+#define SM_RANK4_INLINE __forceinline__
+#endif
 // rank slice [q0, q0 + sn) of the bucket (records in pre[]) into slot S: key runs (kst), key-grouped {code, ts}
 // and arrival positions | c1, ordinals by arrival position
-__device__ __forceinline__ void rank4(Slot4& S, const uint4 (&pre)[kI4], int sn, uint32_t* lw) {
+__device__ SM_RANK4_INLINE void rank4(Slot4& S, const uint4 (&pre)[kI4], int sn, uint32_t* lw) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint8_t* cnt = (uint8_t*)S.pk;  // [key][wave]
   *(uint4*)(cnt + 16 * tid) = make_uint4(0, 0, 0, 0);
@@ -327,6 +352,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
   const bool has = h < a.H;
   const int32_t within32 = a.within;
   uint4* sp = a.spill + ((int64_t)blockIdx.x * kKeys + h) * kQ;
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st_last = SM4_CLOCK();
 
   for (int d = blockIdx.x; d < kBins; d += gridDim.x) {
     const uint32_t b0 = a.dbase[d];
@@ -370,6 +396,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
     auto slice_n = [&](uint32_t s) { return (int)(blen - s * kSS < (uint32_t)kSS ? blen - s * kSS : (uint32_t)kSS); };
     // the lane's runs in the held slices, relative to the epoch: k = 0 is slice e
     uint32_t off[kR], cnt[kR];
+    SM4_PHASE(4);
     for (uint32_t s = 0; s < (uint32_t)kR; ++s) {
       off[s] = cnt[s] = 0;
       if (s < nsl) {
@@ -382,25 +409,31 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
     }
     if (kR < nsl) load(kR);
 
+    SM4_PHASE(0);
     for (uint32_t e = 0; e < nsl; ++e) {
       const int q0 = (int)(e % kR);
       // ---- stack phase: finish this lane's events of slice e; go on into the later held slices meanwhile
       while (__any(cnt[0] != 0)) {
-        int k = -1;
+        // the lane's next event: its first held slice with events left
+        int k = kR - 1;
 #pragma unroll
-        for (int u = kR - 1; u >= 0; --u)
+        for (int u = kR - 2; u >= 0; --u)
           if (cnt[u]) k = u;
-        if (k < 0) continue;
-        uint32_t o_ = 0;
-        int q = 0;
+        uint32_t o_ = off[kR - 1], c_ = cnt[kR - 1];
+#pragma unroll
+        for (int u = kR - 2; u >= 0; --u)
+          if (u == k) {
+            o_ = off[u];
+            c_ = cnt[u];
+          }
+        if (c_ == 0) continue;  // nothing held for this lane: it waits for the wave
 #pragma unroll
         for (int u = 0; u < kR; ++u)
           if (u == k) {
-            o_ = off[u];
-            off[u] += 1;
-            cnt[u] -= 1;
-            q = q0 + u >= kR ? q0 + u - kR : q0 + u;
+            off[u] = o_ + 1;
+            cnt[u] = c_ - 1;
           }
+        const int q = q0 + k >= kR ? q0 + k - kR : q0 + k;
         Slot4& S = sl[q];
         const uint2 g = S.grp[o_];
         const uint32_t ep = S.epos[o_];
@@ -409,26 +442,28 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
         const int32_t jt = (int32_t)g.y;
         tl = jt;
         seen = true;
+        // a NaN anywhere sends the batch to the sort / walk kernels (SE_NAN), so the codes alone decide here
         if (FP && cj == kNanCode) atomicOr(a.err, SE_NAN);
         uint32_t hit = 0, exp = 0, tie = 0;
 #pragma unroll
         for (int u = 0; u < kC; ++u) {
           const bool lv = u < st.n;
-          const bool x = within32 >= 0 && jt - st.t[u] > within32;
-          const bool t = !a.exact_codes && st.c[u] == cj;
-          const bool nan = FP && ((st.c[u] == kNanCode) | (cj == kNanCode));
           hit |= (lv && cmp_fixed<OP>(cj, st.c[u])) ? (1u << u) : 0u;
-          exp |= (lv && x) ? (1u << u) : 0u;
-          tie |= (lv && (t || nan)) ? (1u << u) : 0u;
+          exp |= (lv && within32 >= 0 && jt - st.t[u] > within32) ? (1u << u) : 0u;
+          tie |= (lv && !a.exact_codes && st.c[u] == cj) ? (1u << u) : 0u;
         }
-        if (tie) {  // equal inexact codes (or NaN): the exact values decide (out of line)
+        if (tie) {  // equal inexact codes: the exact values decide (out of line, one call site)
           const uint32_t oj = S.ordt[p];
+#pragma unroll 1
+          for (uint32_t m = tie; m; m &= m - 1u) {
+            const int u = __builtin_ctz(m);
+            uint32_t oi = st.o[0];
 #pragma unroll
-          for (int u = 0; u < kC; ++u)
-            if ((tie >> u) & 1u) {
-              const bool hh = c2_exact4<OP, FP>(a.cold, cs, ce, st.o[u], oj);
-              hit = hh ? (hit | (1u << u)) : (hit & ~(1u << u));
-            }
+            for (int v = 1; v < kC; ++v)
+              if (v == u) oi = st.o[v];
+            if (c2_exact4<OP, FP>(a.cold, cs, ce, oi, oj)) hit |= 1u << u;
+            else hit &= ~(1u << u);
+          }
         }
         const uint32_t ok = hit & ~exp;
         uint32_t npop = (uint32_t)__builtin_ctz(~ok);  // leading entries popped
@@ -436,72 +471,60 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
         const bool stop_expired = npop < (uint32_t)st.n && ((exp >> npop) & 1u);
         const bool cont = !stop_expired && npop == (uint32_t)st.n && st.hn > 0;
         if (npop) S.pk[p] = st.o[0];
-        if (npop > 1 || cont) {  // further pops go to the slot's pool (each spilled one reserves its own entry)
-          if (npop > 1) {
-            const uint32_t base = atomicAdd(&s_pool[q], npop - 1u);
-            if (base + npop - 1u > (uint32_t)kPool) atomicOr(a.err, SE_LOG);
+        if (npop > 1) {  // further pops go to the slot's pool
+          const uint32_t base = atomicAdd(&s_pool[q], npop - 1u);
+          if (base + npop - 1u > (uint32_t)kPool) atomicOr(a.err, SE_LOG);
 #pragma unroll
-            for (int u = 1; u < kC; ++u)
-              if ((uint32_t)u < npop && base + u - 1u < (uint32_t)kPool)
-                S.pool[base + u - 1u] = make_uint2(st.o[u], p | ((uint32_t)u << 16));
-          }
-          // shift the register part down by npop
-#pragma unroll
-          for (int b = 1; b < kC; b <<= 1)
-            if (npop & b) {
-#pragma unroll
-              for (int u = 0; u < kC; ++u)
-                if (u + b < kC) {
-                  st.o[u] = st.o[u + b];
-                  st.c[u] = st.c[u + b];
-                  st.t[u] = st.t[u + b];
-                }
-            }
-          st.n -= (int)npop;
-          if (cont) {  // ran through the registers: continue into the spill ring (rare)
-            for (;;) {
-              st_refill(st, sp);
-              if (within32 >= 0 && jt - st.t[0] > within32) {
-                st.n = 0;
-                st.hn = 0;
-                break;
-              }
-              const bool nan = FP & ((st.c[0] == kNanCode) | (cj == kNanCode));
-              const bool hh = (!nan & (a.exact_codes | (st.c[0] != cj)))
-                                  ? cmp_fixed<OP>(cj, st.c[0])
-                                  : c2_exact4<OP, FP>(a.cold, cs, ce, st.o[0], S.ordt[p]);
-              if (!hh) break;
-              if (npop == 0) {
-                S.pk[p] = st.o[0];
-              } else {
-                const uint32_t b1 = atomicAdd(&s_pool[q], 1u);
-                if (b1 < (uint32_t)kPool) S.pool[b1] = make_uint2(st.o[0], p | (npop << 16));
-                else atomicOr(a.err, SE_LOG);
-              }
-              ++npop;
-              st_pop(st);
-              if (st.hn == 0) break;
-            }
-          }
-        } else {
-          if (npop) {  // one pop: shift by one
-#pragma unroll
-            for (int u = 0; u + 1 < kC; ++u) {
-              st.o[u] = st.o[u + 1];
-              st.c[u] = st.c[u + 1];
-              st.t[u] = st.t[u + 1];
-            }
-            st.n -= 1;
-          }
+          for (int u = 1; u < kC; ++u)
+            if ((uint32_t)u < npop && base + u - 1u < (uint32_t)kPool)
+              S.pool[base + u - 1u] = make_uint2(st.o[u], p | ((uint32_t)u << 16));
         }
+        // shift the register part down by npop
+#pragma unroll
+        for (int b = 1; b < kC; b <<= 1)
+          if (npop & b) {
+#pragma unroll
+            for (int u = 0; u < kC; ++u)
+              if (u + b < kC) {
+                st.o[u] = st.o[u + b];
+                st.c[u] = st.c[u + b];
+                st.t[u] = st.t[u + b];
+              }
+          }
+        st.n -= (int)npop;
         if (stop_expired) {  // the entry that stopped the run has expired: so has every older one
           st.n = 0;
           st.hn = 0;
+        } else if (cont) {  // ran through the registers: continue into the spill ring (rare)
+#pragma unroll 1
+          for (;;) {
+            st_refill(st, sp);
+            if (within32 >= 0 && jt - st.t[0] > within32) {
+              st.n = 0;
+              st.hn = 0;
+              break;
+            }
+            const bool hh = (a.exact_codes | (st.c[0] != cj)) ? cmp_fixed<OP>(cj, st.c[0])
+                                                               : c2_exact4<OP, FP>(a.cold, cs, ce, st.o[0], S.ordt[p]);
+            if (!hh) break;
+            if (npop == 0) {
+              S.pk[p] = st.o[0];
+            } else {  // each spilled pop reserves its own pool entry
+              const uint32_t b1 = atomicAdd(&s_pool[q], 1u);
+              if (b1 < (uint32_t)kPool) S.pool[b1] = make_uint2(st.o[0], p | (npop << 16));
+              else atomicOr(a.err, SE_LOG);
+            }
+            ++npop;
+            st_pop(st);
+            if (st.hn == 0) break;
+          }
         }
         S.jc[p] = (uint8_t)npop;
         if (ep >> 15) st_push(st, sp, S.ordt[p], cj, jt, jt, within32, a.err);
       }
+      SM4_PHASE(1);
       lds_barrier();  // every lane is done with slice e
+      SM4_PHASE(2);
 
       // ---- slice e's matches, in arrival order of j
       {
@@ -553,6 +576,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
           s_pool[q0] = 0;
         }
       }
+      SM4_PHASE(3);
       // ---- slice e + kR into the freed slot
       off[0] = off[1];
       cnt[0] = cnt[1];
@@ -569,6 +593,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
         cnt[kR - 1] = vv >> 16;
         if (e + kR + 1 < nsl) load(e + kR + 1);  // lands during the next stack phase
       }
+      SM4_PHASE(0);
     }
     // tiles after the bucket's last record start at its end
     __syncthreads();
@@ -627,6 +652,9 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
         if (k < st.n) put(st.o[k], st.t[k]);
     }
   }
+  SM4_PHASE(4);
+  if (SM_STACK4_STAMPS && a.stamps && lane == 0)
+    for (int i = 0; i < 5; ++i) atomicAdd(&a.stamps[i], st_acc[i]);
 }
 
 }  // namespace
