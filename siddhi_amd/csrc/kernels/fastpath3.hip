@@ -137,6 +137,8 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
       if (p < hi0) {
         if (kcol) kk[k] = __builtin_nontemporal_load(kcol + p);
         if (TS) tt[k] = __builtin_nontemporal_load(ts + p);
+        // TS = false: the pairs that straddle 64-element items (pass 0 checks the rest with wave shuffles)
+        if (!TS && lane == 0 && p > 0 && ts[p] < ts[p - 1]) bad = 1;
         if (ord) oo[k] = ord[p];
         if (vlong) vv[k] = vlong[p];
         if (lane == 0 && p > 0) {  // the element before each wave-item (other lanes take it from lane - 1)
@@ -406,7 +408,7 @@ struct OrigSrc {
   struct Raw {
     KT k;
     VT v;
-    int64_t t, tp, o;
+    int64_t t, o;
     uint64_t m;
   };
   __device__ Raw load(int64_t p) const {
@@ -414,13 +416,18 @@ struct OrigSrc {
     r.k = kcol[p];
     r.v = vcol[p];
     r.t = ts[p];
-    r.tp = bad_ts && p > 0 ? ts[p - 1] : r.t;  // the previous element: same or adjacent line, an L1 hit
     r.o = ord ? ord[p] - obase : p;
     r.m = c1_inline ? 0ull : c1mask[p >> 6];
     return r;
   }
-  __device__ void split(const Raw& r, int64_t p, uint64_t& a, uint64_t& b) {
-    if (r.t < r.tp) bad = true;
+  // event time against the previous element, inside a wave-item of 64 consecutive elements (every lane, once per
+  // item; prep checked the pairs that straddle items)
+  __device__ void check(const Raw& r, bool valid) {
+    if (!bad_ts) return;
+    const int64_t prev = __shfl_up(r.t, 1, 64);
+    if (valid && (threadIdx.x & 63) != 0 && r.t < prev) bad = true;
+  }
+  __device__ void split(const Raw& r, int64_t p, uint64_t& a, uint64_t& b) const {
     const uint32_t c1 = c1_bit(r.v, r.m, p);
     a = (uint64_t)((uint32_t)((int64_t)r.k - kmin) | (c1 << 31)) | ((uint64_t)(uint32_t)r.o << 32);
     b = (uint64_t)vcode<VT>(r.v, vmode, vmin) | ((uint64_t)(uint32_t)(r.t - ts0) << 32);
@@ -431,6 +438,8 @@ struct RecSrc {
   const uint4* r;
   __device__ void init() {}
   __device__ void flush() {}
+  template <typename R>
+  __device__ void check(const R&, bool) {}
   typedef unsigned int Raw __attribute__((ext_vector_type(4)));
   // read-once stream: nontemporal loads keep the L2 for the scattered stores (PMC: -10 % pass time)
   __device__ uint4 rec(int64_t p) const {
@@ -448,6 +457,8 @@ struct PairSrc {  // (j << 32) | i
   const uint64_t* q;
   __device__ void init() {}
   __device__ void flush() {}
+  template <typename R>
+  __device__ void check(const R&, bool) {}
   using Raw = uint64_t;
   __device__ Raw load(int64_t p) const { return __builtin_nontemporal_load(q + p); }
   __device__ void split(const Raw& v, int64_t, uint64_t& a, uint64_t&) const { a = v; }
@@ -674,6 +685,7 @@ downsweep_wc_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dp
 #pragma unroll
     for (int k = 0; k < kWcItems; ++k) {
       const int e = w * 64 * kWcItems + k * 64 + lane;
+      src.check(raw[k], e < tile_n);
       if (e < tile_n) src.split(raw[k], base + e, a[k], b[k]);
     }
     lds_barrier();  // previous tile's readers of wcnt / xb64 / run / tstart are done

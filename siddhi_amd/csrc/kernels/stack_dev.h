@@ -16,7 +16,7 @@ constexpr int kC = SM_STACK_KC;  // stack entries held in registers
 constexpr int kQ = 32;           // spilled entries per thread (HBM ring)
 constexpr int kOB = 1024;        // order workgroup: thread d owns bucket d
 #ifndef SM_ORDER_TB
-#define SM_ORDER_TB 15  // A/B build flag (config 4 order kernel: 13 -> 6.6 ms)
+#define SM_ORDER_TB 13  // A/B build flag (config 4 order kernel: 13 -> 6.65 ms, 15 (direct writes) -> 9.8 ms)
 #endif
 constexpr int kTB = SM_ORDER_TB;  // order tile: 2^kTB consecutive relative ordinals
 constexpr int kOT = 1 << kTB;
@@ -259,6 +259,9 @@ struct Stack4Args {
   unsigned long long* stamps;  // SM_STACK4_STAMPS builds: shader clocks per phase, summed over waves
 };
 
+#ifndef SM_STACK4_SKIP
+#define SM_STACK4_SKIP 0  // diagnostic build flag: 1 = no event loop (every pop count 0; wrong results, timing only)
+#endif
 #ifndef SM_STACK4_STAMPS
 #define SM_STACK4_STAMPS 0  // diagnostic build flag: phase clock of stack4_kernel (0 rank, 1 stacks, 2 wait, 3 emit, 4 rest)
 #endif
@@ -287,17 +290,20 @@ __device__ SM_EXACT4_INLINE bool c2_exact4(const Stack4Cold* c, uint32_t cs, uin
 #endif
 // rank slice [q0, q0 + sn) of the bucket (records in pre[]) into slot S: key runs (kst), key-grouped {code, ts}
 // and arrival positions | c1, ordinals by arrival position
-__device__ SM_RANK4_INLINE void rank4(Slot4& S, const uint4 (&pre)[kI4], int sn, uint32_t* lw) {
+__device__ SM_RANK4_INLINE void rank4(Slot4& S, const uint4 (&pre)[kI4], int sn, uint32_t* lw, bool fp,
+                                       uint32_t* err) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint8_t* cnt = (uint8_t*)S.pk;  // [key][wave]
   *(uint4*)(cnt + 16 * tid) = make_uint4(0, 0, 0, 0);
   lds_barrier();
   const uint64_t lt = lanemask_lt();
   uint32_t hk[kI4], lp[kI4];
+  bool nan = false;
 #pragma unroll
   for (int k = 0; k < kI4; ++k) {
     const int e = w * 64 * kI4 + k * 64 + lane;
     const bool valid = e < sn;
+    nan |= fp && valid && pre[k].z == kNanCode;  // a NaN sends the batch to the sort / walk kernels (SE_NAN)
     hk[k] = valid ? (pre[k].x & kKeyMask) >> kRB : 0u;
     const uint64_t peers = peer_mask(hk[k], valid);
     uint32_t old = 0;
@@ -308,6 +314,7 @@ __device__ SM_RANK4_INLINE void rank4(Slot4& S, const uint4 (&pre)[kI4], int sn,
     wave_lockstep();
     lp[k] = old + below;
   }
+  if (__any(nan) && lane == 0) atomicOr(err, SE_NAN);
   lds_barrier();
   {  // key h = tid: its count over the waves, block scan over keys
     const uint4 c = *(const uint4*)(cnt + 16 * tid);
@@ -336,6 +343,7 @@ __device__ SM_RANK4_INLINE void rank4(Slot4& S, const uint4 (&pre)[kI4], int sn,
       S.grp[pos] = make_uint2(pre[k].z, pre[k].w);
       S.epos[pos] = (uint16_t)((uint32_t)e | ((pre[k].x >> 31) << 15));
       S.ordt[e] = pre[k].y;
+      if (SM_STACK4_SKIP) S.jc[e] = 0;
     }
   }
   lds_barrier();
@@ -401,7 +409,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
       off[s] = cnt[s] = 0;
       if (s < nsl) {
         load(s);
-        rank4(sl[s], pre, slice_n(s), lw);
+        rank4(sl[s], pre, slice_n(s), lw, FP, a.err);
         const uint32_t v = sl[s].kst[h];
         off[s] = v & 0xffffu;
         cnt[s] = v >> 16;
@@ -413,7 +421,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
     for (uint32_t e = 0; e < nsl; ++e) {
       const int q0 = (int)(e % kR);
       // ---- stack phase: finish this lane's events of slice e; go on into the later held slices meanwhile
-      while (__any(cnt[0] != 0)) {
+      while (!SM_STACK4_SKIP && __any(cnt[0] != 0)) {
         // the lane's next event: its first held slice with events left
         int k = kR - 1;
 #pragma unroll
@@ -426,7 +434,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
             o_ = off[u];
             c_ = cnt[u];
           }
-        if (c_ == 0) continue;  // nothing held for this lane: it waits for the wave
+        if (c_ != 0) {  // else nothing is held for this lane: it waits for the wave
 #pragma unroll
         for (int u = 0; u < kR; ++u)
           if (u == k) {
@@ -442,8 +450,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
         const int32_t jt = (int32_t)g.y;
         tl = jt;
         seen = true;
-        // a NaN anywhere sends the batch to the sort / walk kernels (SE_NAN), so the codes alone decide here
-        if (FP && cj == kNanCode) atomicOr(a.err, SE_NAN);
+        // a NaN anywhere sent the batch to the sort / walk kernels (rank4: SE_NAN), so the codes alone decide here
         uint32_t hit = 0, exp = 0, tie = 0;
 #pragma unroll
         for (int u = 0; u < kC; ++u) {
@@ -521,6 +528,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
         }
         S.jc[p] = (uint8_t)npop;
         if (ep >> 15) st_push(st, sp, S.ordt[p], cj, jt, jt, within32, a.err);
+        }
       }
       SM4_PHASE(1);
       lds_barrier();  // every lane is done with slice e
@@ -587,7 +595,7 @@ __global__ void __launch_bounds__(kT4) stack4_kernel(Stack4Args a) {
       }
       off[kR - 1] = cnt[kR - 1] = 0;
       if (e + kR < nsl) {
-        rank4(sl[q0], pre, slice_n(e + kR), lw);
+        rank4(sl[q0], pre, slice_n(e + kR), lw, FP, a.err);
         const uint32_t vv = sl[q0].kst[h];
         off[kR - 1] = vv & 0xffffu;
         cnt[kR - 1] = vv >> 16;
