@@ -545,9 +545,9 @@ KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j
 
 def alg_bytes(label, n, m, config):
     keyed = config == 4
-    return {"prep": (4 * n) if keyed else (16 * n + n // 8),  # keyed: key i32 (c1 = price > 20 and the event-time
-                                                             # order are evaluated in pass 0); unkeyed: ts +
-                                                             # price in, c1 bit out
+    return {"prep": (12 * n) if keyed else (16 * n + n // 8),  # keyed: key i32 + ts i64 (c1 = price > 20 is
+                                                              # evaluated in pass 0); unkeyed: ts + price in,
+                                                              # c1 bit out
             "key_up": 16 * n,               # pass-1 digits: one 16-B record per event (the key word of each)
             "scan": 0,                      # per-chunk digit counts (O(chunks x 1024), not per event)
             "key_pass0": 20 * n + 16 * n,   # key i32 + price f64 + ts i64 in, 16-B keyed record out

@@ -109,9 +109,7 @@ __device__ unsigned long long sm_stamps[16];
 //   * per-chunk counts of the pass-0 digit. Keys are rebased by kmin rounded down to a multiple of kBins, so
 //     the low digit of the rebased key is the low digit of the key itself and needs no kmin yet.
 // Tiles of kTile events (kItems per thread, every load of the tile issued before any is used).
-// TS = false: event time is not read here (keyed batches on the write-combining pass 0, which checks the order of
-// event time on the loads it makes anyway); ts0 / ts_last are single reads.
-template <typename KT, bool MASK, bool TS>
+template <typename KT, bool MASK>
 __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kcol, const int64_t* __restrict__ vlong,
                                                       const int64_t* __restrict__ ts, const int64_t* __restrict__ ord,
                                                       int64_t obase, int64_t n, int64_t per, int G,
@@ -136,13 +134,11 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
       const int64_t p = base + w * 64 * kItems + k * 64 + lane;
       if (p < hi0) {
         if (kcol) kk[k] = __builtin_nontemporal_load(kcol + p);
-        if (TS) tt[k] = __builtin_nontemporal_load(ts + p);
-        // TS = false: the pairs that straddle 64-element items (pass 0 checks the rest with wave shuffles)
-        if (!TS && lane == 0 && p > 0 && ts[p] < ts[p - 1]) bad = 1;
+        tt[k] = __builtin_nontemporal_load(ts + p);
         if (ord) oo[k] = ord[p];
         if (vlong) vv[k] = vlong[p];
         if (lane == 0 && p > 0) {  // the element before each wave-item (other lanes take it from lane - 1)
-          if (TS) tp[k] = ts[p - 1];
+          tp[k] = ts[p - 1];
           if (ord) op[k] = ord[p - 1];
         }
       }
@@ -151,11 +147,9 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
     for (int k = 0; k < kItems; ++k) {
       const int64_t p = base + w * 64 * kItems + k * 64 + lane;
       const bool in = p < hi0;
-      if (TS) {
-        int64_t pt = __shfl_up(tt[k], 1, 64);
-        if (lane == 0) pt = p > 0 ? tp[k] : tt[k];
-        if (in && tt[k] < pt) bad = 1;
-      }
+      int64_t pt = __shfl_up(tt[k], 1, 64);
+      if (lane == 0) pt = p > 0 ? tp[k] : tt[k];
+      if (in && tt[k] < pt) bad = 1;
       if (ord) {
         int64_t po = __shfl_up(oo[k], 1, 64);
         if (lane == 0) po = p > 0 ? op[k] : oo[k] - 1;
@@ -380,15 +374,9 @@ struct OrigSrc {
   int c1len;
   const DVal* consts;
   bool c1_inline;
-  unsigned int* bad_ts;  // non-null: check that event time does not decrease (prep did not), flag it here
   Cond c1;
-  bool bad;
   __device__ void init() {
     if (c1_inline) c1 = make_cond(c1code, c1len, consts);
-    bad = false;
-  }
-  __device__ void flush() {  // every lane of the workgroup, once at the end
-    if (bad_ts && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(bad_ts, 1u);
   }
   __device__ uint32_t c1_bit(VT v, uint64_t m, int64_t p) const {
     if (c1_inline) return eval_simple(c1, ValLoader<VT>{v}) ? 1u : 0u;
@@ -420,13 +408,6 @@ struct OrigSrc {
     r.m = c1_inline ? 0ull : c1mask[p >> 6];
     return r;
   }
-  // event time against the previous element, inside a wave-item of 64 consecutive elements (every lane, once per
-  // item; prep checked the pairs that straddle items)
-  __device__ void check(const Raw& r, bool valid) {
-    if (!bad_ts) return;
-    const int64_t prev = __shfl_up(r.t, 1, 64);
-    if (valid && (threadIdx.x & 63) != 0 && r.t < prev) bad = true;
-  }
   __device__ void split(const Raw& r, int64_t p, uint64_t& a, uint64_t& b) const {
     const uint32_t c1 = c1_bit(r.v, r.m, p);
     a = (uint64_t)((uint32_t)((int64_t)r.k - kmin) | (c1 << 31)) | ((uint64_t)(uint32_t)r.o << 32);
@@ -437,9 +418,6 @@ struct OrigSrc {
 struct RecSrc {
   const uint4* r;
   __device__ void init() {}
-  __device__ void flush() {}
-  template <typename R>
-  __device__ void check(const R&, bool) {}
   typedef unsigned int Raw __attribute__((ext_vector_type(4)));
   // read-once stream: nontemporal loads keep the L2 for the scattered stores (PMC: -10 % pass time)
   __device__ uint4 rec(int64_t p) const {
@@ -456,9 +434,6 @@ struct RecSrc {
 struct PairSrc {  // (j << 32) | i
   const uint64_t* q;
   __device__ void init() {}
-  __device__ void flush() {}
-  template <typename R>
-  __device__ void check(const R&, bool) {}
   using Raw = uint64_t;
   __device__ Raw load(int64_t p) const { return __builtin_nontemporal_load(q + p); }
   __device__ void split(const Raw& v, int64_t, uint64_t& a, uint64_t&) const { a = v; }
@@ -617,7 +592,6 @@ downsweep_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dpair
       if (threadIdx.x * kBinsPerThread + bb < kBins) run[threadIdx.x * kBinsPerThread + bb] += cnt_t[bb];
     SM_STAMP(6);
   }
-  src.flush();
   SM_STAMP_FLUSH;
 }
 
@@ -685,7 +659,6 @@ downsweep_wc_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dp
 #pragma unroll
     for (int k = 0; k < kWcItems; ++k) {
       const int e = w * 64 * kWcItems + k * 64 + lane;
-      src.check(raw[k], e < tile_n);
       if (e < tile_n) src.split(raw[k], base + e, a[k], b[k]);
     }
     lds_barrier();  // previous tile's readers of wcnt / xb64 / run / tstart are done
@@ -851,7 +824,6 @@ downsweep_wc_kernel(Src src, uint4* __restrict__ drec, uint64_t* __restrict__ dp
     }
     SM_STAMP(6);
   }
-  src.flush();
   SM_STAMP_FLUSH;
 }
 
@@ -1296,9 +1268,9 @@ bool c1_inline(const FastHostInfo& hi, const FastArgs& a) {
 template <typename KT, typename VT>
 void launch_down0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int vmode, int64_t vmin,
                     const uint64_t* c1mask, int64_t ts0, int G, int64_t per, hipStream_t s, uint4* dst,
-                    const uint32_t* cnt, const uint32_t* dbase, unsigned int* bad_ts) {
+                    const uint32_t* cnt, const uint32_t* dbase) {
   OrigSrc<KT, VT> os{a.st, (const KT*)kcol, (const VT*)hi.cols[hi.vattr], kmin, vmode, vmin, c1mask, a.ts, ts0,
-                     a.ordinals, a.ordinal_base, a.code + a.c1_off, a.c1_len, a.consts, c1_inline(hi, a), bad_ts};
+                     a.ordinals, a.ordinal_base, a.code + a.c1_off, a.c1_len, a.consts, c1_inline(hi, a)};
   if (sort_wc())
     hipLaunchKernelGGL((downsweep_wc_kernel<0, OrigSrc<KT, VT>>), dim3(G), dim3(kWcBlock), 0, s, os, dst, nullptr, a.n,
                        per, nullptr, G, 0, cnt, dbase);
@@ -1310,20 +1282,12 @@ void launch_down0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol,
 template <typename KT>
 void launch_down0_k(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int vmode, int64_t vmin,
                     const uint64_t* m, int64_t ts0, int G, int64_t per, hipStream_t s, uint4* dst,
-                    const uint32_t* cnt, const uint32_t* dbase, unsigned int* bad_ts) {
+                    const uint32_t* cnt, const uint32_t* dbase) {
   switch (hi.vtype) {
-    case T_INT:
-      launch_down0_t<KT, int32_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase, bad_ts);
-      break;
-    case T_LONG:
-      launch_down0_t<KT, int64_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase, bad_ts);
-      break;
-    case T_FLOAT:
-      launch_down0_t<KT, float>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase, bad_ts);
-      break;
-    case T_DOUBLE:
-      launch_down0_t<KT, double>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase, bad_ts);
-      break;
+    case T_INT: launch_down0_t<KT, int32_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_LONG: launch_down0_t<KT, int64_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_FLOAT: launch_down0_t<KT, float>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_DOUBLE: launch_down0_t<KT, double>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
     default: throw std::runtime_error("fast path: unsupported compared-attribute type");
   }
 }
@@ -1582,25 +1546,18 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     tmark("scan");
   };
 
-  // column facts + c1 mask + pass-0 digit counts, one pass. Keyed batches without explicit ordinals on the
-  // write-combining pass 0 leave the event-time order check to pass 0 (its own loads), so prep reads the key column
-  // only (and the c1 / LONG attribute columns when needed)
+  // column facts + c1 mask + pass-0 digit counts, one pass
   const bool mask = !keyed || !c1_inline(hi, a);
-  const bool ts_in_pass0 = keyed && !a.ordinals && sort_wc();
-#define SM_PREP(KT, M, T)                                                                                           \
-  hipLaunchKernelGGL((prep_kernel<KT, M, T>), dim3(G), dim3(kBlock), 0, s, (const KT*)kcol, vlong, a.ts, a.ordinals, \
+#define SM_PREP(KT, M)                                                                                              \
+  hipLaunchKernelGGL((prep_kernel<KT, M>), dim3(G), dim3(kBlock), 0, s, (const KT*)kcol, vlong, a.ts, a.ordinals,    \
                      a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt, c)
-#define SM_PREP_M(KT, T)  \
-  if (mask) SM_PREP(KT, true, T); \
-  else SM_PREP(KT, false, T)
   if (hi.key_type == T_LONG && keyed) {
-    if (ts_in_pass0) { SM_PREP_M(int64_t, false); }
-    else { SM_PREP_M(int64_t, true); }
+    if (mask) SM_PREP(int64_t, true);
+    else SM_PREP(int64_t, false);
   } else {
-    if (ts_in_pass0) { SM_PREP_M(int32_t, false); }
-    else { SM_PREP_M(int32_t, true); }
+    if (mask) SM_PREP(int32_t, true);
+    else SM_PREP(int32_t, false);
   }
-#undef SM_PREP_M
 #undef SM_PREP
   tmark("prep");
   Ctrl hc;
@@ -1685,20 +1642,10 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     uint4* B = (uint4*)sc.take(n * 16);
     // key pass 0 from the original columns (its digit counts came from prep)
     scan_counts(G);
-    unsigned int* bad_ts = ts_in_pass0 ? &c->bad_ts : nullptr;
     if (hi.key_type == T_INT)
-      launch_down0_k<int32_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase, bad_ts);
-    else launch_down0_k<int64_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase, bad_ts);
+      launch_down0_k<int32_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
+    else launch_down0_k<int64_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
     tmark("key_pass0");
-    if (ts_in_pass0 && a.within >= 0) {  // the event-time order check prep left to pass 0
-      unsigned int bt = 0;
-      SM_HIP(hipMemcpyAsync(&bt, &c->bad_ts, sizeof(bt), hipMemcpyDeviceToHost, s));
-      SM_HIP(hipStreamSynchronize(s));
-      if (bt) {
-        sc.used = mark;
-        return FAST_NON_MONOTONE;
-      }
-    }
     // bucket-stack pipeline when the per-bucket keys fill a workgroup (stack.hip); it falls back here otherwise
     const int H = (int)std::min<uint64_t>(kspan >> kRB, 1ull << 20) + 1;
     const bool order_op = spec >= 0 && (spec >> 1) != CMP_EQ && (spec >> 1) != CMP_NE;
