@@ -34,6 +34,7 @@
 #include "expr.h"
 #include "fastpath.h"
 #include "fastpath_dev.h"
+#include "pass0_dev.h"
 
 namespace sm {
 
@@ -413,6 +414,12 @@ struct OrigSrc {
     a = (uint64_t)((uint32_t)((int64_t)r.k - kmin) | (c1 << 31)) | ((uint64_t)(uint32_t)r.o << 32);
     b = (uint64_t)vcode<VT>(r.v, vmode, vmin) | ((uint64_t)(uint32_t)(r.t - ts0) << 32);
   }
+  __device__ uint4 record(const Raw& r, int64_t p) const {  // pass0_kernel (pass0_dev.h)
+    const uint32_t c1 = c1_bit(r.v, r.m, p);
+    return make_uint4((uint32_t)((int64_t)r.k - kmin) | (c1 << 31), (uint32_t)r.o, vcode<VT>(r.v, vmode, vmin),
+                      (uint32_t)(r.t - ts0));
+  }
+  __device__ void flush() {}
 };
 
 struct RecSrc {
@@ -1271,7 +1278,10 @@ void launch_down0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol,
                     const uint32_t* cnt, const uint32_t* dbase) {
   OrigSrc<KT, VT> os{a.st, (const KT*)kcol, (const VT*)hi.cols[hi.vattr], kmin, vmode, vmin, c1mask, a.ts, ts0,
                      a.ordinals, a.ordinal_base, a.code + a.c1_off, a.c1_len, a.consts, c1_inline(hi, a)};
-  if (sort_wc())
+  static const bool p0v2 = !(getenv("SM_PASS0_V2") && getenv("SM_PASS0_V2")[0] == '0');
+  if (sort_wc() && p0v2)  // pass0_dev.h (A/B: SM_PASS0_V2=0 runs the generic write-combining down-sweep)
+    hipLaunchKernelGGL((pass0_kernel<OrigSrc<KT, VT>>), dim3(G), dim3(kP0Block), 0, s, os, dst, a.n, per, G, cnt, dbase);
+  else if (sort_wc())
     hipLaunchKernelGGL((downsweep_wc_kernel<0, OrigSrc<KT, VT>>), dim3(G), dim3(kWcBlock), 0, s, os, dst, nullptr, a.n,
                        per, nullptr, G, 0, cnt, dbase);
   else

@@ -7,10 +7,11 @@ import re
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in sorted(glob.glob("gpurun_out/pmc_*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        m = re.search(r"(walk_kernel<\w+>|onesweep_kernel<\d|prep_kernel|key_hist|u32_hist|hist_scan|filter_\w+_kernel)",
+        m = re.search(r"(walk_kernel<\w+>|onesweep_kernel<\d|prep_kernel|key_hist|u32_hist|hist_scan|filter_\w+_kernel|pass0_kernel|downsweep_wc_kernel<\d|stack4_kernel|order_kernel)",
                       r["Kernel_Name"])
         if m:
             agg[m.group(1)][r["Counter_Name"]] += float(r["Counter_Value"])
+            agg[m.group(1)]["rows:" + r["Counter_Name"]] += 1
 for k, d in agg.items():
     print(k)
     waves = d.get("SQ_WAVES", 0)
