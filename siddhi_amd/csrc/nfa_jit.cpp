@@ -93,11 +93,15 @@ std::string blob_array(const std::vector<char>& blob) {
 
 std::string nfa_jit_source(const std::vector<char>& blob, bool lds) {
   std::string src = kPrelude;
-  // Occupancy: room for 3 waves per SIMD (170 VGPRs). Measured on config 5 (N = 1e8, heap_words 1024, NFA kernel
+  // Occupancy: room for 2 waves per SIMD (256 VGPRs). Measured on config 5 (N = 1e8, heap_words 1024, NFA kernel
   // ms): interpreter 74.3; JIT with the compiler's choice (268 VGPRs, 1 wave) 74.9, 2 waves 65.5, 4 waves 63.5;
-  // with every event-path function inline, 4 waves 64.4, 3 waves 60.6. A/B: SM_NFA_JIT_WAVES=<n> (0 = no hint).
+  // with every event-path function inline, 4 waves 64.4, 3 waves 60.6. Round 3 (LDS-staged key state, no event
+  // copies; config 5 plan): 3 waves = 168 VGPRs + 405 spilled (528 B of scratch per lane, 1e6 lanes: the spills
+  // reach HBM, and under rocprofv3 the kernel ran 27 ms against 18 ms), 2 waves = 256 VGPRs + 32 spilled (144 B),
+  // 1 wave = 288 with no scratch; NFA kernel 19.1 / 18.1 / 19.2 ms, 4 waves 20.4 ms. Default 2.
+  // A/B: SM_NFA_JIT_WAVES=<n> (0 = no hint).
   const char* w = getenv("SM_NFA_JIT_WAVES");
-  const int waves = w ? atoi(w) : 3;
+  const int waves = w ? atoi(w) : 2;
   if (waves > 0)
     src += "#define SM_NFA_JIT_ATTR __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))\n";
   else
