@@ -101,7 +101,12 @@ struct StateLoader {  // OP_VAR loads for a run record
 // flags, timer queues: fixed offsets) then share cache lines instead of each pulling its own line.
 // stride 1 = the plain key-major layout (the heap).
 #ifdef SM_COUNT_ACCESS
-extern int64_t g_access[2];
+// [0] key-state word accesses, [1] heap word accesses, [2] words allocated, [3] words copied by collections
+// (gc + promote), [4] collections, [5] events delivered, [6] run records allocated, [7] chain nodes allocated
+extern int64_t g_access[8];
+#define SM_COUNT(i, v) (::sm::g_access[i] += (v))
+#else
+#define SM_COUNT(i, v) ((void)0)
 #endif
 struct LaneWords {
   int64_t* p;      // &base[lane]
@@ -164,6 +169,7 @@ struct Lane {
       return 2 * half;  // dummy region (writes harmless; lane aborts at the next safe point)
     }
     misc(1) = bump + words;
+    SM_COUNT(2, words);
     return (int32_t)bump;
   }
   __device__ int kind_of(int32_t o) const { return (int)(heap[o] & 0xFF); }
@@ -184,6 +190,7 @@ struct Lane {
   }
   SM_JIT_INL __device__ int32_t new_rec() {
     int32_t r = alloc(PQ->rec_words);
+    SM_COUNT(6, 1);
     heap[r] = K_REC;
     heap[r + 1] = -1;  // StateEvent.timestamp = -1
     for (int k = 2; k < PQ->rec_words; ++k) heap[r + k] = -1;  // all slots null (two -1 halves)
@@ -192,6 +199,7 @@ struct Lane {
   // StateEventCloner.copyStateEvent :46-57 (shallow)
   SM_JIT_INL __device__ int32_t copy_rec(int32_t src) {
     int32_t r = alloc(PQ->rec_words);
+    SM_COUNT(6, 1);
     for (int k = 0; k < PQ->rec_words; ++k) heap[r + k] = heap[src + k];
     return r;
   }
@@ -202,12 +210,14 @@ struct Lane {
   __device__ int64_t nord(int32_t n) const { return heap[n + 2]; }
   SM_INL_SMALL __device__ int32_t copy_node(int32_t src) {  // StreamEventCloner.copyStreamEvent: next = null
     int32_t n = alloc(PQ->node_words);
+    SM_COUNT(7, 1);
     for (int k = 1; k < PQ->node_words; ++k) heap[n + k] = heap[src + k];
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
     return n;
   }
   SM_JIT_INL __device__ int32_t empty_node() {  // streamEventPool.borrowEvent(): ts -1, null data
     int32_t n = alloc(PQ->node_words);
+    SM_COUNT(7, 1);
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
     heap[n + 1] = -1;
     heap[n + 2] = -1;
@@ -220,6 +230,7 @@ struct Lane {
   // in processAndReturn is such a copy, so an event no pending partial takes allocates nothing.
   SM_INL_SMALL __device__ int32_t copy_event(const int64_t* __restrict__ r) {
     int32_t n = alloc(PQ->node_words);
+    SM_COUNT(7, 1);
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
     for (int w = 1; w < PQ->node_words; ++w) heap[n + w] = r[LaneEv::kNode + w];
     return n;
@@ -998,6 +1009,7 @@ struct Lane {
     if (k == K_FWD) return hi(o);
     int words = (k == K_REC) ? PQ->rec_words : (k == K_NODE) ? PQ->node_words : 2;
     int32_t n = (int32_t)top;
+    SM_COUNT(3, words);
     for (int w = 0; w < words; ++w) heap[n + w] = heap[o + w];
     top += words;
     heap[o] = K_FWD | ((int64_t)(uint32_t)n << 32);
@@ -1015,6 +1027,7 @@ struct Lane {
     if (k == K_FWD) return (int32_t)(h0 >> 32);
     const int words = (k == K_REC) ? PQ->rec_words : (k == K_NODE) ? PQ->node_words : 2;
     const int32_t n = (int32_t)top;
+    SM_COUNT(3, words);
     for (int w = 0; w < words; ++w) dst[n + w] = heap[o + w];
     top += words;
     heap[o] = K_FWD | ((int64_t)(uint32_t)n << 32);
@@ -1069,6 +1082,7 @@ struct Lane {
   }
   __device__ void gc() {
     int64_t space = misc(2);
+    SM_COUNT(4, 1);
     int64_t to = (1 - space) * half;
     int64_t top = to, scan = to;
     for (int p = 0; p < PQ->npre; ++p)
@@ -1114,6 +1128,7 @@ struct Lane {
     for (int k = 0; k < PQ->nrecv; ++k)
       if (PRECV[k].stream == s) R = &PRECV[k];
     if (!R) return;
+    SM_COUNT(5, 1);
     pos = p;
     time = 0;
     phase = 1;
@@ -1412,10 +1427,21 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
   // Walk this key's events; before each, fire timers due at clock-advance points (playback) in order.
   int64_t k = ebeg;
   int64_t search_from = 0;  // advance-point index
+#ifndef SM_NFA_NO_PREFETCH
+  // the next event's record line is requested while this event is processed: its position word is loaded one
+  // iteration ahead, so the line is in cache when the next iteration reads the rest of the record (without it every
+  // event starts with a dependent HBM round trip)
+  int64_t pf_pos = (k < eend) ? b.lane_ev[k * W + LaneEv::kPos] : INT64_MAX;
+#endif
   for (;;) {
     // this key's events are consecutive LaneEv records (key order): one contiguous read per event
     const int64_t* __restrict__ r = b.lane_ev + k * W;
+#ifndef SM_NFA_NO_PREFETCH
+    const int64_t next_pos = pf_pos;
+    pf_pos = (k + 1 < eend) ? r[W + LaneEv::kPos] : INT64_MAX;
+#else
     const int64_t next_pos = (k < eend) ? r[LaneEv::kPos] : INT64_MAX;
+#endif
     if (has_timers) {
       for (;;) {
         if (L.err) break;

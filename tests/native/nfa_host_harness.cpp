@@ -55,7 +55,7 @@ struct HApp {
   std::vector<int64_t> ev_row, ev_ts, ev_clock, ev_ord, adv_pos, adv_clock, adv_wall;
   int64_t next_ord = 0;
   int64_t base = 0, clock = 0, clock_in = 0;
-  int32_t heap_half = 1024;
+  int32_t heap_half = getenv("SM_HOST_HEAP_HALF") ? atoi(getenv("SM_HOST_HEAP_HALF")) : 1024;
   bool started = false;
   std::map<std::string, std::vector<std::string>> so, qo;
   std::string err;
@@ -329,12 +329,11 @@ void flush(HApp* a) {
 #ifdef SM_COUNT_ACCESS
 namespace sm {
 namespace {
-int64_t g_access[2];
+int64_t g_access[8];
 }
 }  // namespace sm
 extern "C" void h_access(int64_t* out) {
-  out[0] = sm::g_access[0];
-  out[1] = sm::g_access[1];
+  for (int i = 0; i < 8; ++i) out[i] = sm::g_access[i];
 }
 #endif
 
