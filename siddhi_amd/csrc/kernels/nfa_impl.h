@@ -1427,21 +1427,10 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
   // Walk this key's events; before each, fire timers due at clock-advance points (playback) in order.
   int64_t k = ebeg;
   int64_t search_from = 0;  // advance-point index
-#ifndef SM_NFA_NO_PREFETCH
-  // the next event's record line is requested while this event is processed: its position word is loaded one
-  // iteration ahead, so the line is in cache when the next iteration reads the rest of the record (without it every
-  // event starts with a dependent HBM round trip)
-  int64_t pf_pos = (k < eend) ? b.lane_ev[k * W + LaneEv::kPos] : INT64_MAX;
-#endif
   for (;;) {
     // this key's events are consecutive LaneEv records (key order): one contiguous read per event
     const int64_t* __restrict__ r = b.lane_ev + k * W;
-#ifndef SM_NFA_NO_PREFETCH
-    const int64_t next_pos = pf_pos;
-    pf_pos = (k + 1 < eend) ? r[W + LaneEv::kPos] : INT64_MAX;
-#else
     const int64_t next_pos = (k < eend) ? r[LaneEv::kPos] : INT64_MAX;
-#endif
     if (has_timers) {
       for (;;) {
         if (L.err) break;

@@ -1,5 +1,6 @@
 #!/bin/bash
-# SQ counters of the config-4 stack kernel (full size, one step), two passes; CSVs under gpurun_out/sq_<i>/.
+# SQ counters of one kernel (KRE, default the config-4 stack kernel; SQ_ARGS: the bench arguments, default config 4 at
+# full size), one step, two passes; CSVs under gpurun_out/sq_<i>/.
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
 cd /tmp
@@ -9,7 +10,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   i=$((i+1))
   echo "== pass $i: $grp"
   rm -rf "$ROOT/gpurun_out/sq_$i"
-  timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-stack_kernel}" --output-format csv -d "$ROOT/gpurun_out/sq_$i" -o run -- python3 "$ROOT/bench.py" --no-cpu --no-e2e --events ${PMC_EVENTS:-1e9} --steps 1 --warmup 0 > "$ROOT/gpurun_out/sq_$i.log" 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-stack_kernel}" --output-format csv -d "$ROOT/gpurun_out/sq_$i" -o run -- python3 "$ROOT/bench.py" --no-cpu ${SQ_ARGS:---no-e2e --events 1e9} --steps 1 --warmup 0 > "$ROOT/gpurun_out/sq_$i.log" 2>&1
   rc=$?
   echo "rc=$rc"
   [ $rc -ne 0 ] && tail -5 "$ROOT/gpurun_out/sq_$i.log" && exit $rc
