@@ -18,6 +18,8 @@
  *                                   PartitionStreamReceiver.java:156): route each event to its key's owner rank
  *   sm_merge_heartbeats             multi-GPU playback: the global clock advances (StreamJunction.sendData :232)
  *                                   replayed as heartbeats among a rank's received events
+ *   sm_unpack_records               multi-GPU receive side of the key exchange: packed records -> columns + global
+ *                                   ordinals (no reference counterpart: one JVM has no exchange)
  *   sm_order_matches                multi-GPU merge of the per-rank outputs back into the single output order a
  *                                   query callback sees (QueryCallback.receive, query/output/callback/
  *                                   QueryCallback.java:51): no Java counterpart, one JVM has one output queue
@@ -169,6 +171,17 @@ int sm_app_restore(sm_app* app, const uint8_t* buf, size_t len);
 int sm_partition_by_owner(const void* d_keys, int key_width, size_t n, uint32_t world, int ncols,
                           const int32_t* widths, const int32_t* strides, const void* const* d_src,
                           void* const* d_dst, uint64_t* counts, void* hip_stream);
+/* Receive side of the key exchange (siddhi_amd/shard.py exchange_with_ordinals): m packed records of rec_bytes
+ * (8..64, a multiple of 8) as the RCCL all-to-all-v delivered them (runs per source rank, in rank order) split into
+ * contiguous columns in one pass: field c (offsets[c] bytes into the record, widths[c] = 1, 2, 4 or 8) goes to
+ * d_dst[c] (NULL entry or d_dst NULL: not copied). ord_field >= 0 names the 4-byte field holding each record's
+ * offset inside its source rank's ingest slice; d_ordinals[i] then = src_first[source of i] + that offset (the
+ * global arrival ordinal of the unsharded stream), the source runs given by run_counts (host, nsrc <= 64 entries
+ * adding up to m). Replaces the reference's single-JVM junction hand-off (StreamJunction.sendData), which has no
+ * exchange; the received columns feed sm_app_process_device_batch / _events with d_ordinals. */
+int sm_unpack_records(const void* d_rec, size_t m, int rec_bytes, int ncols, const int32_t* offsets,
+                      const int32_t* widths, void* const* d_dst, int ord_field, int nsrc, const uint64_t* run_counts,
+                      const int64_t* src_first, int64_t* d_ordinals, void* hip_stream);
 /* Receive side of the multi-GPU match return: n match pairs (e2 << 32) | uint32(e1) of global ordinals, every e2
  * in [lo, hi) (this rank's ingest slice), given as the concatenation of per-source runs each in reference order
  * (e2, then e1; one e2's matches all in one run) → d_out (n entries, not aliasing d_pairs) in the reference's

@@ -22,6 +22,7 @@ EXPORTS = [
     "sm_app_set_option", "sm_app_process_device_batch", "sm_app_process_device_events", "sm_app_device_matches",
     "sm_app_snapshot", "sm_app_restore", "sm_partition_by_owner", "sm_order_matches", "sm_app_copy_device_matches",
     "sm_app_get_stat", "sm_compile_dump", "sm_nfa_jit_compile", "sm_app_device_project", "sm_merge_heartbeats",
+    "sm_unpack_records",
 ]
 
 
@@ -74,6 +75,9 @@ def lib():
                                             ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                             ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64), vp]
         L.sm_order_matches.argtypes = [vp, sz, i64, i64, vp, vp]
+        L.sm_unpack_records.argtypes = [vp, sz, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64), vp, vp]
         L.sm_merge_heartbeats.argtypes = [sz, vp, vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
                                           ctypes.POINTER(vp), sz, vp, vp, vp, vp, vp, ctypes.POINTER(vp),
                                           ctypes.POINTER(sz), vp]

@@ -888,6 +888,13 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
   __shared__ uint32_t wtot[kWalkWaves];
   __shared__ uint32_t jh[kBins];
   __shared__ uint32_t sh_run;
+  // unkeyed ordered compare (`e2.x OP e1.x`, OP one of < <= > >=): per block of kSkipBlk staged records the value
+  // that would satisfy c2 for the most e1 (max for > / >=, min for < / <=, NaN excluded), so a scan can step over a
+  // whole block none of whose records can match (event time is non-decreasing: a block that holds the window's end
+  // and no match ends the scan like the first record after it)
+  constexpr bool kSkip = !KEYED && (OP == CMP_LT || OP == CMP_LE || OP == CMP_GT || OP == CMP_GE);
+  constexpr int kSkipBlk = 16;
+  __shared__ uint64_t bx[kSkip ? kWalkLds / kSkipBlk : 1];
 
   const int64_t n = a.n;
   int64_t lo, len;
@@ -940,6 +947,27 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
       }
     }
     lds_barrier();
+    if constexpr (kSkip) {
+      for (int b = threadIdx.x; b < nload / kSkipBlk; b += kWalkBlock) {
+        constexpr bool kMax = OP == CMP_GT || OP == CMP_GE;
+        if constexpr (FP) {
+          double x = kMax ? -__builtin_inf() : __builtin_inf();
+          for (int e = 0; e < kSkipBlk; ++e) {
+            const double y = __longlong_as_double((long long)L.v[b * kSkipBlk + e]);
+            if (kMax ? y > x : y < x) x = y;  // NaN never replaces (and never matches)
+          }
+          bx[b] = (uint64_t)__double_as_longlong(x);
+        } else {
+          int64_t x = kMax ? INT64_MIN : INT64_MAX;
+          for (int e = 0; e < kSkipBlk; ++e) {
+            const int64_t y = (int64_t)L.v[b * kSkipBlk + e];
+            if (kMax ? y > x : y < x) x = y;
+          }
+          bx[b] = (uint64_t)x;
+        }
+      }
+      lds_barrier();
+    }
     SM_STAMP(1);
     const int lend = nload;  // staged positions are [0, lend) relative to base
     uint32_t c1m = 0;        // c1 of each item (bit k)
@@ -957,7 +985,7 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
     // predicated take): every live lane advances its scan by one record per iteration.
     uint32_t hasm = 0, openm = 0, pendm = 0;  // matched / scan left the staged records / key's events ran out
     uint32_t todo = c1m;
-    int k = 0, v = 0;
+    int k = 0, v = 0, steps = 0;
     uint64_t vu = 0;
     int64_t tu = 0;
     uint32_t key = 0, cu = 0, ou = 0;
@@ -980,13 +1008,17 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
       }
       v = lu + 1;
       vstart = v;
+      steps = 0;
     };
     SM_STAMP(2);
     take();
     while (__any(live)) {
       // unkeyed scans run until c2 holds or the window closes (up to window-many events: no key run bounds them),
       // so a lane scans privately for kUnkeyedBudget records and leaves the rest to the wave-cooperative finish
-      const bool inb = v < lend && (KEYED || v - vstart < kUnkeyedBudget);
+      const bool inb = v < lend && (KEYED || (kSkip ? steps : v - vstart) < kUnkeyedBudget);
+      // a whole block without a possible match: step over it (its window end, if any, is seen at the next record)
+      bool skip = false;
+      if constexpr (kSkip) skip = live && inb && (v % kSkipBlk) == 0 && v + kSkipBlk <= lend && !c2(vu, bx[v / kSkipBlk]);
       const int vv = inb ? v : lend - 1;
       bool stop, hit, kchg = false;
       if constexpr (KEYED) {
@@ -1002,8 +1034,8 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
           if (ex) hit = cc.exact(ou, r.y);
       } else {
         const int64_t d = L.t[vv] - tu;
-        stop = !inb || (a.within >= 0 && (d < 0 ? -d : d) > a.within);
-        hit = live && !stop && c2(vu, L.v[vv]);
+        stop = !skip && (!inb || (a.within >= 0 && (d < 0 ? -d : d) > a.within));
+        hit = live && !skip && !stop && c2(vu, L.v[vv]);
       }
       const bool open = live && !inb && base + v < n;  // leaves the staged records: finished from global below
       const bool pend = live && (kchg || (!inb && base + v >= n));  // the key's events (or the batch) ran out
@@ -1012,7 +1044,8 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
       pendm |= pend ? (1u << k) : 0u;
       if (hit || open) sj[k][threadIdx.x] = (uint32_t)v;
       const bool done = live && (stop || hit);
-      ++v;
+      v += skip ? kSkipBlk : 1;
+      ++steps;
       if (done) take();
     }
     SM_STAMP(3);

@@ -57,4 +57,23 @@ struct MergeOut {
 int64_t merge_heartbeats(const int64_t* ord, const int32_t* sid, const int64_t* ts, int64_t n, const int64_t* tord,
                          const int64_t* tts, int64_t m, const MergeOut& o, Scratch& sc, hipStream_t s);
 
+// Receive side of the key exchange: the packed records the all-to-all-v delivered (m records of rec_words 8-byte
+// words, runs per source rank in rank order) split into contiguous columns in ONE pass, and the field holding each
+// record's uint32 offset inside its source's ingest slice turned into the int64 global ordinal
+// (src_first[source] + offset). Replaces one strided copy per column plus the ordinal arithmetic.
+struct UnpackCols {
+  int32_t n;                     // fields
+  int32_t rec_words;             // record size in 8-byte words (<= 8)
+  int32_t off[kMaxPartCols];     // byte offset of each field in the record
+  int32_t width[kMaxPartCols];   // 1, 2, 4 or 8
+  void* dst[kMaxPartCols];       // contiguous output column (nullptr: not copied)
+  int32_t ord_field;             // field with the in-slice uint32 offset (-1: none)
+  int32_t nsrc;                  // source ranks (runs), <= kMaxOwners
+  int64_t run_end[kMaxOwners];   // exclusive end of each source's run in the received buffer
+  int64_t src_first[kMaxOwners]; // first global ordinal of each source's ingest slice
+  int64_t* ord_out;
+};
+
+void unpack_records(const uint64_t* rec, int64_t m, const UnpackCols& u, hipStream_t s);
+
 }  // namespace sm

@@ -234,4 +234,47 @@ void partition_by_owner(const void* keys, int key_width, int64_t n, uint32_t wor
   else throw std::invalid_argument("partition keys must be 4- or 8-byte integers");
 }
 
+namespace {
+// one thread per record: its words are loaded once (the wave's loads cover consecutive records, so every line is
+// used whole), each field goes to its column with a coalesced store
+__global__ void __launch_bounds__(256) unpack_records_kernel(const uint64_t* __restrict__ rec, int64_t m,
+                                                             UnpackCols u) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  uint64_t w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (k < u.rec_words) w[k] = rec[i * u.rec_words + k];
+  for (int c = 0; c < u.n; ++c) {
+    const int o = u.off[c], wd = u.width[c];
+    uint64_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k == (o >> 3)) x = w[k];
+    x >>= (o & 7) * 8;
+    if (c == u.ord_field) {
+      // source run of record i (runs in rank order): its slice's first ordinal + the in-slice offset
+      int lo = 0, hi = u.nsrc - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (i < u.run_end[mid]) hi = mid;
+        else lo = mid + 1;
+      }
+      u.ord_out[i] = u.src_first[lo] + (int64_t)(uint32_t)x;
+    }
+    void* d = u.dst[c];
+    if (!d) continue;
+    if (wd == 8) ((uint64_t*)d)[i] = x;
+    else if (wd == 4) ((uint32_t*)d)[i] = (uint32_t)x;
+    else if (wd == 2) ((uint16_t*)d)[i] = (uint16_t)x;
+    else ((uint8_t*)d)[i] = (uint8_t)x;
+  }
+}
+}  // namespace
+
+void unpack_records(const uint64_t* rec, int64_t m, const UnpackCols& u, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(unpack_records_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, rec, m, u);
+}
+
 }  // namespace sm

@@ -118,6 +118,10 @@ __global__ __launch_bounds__(kRsThreads) void rs_upsweep(const K* __restrict__ k
   hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }
 
+// Stable scatter of one 4096-item tile by its digit. Ranks within (wave, digit) come from ballot peer masks; the
+// tile is then regrouped in LDS by digit (digit-major, arrival order within a digit) and leaves as contiguous digit
+// runs, so consecutive lanes store consecutive addresses (about 16 items of 4 + 4 bytes per run at 256 digits):
+// one or two lines per run instead of one line touched per lane and store instruction.
 template <typename K>
 __global__ __launch_bounds__(kRsThreads) void rs_downsweep(const K* __restrict__ kin, K* __restrict__ kout,
                                                            const uint32_t* __restrict__ vin,
@@ -127,11 +131,16 @@ __global__ __launch_bounds__(kRsThreads) void rs_downsweep(const K* __restrict__
   __shared__ uint32_t wcount[4][256];
   __shared__ uint32_t wbase[4][256];
   __shared__ uint32_t gbase[256];
+  __shared__ uint32_t tstart[256];
+  __shared__ uint32_t wsum[4];
+  __shared__ K lkey[kRsTile];
+  __shared__ uint32_t lval[kRsTile];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int k = 0; k < 4; ++k) wcount[k][threadIdx.x] = 0;
   __syncthreads();
   const uint32_t dmask = (1u << bits) - 1;
-  const size_t wbeg = (size_t)blockIdx.x * kRsTile + (size_t)w * kRsWaveTile;
+  const size_t tbeg = (size_t)blockIdx.x * kRsTile;
+  const size_t wbeg = tbeg + (size_t)w * kRsWaveTile;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   K key[kRsItems];
   uint32_t val[kRsItems];
@@ -157,21 +166,42 @@ __global__ __launch_bounds__(kRsThreads) void rs_downsweep(const K* __restrict__
   }
   __syncthreads();
   {
+    // digit threadIdx.x: its items before each wave, its tile start (block scan of the tile's digit counts)
     uint32_t acc = 0;
     for (int k = 0; k < 4; ++k) {
       wbase[k][threadIdx.x] = acc;
       acc += wcount[k][threadIdx.x];
     }
     gbase[threadIdx.x] = hist[(size_t)threadIdx.x * nblocks + blockIdx.x];
+    uint32_t inc = acc;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    tstart[threadIdx.x] = off + inc - acc;
   }
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < kRsItems; ++it) {
     if (lrank[it] == 0xffffffffu) continue;
-    uint32_t d = (uint32_t)(key[it] >> shift) & dmask;
-    size_t dest = (size_t)gbase[d] + wbase[w][d] + lrank[it];
-    kout[dest] = key[it];
-    if (vout) vout[dest] = val[it];
+    const uint32_t d = (uint32_t)(key[it] >> shift) & dmask;
+    const uint32_t slot = tstart[d] + wbase[w][d] + lrank[it];
+    lkey[slot] = key[it];
+    lval[slot] = val[it];
+  }
+  __syncthreads();
+  const uint32_t tn = n - tbeg < (size_t)kRsTile ? (uint32_t)(n - tbeg) : (uint32_t)kRsTile;
+#pragma unroll 4
+  for (uint32_t sl = threadIdx.x; sl < tn; sl += kRsThreads) {
+    const K k = lkey[sl];
+    const uint32_t d = (uint32_t)(k >> shift) & dmask;
+    const size_t dest = (size_t)gbase[d] + (sl - tstart[d]);
+    kout[dest] = k;
+    if (vout) vout[dest] = lval[sl];
   }
 }
 

@@ -242,66 +242,59 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
-// partition key per selected record; invalid (null key / other stream) → valid = 0
-__global__ void key_eval_kernel(const int64_t* __restrict__ pos, int64_t n, const int32_t* __restrict__ ev_stream,
-                                const int64_t* __restrict__ ev_row, const NfaStream* __restrict__ streams,
-                                const KeyProg* __restrict__ progs, int nprogs, int64_t* __restrict__ keys,
-                                uint8_t* __restrict__ valid) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int64_t p = pos ? pos[i] : i;  // no pos: the query keeps every batch record
-  int s = ev_stream[p];
-  keys[i] = 0;
-  valid[i] = 0;
-  for (int k = 0; k < nprogs; ++k) {
-    if (progs[k].stream != s) continue;
-    ColLoader ld{&streams[s], ev_row[p]};
-    StackVal v = eval_prog(progs[k].code, progs[k].len, progs[k].consts, ld);
-    if (v.null) return;
-    int64_t key;
-    if (progs[k].type == T_FLOAT || progs[k].type == T_DOUBLE) {
-      double d = v.d;
-      if (d != d) d = __longlong_as_double(0x7ff8000000000000ll);  // String.valueOf(NaN) == "NaN" for every NaN
-      key = __double_as_longlong(d);
-    } else {
-      key = v.i;
-    }
-    keys[i] = key;
-    valid[i] = 1;
-    return;
-  }
-}
-
-// Grid-stride lookup; misses are counted per workgroup and added once per workgroup (a batch of new keys
-// misses on every record, and atomics on one address serialise in the L2 even when a wave coalesces them).
-__global__ __launch_bounds__(256) void table_lookup_kernel(const int64_t* __restrict__ keys,
-                                                           const uint8_t* __restrict__ valid, int64_t n,
-                                                           const int64_t* __restrict__ tkeys,
-                                                           const int32_t* __restrict__ tslots, uint64_t mask,
-                                                           int32_t* __restrict__ slot_out,
-                                                           uint32_t* __restrict__ nmissing) {
+// Key evaluation and key-table lookup in one pass (group_by_key): each record's partition key, then its slot (-1: not in the
+// table, -2: null key / other stream). A key that is one column (the common `partition with (symbol of S)`) is
+// loaded directly instead of through the expression evaluator's operand stack. Misses are counted per workgroup.
+__global__ __launch_bounds__(256) void key_lookup_kernel(const int64_t* __restrict__ pos, int64_t n,
+                                                         const int32_t* __restrict__ ev_stream,
+                                                         const int64_t* __restrict__ ev_row,
+                                                         const NfaStream* __restrict__ streams,
+                                                         const KeyProg* __restrict__ progs, int nprogs,
+                                                         const int64_t* __restrict__ tkeys,
+                                                         const int32_t* __restrict__ tslots, uint64_t mask, bool empty,
+                                                         int64_t* __restrict__ keys, int32_t* __restrict__ slot_out,
+                                                         uint32_t* __restrict__ nmissing) {
   __shared__ uint32_t wmiss[4];
   uint32_t miss = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (valid && !valid[i]) {
-      slot_out[i] = -2;
-      continue;
-    }
-    int64_t k = keys[i];
-    uint64_t h = mix64((uint64_t)k) & mask;
-    for (;;) {
-      int32_t s = tslots[h];
-      if (s == 0) {
-        slot_out[i] = -1;
-        ++miss;
-        break;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int64_t p = pos ? pos[i] : i;  // no pos: the query keeps every batch record
+    const int s = ev_stream[p];
+    int32_t slot = -2;
+    int64_t key = 0;
+    for (int k = 0; k < nprogs; ++k) {
+      if (progs[k].stream != s) continue;
+      ColLoader ld{&streams[s], ev_row[p]};
+      const Instr i0 = progs[k].code[0];
+      const StackVal v = (progs[k].len == 1 && (i0.op == OP_VAR || i0.op == OP_COL))
+                             ? ld.var(i0)
+                             : eval_prog(progs[k].code, progs[k].len, progs[k].consts, ld);
+      if (v.null) break;
+      if (progs[k].type == T_FLOAT || progs[k].type == T_DOUBLE) {
+        double d = v.d;
+        if (d != d) d = __longlong_as_double(0x7ff8000000000000ll);  // String.valueOf(NaN) == "NaN" for every NaN
+        key = __double_as_longlong(d);
+      } else {
+        key = v.i;
       }
-      if (tkeys[h] == k) {
-        slot_out[i] = s - 1;
-        break;
+      slot = -1;
+      if (!empty) {
+        uint64_t h = mix64((uint64_t)key) & mask;
+        for (;;) {
+          const int32_t t = tslots[h];
+          if (t == 0) break;
+          if (tkeys[h] == key) {
+            slot = t - 1;
+            break;
+          }
+          h = (h + 1) & mask;
+        }
       }
-      h = (h + 1) & mask;
+      break;
     }
+    keys[i] = key;
+    slot_out[i] = slot;
+    miss = slot == -1;
   }
   for (int o = 32; o > 0; o >>= 1) miss += __shfl_xor(miss, o, 64);
   if ((threadIdx.x & 63) == 0) wmiss[threadIdx.x >> 6] = miss;
@@ -737,17 +730,13 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
                      const NfaStream* streams_dev, const KeyProg* progs_dev, int nprogs, int64_t** key_pos_out,
                      int64_t** key_off_out, Scratch& sc, hipStream_t s, bool pos_identity) {
   int64_t* keys = (int64_t*)sc.take(std::max<int64_t>(n, 1) * 8);
-  uint8_t* valid = (uint8_t*)sc.take(std::max<int64_t>(n, 1));
   int32_t* slot = (int32_t*)sc.take(std::max<int64_t>(n, 1) * 4);
   uint32_t* nmiss = (uint32_t*)sc.take(4);
-  if (n > 0)
-    hipLaunchKernelGGL(key_eval_kernel, grid_for(n), dim3(256), 0, s, pos_identity ? nullptr : pos, n, ev_stream, ev_row, streams_dev, progs_dev,
-                       nprogs, keys, valid);
   SM_HIP(hipMemsetAsync(nmiss, 0, 4, s));
   if (n > 0)
-    hipLaunchKernelGGL(table_lookup_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
-                       keys, valid, n, T.tkeys, T.tslots, T.mask,
-                       slot, nmiss);
+    hipLaunchKernelGGL(key_lookup_kernel, grid_for(n), dim3(256), 0, s, pos_identity ? nullptr : pos, n, ev_stream,
+                       ev_row, streams_dev, progs_dev, nprogs, T.tkeys, T.tslots, T.mask, T.nslots == 0, keys, slot,
+                       nmiss);
   uint32_t hm = 0;
   SM_HIP(hipMemcpyAsync(&hm, nmiss, 4, hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));

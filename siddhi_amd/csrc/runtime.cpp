@@ -1193,7 +1193,7 @@ struct EvHost {
   std::vector<int64_t>*row, *ts, *clock, *ord, *adv_pos, *adv_clock, *adv_wall;
 };
 
-// Key code (the int64 the key table hashes: key_eval_kernel) of a row's key column, false if it is null.
+// Key code (the int64 the key table hashes: key_lookup_kernel) of a row's key column, false if it is null.
 bool host_key_code(const StreamStage& st, int col, int64_t row, int64_t* code) {
   if (st.any_null[col] && st.nulls[col][row]) return false;
   const uint8_t* b = st.cols[col].data();
@@ -2643,6 +2643,46 @@ int sm_merge_heartbeats(size_t n, const int64_t* d_ord, const int32_t* d_sid, co
     HelperLock lk{h};
     *n_out = (size_t)sm::merge_heartbeats(d_ord, d_sid, d_ts, (int64_t)n, d_tick_ord, d_tick_ts, (int64_t)m, o, h.sc,
                                           (hipStream_t)hip_stream);
+  });
+}
+
+int sm_unpack_records(const void* d_rec, size_t m, int rec_bytes, int ncols, const int32_t* offsets,
+                      const int32_t* widths, void* const* d_dst, int ord_field, int nsrc, const uint64_t* run_counts,
+                      const int64_t* src_first, int64_t* d_ordinals, void* hip_stream) {
+  return guarded([&] {
+    if (ncols < 0 || ncols > sm::kMaxPartCols) throw std::invalid_argument("ncols out of range");
+    if (rec_bytes <= 0 || rec_bytes > 64 || rec_bytes % 8) throw std::invalid_argument("record size must be 8..64 bytes, a multiple of 8");
+    if ((uintptr_t)d_rec % 8) throw std::invalid_argument("record buffer not 8-byte aligned");
+    sm::UnpackCols u{};
+    u.n = ncols;
+    u.rec_words = rec_bytes / 8;
+    for (int c = 0; c < ncols; ++c) {
+      if (widths[c] != 1 && widths[c] != 2 && widths[c] != 4 && widths[c] != 8)
+        throw std::invalid_argument("field width must be 1, 2, 4 or 8 bytes");
+      if (offsets[c] < 0 || offsets[c] + widths[c] > rec_bytes || offsets[c] % widths[c])
+        throw std::invalid_argument("field outside the record or not aligned to its width");
+      u.off[c] = offsets[c];
+      u.width[c] = widths[c];
+      u.dst[c] = d_dst ? d_dst[c] : nullptr;
+    }
+    u.ord_field = -1;
+    if (ord_field >= 0) {
+      if (ord_field >= ncols || widths[ord_field] != 4) throw std::invalid_argument("ordinal field must be a 4-byte field");
+      if (nsrc <= 0 || nsrc > sm::kMaxOwners || !run_counts || !src_first || !d_ordinals)
+        throw std::invalid_argument("ordinal field needs 1..64 source runs, their first ordinals and an output");
+      uint64_t end = 0;
+      for (int r = 0; r < nsrc; ++r) {
+        end += run_counts[r];
+        u.run_end[r] = (int64_t)end;
+        u.src_first[r] = src_first[r];
+      }
+      if (end != m) throw std::invalid_argument("source run counts do not add up to the record count");
+      u.ord_field = ord_field;
+      u.nsrc = nsrc;
+      u.ord_out = d_ordinals;
+    }
+    sm::unpack_records((const uint64_t*)d_rec, (int64_t)m, u, (hipStream_t)hip_stream);
+    SM_HIP(hipGetLastError());
   });
 }
 

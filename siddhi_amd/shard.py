@@ -140,7 +140,37 @@ def _all_to_all_counts(send_counts, device, group):
     return rc.tolist()
 
 
-def exchange_by_key(keys: torch.Tensor, columns, world: int, group=None):
+def unpack_with_ordinals(rec: torch.Tensor, lay, dtypes, rc, starts):
+    """Received packed records → contiguous columns (all but the last field) + int64 global ordinals from the last
+    field (the uint32 offset inside the source rank's slice) and the sources' first ordinals `starts`, the runs given
+    by the received counts `rc`. GPU: one pass of the native library (sm_unpack_records); host tensors: unpack +
+    torch arithmetic (the same values)."""
+    m = rec.shape[0]
+    if rec.is_cuda:
+        import ctypes
+        from siddhi_amd import _lib
+        R = rec.shape[1] * 8
+        k = len(lay)
+        outs = [torch.empty(m, dtype=dt, device=rec.device) for dt in dtypes[:-1]]
+        ords = torch.empty(m, dtype=torch.int64, device=rec.device)
+        offs = (ctypes.c_int32 * k)(*[o for o, _ in lay])
+        wids = (ctypes.c_int32 * k)(*[w for _, w in lay])
+        dst = (ctypes.c_void_p * k)(*([t.data_ptr() for t in outs] + [None]))
+        cnt = (ctypes.c_uint64 * len(rc))(*[int(x) for x in rc])
+        first = (ctypes.c_int64 * len(rc))(*[int(x) for x in starts])
+        stream = ctypes.c_void_p(torch.cuda.current_stream(rec.device).cuda_stream)
+        r = _lib.lib().sm_unpack_records(rec.data_ptr(), m, R, k, offs, wids, dst, k - 1, len(rc), cnt, first,
+                                         ords.data_ptr(), stream)
+        if r != _lib.SM_OK:
+            raise RuntimeError(_lib.lib().sm_last_error().decode(errors="replace"))
+        return outs, ords
+    cols = unpack(rec, lay, dtypes)
+    base = torch.repeat_interleave(torch.tensor(starts, dtype=torch.int64, device=rec.device),
+                                   torch.tensor(rc, dtype=torch.int64, device=rec.device))
+    return cols[:-1], base + (cols[-1].to(torch.int64) & 0xFFFFFFFF)
+
+
+def exchange_by_key(keys: torch.Tensor, columns, world: int, group=None, packed=False):
     """All-to-all-v of `columns` (list of 1-D tensors aligned with `keys`) so that each rank receives the rows
     whose key it owns, as ONE packed record per row through ONE collective. Returns (received columns, received
     counts per source rank). Row order in the result: by source rank, then original order — i.e. global arrival
@@ -152,6 +182,8 @@ def exchange_by_key(keys: torch.Tensor, columns, world: int, group=None):
     rc = _all_to_all_counts(sc, keys.device, group)
     buf = torch.empty((sum(rc), rec.shape[1]), dtype=torch.int64, device=keys.device)
     dist.all_to_all_single(buf, rec, rc, sc, group=group)
+    if packed:  # the caller unpacks (exchange_with_ordinals: one pass with the ordinals)
+        return (buf, lay), rc
     return unpack(buf, lay, [c.dtype for c in columns]), rc
 
 
@@ -175,12 +207,12 @@ def exchange_with_ordinals(keys: torch.Tensor, columns, world: int, lo: int, gro
     if n >= 2**31:
         raise ValueError("exchange_with_ordinals: more than 2^31 events in one rank's slice")
     off = offsets if offsets is not None else torch.arange(n, dtype=torch.int32, device=keys.device)
-    out, rc = exchange_by_key(keys, list(columns) + [off], world, group=group)
+    cols = list(columns) + [off]
+    (buf, lay), rc = exchange_by_key(keys, cols, world, group=group, packed=True)
     if starts is None:
         starts = slice_starts(lo, world, keys.device, group)
-    base = torch.repeat_interleave(torch.tensor(starts, dtype=torch.int64, device=keys.device),
-                                   torch.tensor(rc, dtype=torch.int64, device=keys.device))
-    return out[:-1], base + out[-1].to(torch.int64), rc
+    out, ords = unpack_with_ordinals(buf, lay, [c.dtype for c in cols], rc, starts)
+    return out, ords, rc
 
 
 def pack_pairs(e1: torch.Tensor, e2: torch.Tensor) -> torch.Tensor:

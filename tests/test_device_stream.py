@@ -95,6 +95,28 @@ def test_unpartitioned_split_batches(splits):
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize("c2", ["price > e1.price", "e1.price <= price", "price < e1.price", "price <= e1.price",
+                                "price == e1.price"])
+@pytest.mark.parametrize("kind", ["double_ties", "double_special", "float", "int", "long_wide"])
+def test_unpartitioned_ordered_compares(c2, kind):
+    """Unkeyed walk (config 3 shape) for every ordered compare and value kind (ties, NaN, -0.0, infinities): the
+    scans step over 16-record blocks whose extreme value cannot satisfy c2; windows of 1000 / 4000 events, so long
+    scans, block skips across the window end and scans past the staged records all occur."""
+    n = 30000
+    rng = np.random.default_rng(abs(hash((c2, kind))) % (1 << 32))
+    vt, price = value_column(kind, n, rng)
+    sym = rng.integers(0, 10, n).astype(np.int32)
+    vol = rng.integers(0, 2000, n).astype(np.int64)
+    tsa = np.arange(n, dtype=np.int64)
+    for within, div in ((" within 1 sec", 1), (" within 4 sec", 1), ("", 1)):
+        text = (f"define stream StockStream (symbol int, price {vt}, volume long, timestamp long); "
+                + Q.format(c1="", c2=c2, within=within))
+        cols = [sym, price, vol, tsa]
+        exp = oracle_pairs(text, cols, tsa // div)
+        got = run_stream(text, cols, tsa // div, pieces(n, [1, 8191, 3333]), expect_path=2)
+        np.testing.assert_array_equal(got, exp)
+
+
 @pytest.mark.parametrize("stack", [1, 2])
 @pytest.mark.parametrize("variant", ["no_within", "c2_ge", "c2_lt", "c2_le", "c1_and", "long_keys"])
 def test_split_variants(stack, variant):

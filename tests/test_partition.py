@@ -4,7 +4,8 @@ keys, ragged sizes and 1/2/4/8-byte columns; the packed-record form and the matc
 import pytest
 import torch
 
-from siddhi_amd.shard import owner_of, pack_by_owner, partition_by_owner, order_matches, pack_pairs, unpack
+from siddhi_amd.shard import (owner_of, pack_by_owner, partition_by_owner, order_matches, pack_pairs, unpack,
+                              unpack_with_ordinals)
 
 pytestmark = pytest.mark.gpu
 
@@ -84,3 +85,24 @@ def test_merge_heartbeats_hip_equals_torch(n, m, overlap):
     for a, b in zip([got[0], got[1], got[3]] + got[2], [want[0], want[1], want[3]] + want[2]):
         assert torch.equal(a.cpu(), b)
     assert got[0].numel() == n + tord.numel() - torch.isin(tord, ords).sum().item()
+
+
+@pytest.mark.parametrize("n,world", [(1, 1), (1000, 3), (300_001, 8), (70_000, 64)])
+def test_unpack_with_ordinals_hip_equals_torch(n, world):
+    """sm_unpack_records (one pass over the received packed records: columns + global ordinals) against the torch
+    unpack + ordinal arithmetic of the same records, on records packed by the partition kernel."""
+    d = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(n + world)
+    sym = torch.randint(-2**31, 2**31 - 1, (n,), generator=g, dtype=torch.int64).to(torch.int32).to(d)
+    price = torch.rand(n, generator=g, dtype=torch.float64).to(d)
+    ts = torch.randint(0, 2**40, (n,), generator=g, dtype=torch.int64).to(d)
+    off = torch.randint(0, 2**32 - 1, (n,), generator=g, dtype=torch.int64).to(torch.int32).to(d)
+    cols = [sym, price, ts, off]
+    rec, counts, lay = pack_by_owner(sym, cols, world)
+    starts = [int(x) for x in torch.randint(0, 2**50, (world,), generator=g, dtype=torch.int64)]
+    got_cols, got_ord = unpack_with_ordinals(rec, lay, [c.dtype for c in cols], counts, starts)
+    exp = unpack(rec, lay, [c.dtype for c in cols])
+    for a, b in zip(got_cols, exp[:-1]):
+        assert torch.equal(a, b)
+    base = torch.repeat_interleave(torch.tensor(starts, dtype=torch.int64), torch.tensor(counts, dtype=torch.int64))
+    assert torch.equal(got_ord.cpu(), base + exp[-1].cpu().to(torch.int64) % 2**32)

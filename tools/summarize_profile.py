@@ -35,8 +35,8 @@ FAMILIES = [("walk_kernel<", "walk"), ("downsweep_wc_kernel<0", "key_pass0"), ("
             ("nfa_kernel", "nfa"), ("sm_nfa_jit", "nfa"), ("lane_events16_kernel", "nfa_setup"),
             ("event_index_kernel", "event_index"), ("ts_tile_max_kernel", "event_index"),
             ("tile_prefix_max_kernel", "event_index"), ("advance_points_kernel", "event_index"), ("advance_rank_kernel", "event_index"),
-            ("select_records_kernel", "nfa_select"), ("select_mask_kernel", "nfa_select"), ("key_eval_kernel", "nfa_group"),
-            ("table_lookup_kernel", "nfa_group"), ("rs_upsweep", "nfa_group"), ("rs_downsweep", "nfa_group"),
+            ("select_records_kernel", "nfa_select"), ("select_mask_kernel", "nfa_select"), ("key_lookup_kernel", "nfa_group"),
+            ("rs_upsweep", "nfa_group"), ("rs_downsweep", "nfa_group"),
             ("all_new_csr_kernel", "nfa_group"), ("lane_events_kernel", "nfa_setup"),
             ("lane_index_kernel", "nfa_setup")]
 
