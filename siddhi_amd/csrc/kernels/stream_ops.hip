@@ -256,8 +256,9 @@ __global__ __launch_bounds__(256) void key_lookup_kernel(const int64_t* __restri
                                                          uint32_t* __restrict__ nmissing) {
   __shared__ uint32_t wmiss[4];
   uint32_t miss = 0;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
+  // grid-stride over a bounded grid: one miss-count atomic per workgroup (all on one address, they serialise in
+  // the L2: a workgroup per 256 records made them 3x the kernel's own time on a batch of new keys)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = pos ? pos[i] : i;  // no pos: the query keeps every batch record
     const int s = ev_stream[p];
     int32_t slot = -2;
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(256) void key_lookup_kernel(const int64_t* __restri
     }
     keys[i] = key;
     slot_out[i] = slot;
-    miss = slot == -1;
+    miss += slot == -1;
   }
   for (int o = 32; o > 0; o >>= 1) miss += __shfl_xor(miss, o, 64);
   if ((threadIdx.x & 63) == 0) wmiss[threadIdx.x >> 6] = miss;
@@ -734,7 +735,8 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
   uint32_t* nmiss = (uint32_t*)sc.take(4);
   SM_HIP(hipMemsetAsync(nmiss, 0, 4, s));
   if (n > 0)
-    hipLaunchKernelGGL(key_lookup_kernel, grid_for(n), dim3(256), 0, s, pos_identity ? nullptr : pos, n, ev_stream,
+    hipLaunchKernelGGL(key_lookup_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
+                       pos_identity ? nullptr : pos, n, ev_stream,
                        ev_row, streams_dev, progs_dev, nprogs, T.tkeys, T.tslots, T.mask, T.nslots == 0, keys, slot,
                        nmiss);
   uint32_t hm = 0;
