@@ -128,7 +128,7 @@ size_t sm_app_dump_outputs(sm_app* app, char* buf, size_t len);
  * "batch_events" (auto-flush threshold), "fast_general" (1 = device batches always take the general
  * closed-form kernels), "fast_timing" (1 = record HIP events around the device-batch phases), "reset" (drop all
  * matching state, keep the device allocations), "lane_balance" (N > 0: order the NFA lanes of a partitioned batch
- * with >= N keys by descending event count; 0 = off; default 65536; outputs are unchanged either way). */
+ * with >= N keys by descending event count; 0 = off, the default; outputs are unchanged either way). */
 int sm_app_set_option(sm_app* app, const char* key, int64_t value);
 
 /* Device-resident batch of ONE stream (columns already in HBM, hipStream given as void*): the device form of a
