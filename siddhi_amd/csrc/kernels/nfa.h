@@ -30,7 +30,16 @@ struct LaneEv {
   static __host__ __device__ constexpr int64_t words(int node_words) {
     return kNode + node_words <= 8 ? 8 : (kNode + node_words + 15) / 16 * 16;
   }
+  // Compact form (NfaBatch::lane_compact; node images of at most 8 words = up to 4 attributes): one 64-byte record
+  //   w0 = position (u32) | advance points up to it (i32) << 32, w1 = clock, w2 = event time,
+  //   w3 = ordinal - lane_ord_base (48 bits, all ones = none) | stream (i8) << 48 | null mask (8 bits) << 56,
+  //   w4..w7 = attribute words.
+  // Half the bytes of the 128-byte form for the lane-events pass to write and the NFA lanes to read.
+  static __host__ __device__ constexpr int64_t words(int node_words, bool compact) {
+    return compact ? 8 : words(node_words);
+  }
 };
+constexpr uint64_t kLeOrdMask = (1ull << 48) - 1;
 
 struct NfaBatch {
   // app batch (all records in arrival order)
@@ -51,6 +60,8 @@ struct NfaBatch {
   const int64_t* key_off;
   const int64_t* key_pos;
   const int64_t* lane_ev;    // LaneEv records, one per key_pos entry (filled by launch_lane_events)
+  int32_t lane_compact;      // LaneEv records in the compact 64-byte form (LaneEv)
+  int64_t lane_ord_base;     // compact form: ordinals are stored relative to it
   int32_t create_all;        // non-partitioned: the single lane exists from app creation
   const uint32_t* lane_perm; // lane -> key slot (launch_lane_balance), nullptr = identity
   // output
@@ -66,14 +77,50 @@ struct NfaBatch {
   int64_t pool_cap;
 };
 
-// LaneEv records for key_pos[0, nq) of a batch of n records: b.lane_ev must point at nq * LaneEv::words(node_words)
-// words, inv_scratch at n int32
+// Fields of a LaneEv record in either form (b.lane_compact; a query-specialised kernel is compiled for one form,
+// SM_LANE_COMPACT_CONST, so the choice folds away)
+#ifdef SM_LANE_COMPACT_CONST
+#define SM_LE_C(b) (SM_LANE_COMPACT_CONST != 0)
+#else
+#define SM_LE_C(b) ((b).lane_compact != 0)
+#endif
+__host__ __device__ inline int64_t le_pos(const NfaBatch& b, const int64_t* r) {
+  return SM_LE_C(b) ? (int64_t)(uint32_t)r[0] : r[LaneEv::kPos];
+}
+__host__ __device__ inline int64_t le_upto(const NfaBatch& b, const int64_t* r) {
+  return SM_LE_C(b) ? (int64_t)(int32_t)((uint64_t)r[0] >> 32) : r[LaneEv::kUpto];
+}
+__host__ __device__ inline int le_stream(const NfaBatch& b, const int64_t* r) {
+  return SM_LE_C(b) ? (int)(int8_t)(uint8_t)((uint64_t)r[3] >> 48) : (int)r[LaneEv::kStream];
+}
+__host__ __device__ inline int64_t le_clock(const NfaBatch& b, const int64_t* r) {
+  return SM_LE_C(b) ? r[1] : r[LaneEv::kClock];
+}
+// word w (1 .. node_words - 1) of the chain-node image: event time, ordinal, null mask, attribute words
+__host__ __device__ inline int64_t le_node(const NfaBatch& b, const int64_t* r, int w) {
+  if (!SM_LE_C(b)) return r[LaneEv::kNode + w];
+  if (w == 1) return r[2];
+  if (w == 2) {
+    const uint64_t v = (uint64_t)r[3] & kLeOrdMask;
+    return v == kLeOrdMask ? -1 : b.lane_ord_base + (int64_t)v;
+  }
+  if (w == 3) return (int64_t)(((uint64_t)r[3] >> 56) & 0xFF);
+  return r[w];  // attribute a = w - 4 at word 4 + a
+}
+
+// LaneEv records for key_pos[0, nq) of a batch of n records: b.lane_ev must point at
+// nq * LaneEv::words(node_words, b.lane_compact) words, inv_scratch at n int32
 void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_words, int32_t* inv_scratch,
                         hipStream_t s);
 // Lane order by descending event count of the batch (stable by slot), so that the 64 lanes of a wave walk about
 // as many events each: a wave runs as long as its longest lane. perm must hold nkeys uint32.
 struct Scratch;
 void launch_lane_balance(const int64_t* key_off, int32_t nkeys, uint32_t* perm, Scratch& sc, hipStream_t s);
+// Whether this batch's LaneEv records can take the compact form: node images of at most 8 words, positions and
+// advance points below 2^31, stream indices in int8, and the data events' ordinals within a 2^48 - 1 range (a
+// reduction over ev_ord; *ord_base = their minimum).
+bool lane_compact_ok(const NfaBatch& b, int64_t n, int32_t node_words, int nstreams, Scratch& sc, hipStream_t s,
+                     int64_t* ord_base);
 // ks is lane-interleaved: word w of key k at [w * lanes + k] (lanes = allocated key capacity); heap is key-major
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
                 int32_t nkeys, int32_t* err_dev, hipStream_t s);

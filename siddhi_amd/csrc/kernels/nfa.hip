@@ -2,6 +2,9 @@
 #include "nfa_impl.h"
 #include "primitives.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace sm {
 namespace {
 
@@ -37,29 +40,54 @@ __global__ void lane_events_kernel(NfaBatch b, int64_t n, const int32_t* __restr
   if (k >= 0) lane_event_record(b, p, k, node_words, out);
 }
 
-// The common record shape (16 words = one 128-byte line): each thread builds the record of its batch position in
-// LDS, then groups of 8 lanes store one record each (8 x 16 B), so a wave's store instruction writes 8 whole lines
-// instead of touching 64 (one 16-byte piece of each of 64 scattered records per instruction).
+// The common record shapes (16 words = one 128-byte line; the compact form, 8 words = 64 bytes): each thread builds
+// the record of its batch position in LDS, then groups of WORDS / 2 lanes store one record each (16 B per lane), so a
+// wave's store instruction writes whole records (8 lines / 16 half-lines) instead of touching 64 (one 16-byte piece
+// of each of 64 scattered records per instruction).
 constexpr int kLeBlock = 256;
-constexpr int kLeStride = 18;  // words per LDS row: 16 + 2 of padding (rows start on rotating banks)
-__global__ void __launch_bounds__(kLeBlock) lane_events16_kernel(NfaBatch b, int64_t n, const int32_t* __restrict__ inv,
-                                                               int32_t node_words, int64_t* __restrict__ out) {
-  __shared__ int64_t lrec[kLeBlock * kLeStride];
+template <int WORDS>
+__global__ void __launch_bounds__(kLeBlock) lane_events_lds_kernel(NfaBatch b, int64_t n, const int32_t* __restrict__ inv,
+                                                                   int32_t node_words, int64_t* __restrict__ out) {
+  constexpr int kStride = WORDS + 2;  // words per LDS row: 2 of padding (rows start on rotating banks)
+  constexpr int kPieces = WORDS / 2;  // 16-byte pieces per record
+  __shared__ int64_t lrec[kLeBlock * kStride];
   __shared__ int32_t lk[kLeBlock];
   const int tid = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * kLeBlock + tid;
   const int32_t k = p < n ? inv[p] : -1;
   lk[tid] = k;
-  if (k >= 0) lane_event_record(b, p, 0, node_words, lrec + tid * kLeStride);
+  if (k >= 0) lane_event_record(b, p, 0, node_words, lrec + tid * kStride);
   __syncthreads();
-  const int piece = tid & 7;
+  const int piece = tid % kPieces;
 #pragma unroll 4
-  for (int r = tid >> 3; r < kLeBlock; r += kLeBlock / 8) {
+  for (int r = tid / kPieces; r < kLeBlock; r += kLeBlock / kPieces) {
     const int32_t kr = lk[r];
     if (kr >= 0) {
-      const longlong2 v = *(const longlong2*)(lrec + r * kLeStride + 2 * piece);
-      *((longlong2*)(out + (int64_t)kr * 16) + piece) = v;
+      const longlong2 v = *(const longlong2*)(lrec + r * kStride + 2 * piece);
+      *((longlong2*)(out + (int64_t)kr * WORDS) + piece) = v;
     }
+  }
+}
+
+// lo / hi of the data events' ordinals (markers carry -1): one atomic pair per workgroup
+__global__ void __launch_bounds__(256) ord_range_kernel(const int64_t* __restrict__ ord, int64_t n,
+                                                        unsigned long long* __restrict__ mm) {
+  uint64_t lo = ~0ull, hi = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = ord[i];
+    if (o >= 0) {
+      lo = (uint64_t)o < lo ? (uint64_t)o : lo;
+      hi = (uint64_t)o > hi ? (uint64_t)o : hi;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t l2 = __shfl_xor(lo, off, 64), h2 = __shfl_xor(hi, off, 64);
+    lo = l2 < lo ? l2 : lo;
+    hi = h2 > hi ? h2 : hi;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&mm[0], (unsigned long long)lo);
+    atomicMax(&mm[1], (unsigned long long)hi);
   }
 }
 
@@ -96,12 +124,38 @@ void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_w
   if (nq < n) SM_HIP(hipMemsetAsync(inv_scratch, 0xff, (size_t)n * 4, s));
   hipLaunchKernelGGL(lane_index_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, b.key_pos, nq,
                      inv_scratch);
-  if (LaneEv::words(node_words) == 16)
-    hipLaunchKernelGGL(lane_events16_kernel, dim3((unsigned)((n + kLeBlock - 1) / kLeBlock)), dim3(kLeBlock), 0, s, b,
-                       n, (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
+  if (b.lane_compact)
+    hipLaunchKernelGGL(lane_events_lds_kernel<8>, dim3((unsigned)((n + kLeBlock - 1) / kLeBlock)), dim3(kLeBlock), 0, s,
+                       b, n, (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
+  else if (LaneEv::words(node_words) == 16)
+    hipLaunchKernelGGL(lane_events_lds_kernel<16>, dim3((unsigned)((n + kLeBlock - 1) / kLeBlock)), dim3(kLeBlock), 0,
+                       s, b, n, (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
   else
     hipLaunchKernelGGL(lane_events_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, n,
                        (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
+}
+
+bool lane_compact_ok(const NfaBatch& b, int64_t n, int32_t node_words, int nstreams, Scratch& sc, hipStream_t s,
+                     int64_t* ord_base) {
+  static const char* env = getenv("SM_LANE_COMPACT");  // A/B: 0 keeps the 128-byte records
+  if (env && atoi(env) == 0) return false;
+  if (node_words > 8 || n >= ((int64_t)1 << 31) || b.nadv >= ((int64_t)1 << 31) || nstreams > 127) return false;
+  *ord_base = 0;
+  if (n == 0) return true;
+  const size_t mark = sc.used;
+  unsigned long long* mm = (unsigned long long*)sc.take(16);
+  const unsigned long long init[2] = {~0ull, 0ull};
+  SM_HIP(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(ord_range_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1024)), dim3(256), 0, s,
+                     b.ev_ord, n, mm);
+  unsigned long long h[2];
+  SM_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+  if (h[0] > h[1]) return true;  // no data event
+  if (h[1] - h[0] >= kLeOrdMask) return false;
+  *ord_base = (int64_t)h[0];
+  return true;
 }
 
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half,

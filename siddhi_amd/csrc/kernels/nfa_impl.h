@@ -232,7 +232,7 @@ struct Lane {
     int32_t n = alloc(PQ->node_words);
     SM_COUNT(7, 1);
     heap[n] = K_NODE | ((int64_t)(uint32_t)-1 << 32);
-    for (int w = 1; w < PQ->node_words; ++w) heap[n + w] = r[LaneEv::kNode + w];
+    for (int w = 1; w < PQ->node_words; ++w) heap[n + w] = le_node(*b, r, w);
     return n;
   }
   // StateEvent.addEvent :212-222
@@ -1122,8 +1122,8 @@ struct Lane {
   // ------------------------------------------------------------ event delivery
   // MultiProcessStreamReceiver.receive / SingleProcessStreamReceiver.processAndClear + selector dispatch
   SM_INL_DELIVER __device__ void deliver(const int64_t* __restrict__ r) {
-    const int64_t p = r[LaneEv::kPos];
-    const int s = (int)r[LaneEv::kStream];
+    const int64_t p = le_pos(*b, r);
+    const int s = le_stream(*b, r);
     const DReceiver* R = nullptr;
     for (int k = 0; k < PQ->nrecv; ++k)
       if (PRECV[k].stream == s) R = &PRECV[k];
@@ -1133,7 +1133,7 @@ struct Lane {
     time = 0;
     phase = 1;
     sched = -1;
-    int64_t now = r[LaneEv::kNode + 1];
+    int64_t now = le_node(*b, r, 1);
     // stabilizeStates
     if (PQ->kind == 2) {
       for (int k = 0; k < PQ->nreset; ++k) resetState(PQ->reset_seq[k]);  // inner reset(), flattened (plan.h)
@@ -1248,12 +1248,30 @@ __device__ __forceinline__ int64_t lane_attr(const NfaStream& st, int a, int64_t
 
 __device__ __forceinline__ void lane_event_record(const NfaBatch& b, int64_t p, int64_t k, int32_t node_words,
                                                   int64_t* __restrict__ out) {
-  const int64_t W = LaneEv::words(node_words);
+  const int64_t W = LaneEv::words(node_words, SM_LE_C(b));
   int64_t* r = out + k * W;
   const int s = b.ev_stream[p];
   const NfaStream* st = s >= 0 ? &b.streams[s] : nullptr;
   const int na = st ? st->nattr : 0;
   const int64_t row = st ? b.ev_row[p] : 0;
+  if (SM_LE_C(b)) {
+    // the compact 64-byte form (nfa.h LaneEv): at most 4 attributes
+    int64_t v[8];
+    int64_t nulls = 0;
+    const int64_t upto = b.adv_upto ? b.adv_upto[p] : -1;
+    v[0] = (int64_t)(((uint64_t)(uint32_t)p) | ((uint64_t)(uint32_t)(int32_t)upto << 32));
+    v[1] = b.ev_clock[p];
+    v[2] = b.ev_ts[p];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) v[4 + a] = (a < na) ? lane_attr(*st, a, row, nulls) : 0;
+    const int64_t o = b.ev_ord[p];
+    const uint64_t ov = o < 0 ? kLeOrdMask : ((uint64_t)(o - b.lane_ord_base) & kLeOrdMask);
+    v[3] = (int64_t)(ov | ((uint64_t)(uint8_t)(int8_t)s << 48) | ((uint64_t)(nulls & 0xFF) << 56));
+    longlong2* r2 = (longlong2*)r;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) r2[w] = make_longlong2(v[2 * w], v[2 * w + 1]);
+    return;
+  }
   if (W == 16) {
     // the common shape (<= 8 attributes): the record in registers, one full 128-byte line in 16-byte stores
     int64_t v[16];
@@ -1396,7 +1414,7 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
 #endif
   const char* blob = (const char*)PQ;
   const int64_t ebeg = b.key_off[key], eend = b.key_off[key + 1];
-  const int64_t W = LaneEv::words(PQ->node_words);
+  const int64_t W = LaneEv::words(PQ->node_words, SM_LE_C(b));
   const bool has_timers = PQ->nsched > 0;
   // lane creation: QueryRuntime constructor → init() seeds the start state (PartitionRuntime.clonePartition)
   if (L.misc(4) == 0) {
@@ -1414,7 +1432,7 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
       L.sq(s)[0] = 0;
       L.sq(s)[1] = 0;
     }
-    L.misc(0) = (ebeg < eend) ? b.lane_ev[ebeg * W + LaneEv::kNode + 2] : -1;  // creation ordinal
+    L.misc(0) = (ebeg < eend) ? le_node(b, b.lane_ev + ebeg * W, 2) : -1;  // creation ordinal
     L.misc(1) = 0;
     L.misc(2) = 0;
     L.misc(3) = 0;
@@ -1430,7 +1448,7 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
   for (;;) {
     // this key's events are consecutive LaneEv records (key order): one contiguous read per event
     const int64_t* __restrict__ r = b.lane_ev + k * W;
-    const int64_t next_pos = (k < eend) ? r[LaneEv::kPos] : INT64_MAX;
+    const int64_t next_pos = (k < eend) ? le_pos(b, r) : INT64_MAX;
     if (has_timers) {
       for (;;) {
         if (L.err) break;
@@ -1438,9 +1456,9 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
         if (!L.min_head(t)) break;
         // first advance point at or after search_from whose position <= next_pos and (clock >= t or wall tick)
         // (both arrays are non-decreasing: positions ascend and the playback clock only moves forward)
-        const int64_t a1 = adv_after(b, search_from, next_pos, k < eend ? r[LaneEv::kUpto] : -1);
+        const int64_t a1 = adv_after(b, search_from, next_pos, k < eend ? le_upto(b, r) : -1);
         // quick reject: every advance point up to next_pos has clock <= the clock after next_pos's sendData
-        if (next_pos != INT64_MAX && r[LaneEv::kClock] < t) {
+        if (next_pos != INT64_MAX && le_clock(b, r) < t) {
           search_from = a1;
           break;
         }
@@ -1450,8 +1468,8 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
     if (L.err || k >= eend) break;
     const int64_t p = next_pos;
     // clock as of this event (sendData advanced it before delivery)
-    L.clock = r[LaneEv::kClock];
-    if (r[LaneEv::kStream] == NFA_START) {
+    L.clock = le_clock(b, r);
+    if (le_stream(b, r) == NFA_START) {
       // SiddhiAppRuntime.start → AbsentStreamPreStateProcessor.start :261-269 (non-partitioned queries)
       for (int pp = 0; pp < PQ->npre; ++pp)
         if (L.is_absent(pp) && PPRE[pp].isStart && PPRE[pp].waitingTime != -1 && L.fl(pp, F_ACTIVE))
@@ -1460,7 +1478,7 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
       L.deliver(r);
     }
     // timers scheduled by this event may only fire at later advance points
-    search_from = adv_after(b, search_from, p, r[LaneEv::kUpto]);
+    search_from = adv_after(b, search_from, p, le_upto(b, r));
     ++k;
     if (L.err) break;
     L.safe_point();

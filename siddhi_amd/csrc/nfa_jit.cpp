@@ -91,7 +91,7 @@ std::string blob_array(const std::vector<char>& blob) {
 
 }  // namespace
 
-std::string nfa_jit_source(const std::vector<char>& blob, bool lds) {
+std::string nfa_jit_source(const std::vector<char>& blob, bool lds, int compact) {
   std::string src = kPrelude;
   // Occupancy: room for 2 waves per SIMD (256 VGPRs). Measured on config 5 (N = 1e8, heap_words 1024, NFA kernel
   // ms): interpreter 74.3; JIT with the compiler's choice (268 VGPRs, 1 wave) 74.9, 2 waves 65.5, 4 waves 63.5;
@@ -110,13 +110,16 @@ std::string nfa_jit_source(const std::vector<char>& blob, bool lds) {
   const char* e = getenv("SM_NFA_JIT_INLINE_ALL");
   if (!e || atoi(e)) src += "#define SM_NFA_JIT_INLINE_ALL 1\n";
   if (lds) src += "#define SM_NFA_LDS 1\n";
+  if (compact >= 0) src += "#define SM_LANE_COMPACT_CONST " + std::to_string(compact ? 1 : 0) + "\n";
   src += blob_array(blob);
   src += kNfaJitBody;
   src += kKernel;
   return src;
 }
 
-std::string nfa_jit_source(const std::vector<char>& blob) { return nfa_jit_source(blob, nfa_jit_lds_bytes(blob) > 0); }
+std::string nfa_jit_source(const std::vector<char>& blob, int compact) {
+  return nfa_jit_source(blob, nfa_jit_lds_bytes(blob) > 0, compact);
+}
 
 bool nfa_jit_lds() {
   static const char* env = getenv("SM_NFA_JIT_LDS");
@@ -161,8 +164,8 @@ std::string nfa_jit_arch() {
   return SM_ARCH;
 }
 
-std::vector<char> nfa_jit_compile(const std::vector<char>& blob) {
-  const std::string src = nfa_jit_source(blob);
+std::vector<char> nfa_jit_compile(const std::vector<char>& blob, int compact) {
+  const std::string src = nfa_jit_source(blob, compact);
   if (const char* dump = getenv("SM_NFA_JIT_DUMP")) {
     if (FILE* f = fopen(dump, "w")) {
       fwrite(src.data(), 1, src.size(), f);
@@ -191,17 +194,17 @@ std::vector<char> nfa_jit_compile(const std::vector<char>& blob) {
   return code;
 }
 
-void* nfa_jit_function(const std::vector<char>& blob) {
+void* nfa_jit_function(const std::vector<char>& blob, int compact) {
   int dev = 0;
   SM_HIP(hipGetDevice(&dev));
-  const std::string key = std::to_string(dev) + ":" + nfa_jit_source(blob);  // the source carries the knobs too
+  const std::string key = std::to_string(dev) + ":" + nfa_jit_source(blob, compact);  // the source carries the knobs too
   {
     std::lock_guard<std::mutex> g(g_mu);
     auto it = cache().find(key);
     if (it != cache().end()) return (void*)it->second->fn;
   }
   // compile (seconds) without holding the cache: other apps' queries keep launching their kernels meanwhile
-  const std::vector<char> code = nfa_jit_compile(blob);
+  const std::vector<char> code = nfa_jit_compile(blob, compact);
   auto k = std::make_unique<JitKernel>();
   SM_HIP(hipModuleLoadData(&k->mod, code.data()));
   SM_HIP(hipModuleGetFunction(&k->fn, k->mod, "sm_nfa_jit"));

@@ -880,7 +880,8 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.clock_in = ev.clock_in;
   b.key_off = key_off;
   b.key_pos = key_pos;
-  b.lane_ev = (const int64_t*)a->sc.take((size_t)std::max<int64_t>(nq, 1) * LaneEv::words(h.node_words) * 8);
+  b.lane_compact = lane_compact_ok(b, N, h.node_words, (int)a->ast.streams.size(), a->sc, hs, &b.lane_ord_base) ? 1 : 0;
+  b.lane_ev = (const int64_t*)a->sc.take((size_t)std::max<int64_t>(nq, 1) * LaneEv::words(h.node_words, b.lane_compact) * 8);
   b.create_all = !partitioned;
   b.out = q.out.p;
   b.out_count = (uint32_t*)a->d_count.p;
@@ -902,7 +903,7 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   void* jit = nullptr;
   if (nfa_jit_wanted(a->nfa_jit, nq)) {
     try {
-      jit = nfa_jit_function(q.cq.blob);
+      jit = nfa_jit_function(q.cq.blob, b.lane_compact);
     } catch (const std::exception& e) {
       // the automatic mode falls back to the interpreter (same semantics); an explicit nfa_jit = 1 reports it
       if (a->nfa_jit == 1) throw;

@@ -257,7 +257,17 @@ void flush(HApp* a) {
     b.out_count = &count;
     b.out_cap = (uint32_t)(out.size() / stride);
     b.out_stride = (uint32_t)stride;
-    std::vector<int64_t> lane_ev(std::max<size_t>(key_pos.size(), 1) * LaneEv::words(h.node_words));
+    {  // the compact LaneEv form under the device's rule (nfa.hip lane_compact_ok); SM_HOST_LANE_COMPACT=0 keeps 128 B
+      const char* e = getenv("SM_HOST_LANE_COMPACT");
+      int64_t lo = INT64_MAX, hi = -1;
+      for (int64_t o : a->ev_ord)
+        if (o >= 0) lo = std::min(lo, o), hi = std::max(hi, o);
+      const bool ok = !(e && atoi(e) == 0) && h.node_words <= 8 && N < ((int64_t)1 << 31) && b.nadv < ((int64_t)1 << 31) &&
+                      a->st.size() <= 127 && (hi < 0 || (uint64_t)(hi - lo) < kLeOrdMask);
+      b.lane_compact = ok ? 1 : 0;
+      b.lane_ord_base = hi < 0 ? 0 : lo;
+    }
+    std::vector<int64_t> lane_ev(std::max<size_t>(key_pos.size(), 1) * LaneEv::words(h.node_words, b.lane_compact));
     b.lane_ev = lane_ev.data();
     for (size_t k = 0; k < key_pos.size(); ++k) lane_event_record(b, key_pos[k], (int64_t)k, h.node_words, lane_ev.data());
     for (int32_t key = 0; key < nkeys; ++key) nfa_lane(b, blob, q.ks.data(), q.heap.data(), a->heap_half, q.state_slots, key, &err);
