@@ -32,7 +32,7 @@ FAMILIES = [("walk_kernel<", "walk"), ("pass0_kernel", "key_pass0"), ("downsweep
             ("carry_in_kernel", "stack_prep"), ("merge_main_kernel", "carry_merge"),
             ("merge_carried_kernel", "carry_merge"),
             ("filter_count", "filter_count"), ("filter_write", "filter_write"), ("filter_block_scan", "filter_scan"),
-            ("nfa_kernel", "nfa"), ("sm_nfa_jit", "nfa"), ("lane_events16_kernel", "nfa_setup"),
+            ("nfa_kernel", "nfa"), ("sm_nfa_jit", "nfa"), ("lane_events_lds_kernel", "nfa_setup"), ("lane_events16_kernel", "nfa_setup"),
             ("event_index_kernel", "event_index"), ("ts_tile_max_kernel", "event_index"),
             ("tile_prefix_max_kernel", "event_index"), ("advance_points_kernel", "event_index"), ("advance_rank_kernel", "event_index"),
             ("select_records_kernel", "nfa_select"), ("select_mask_kernel", "nfa_select"), ("key_lookup_kernel", "nfa_group"),
