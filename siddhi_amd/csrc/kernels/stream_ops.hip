@@ -266,10 +266,11 @@ __global__ __launch_bounds__(256) void key_lookup_kernel(const int64_t* __restri
     for (int k = 0; k < nprogs; ++k) {
       if (progs[k].stream != s) continue;
       ColLoader ld{&streams[s], ev_row[p]};
-      const Instr i0 = progs[k].code[0];
-      const StackVal v = (progs[k].len == 1 && (i0.op == OP_VAR || i0.op == OP_COL))
-                             ? ld.var(i0)
-                             : eval_prog(progs[k].code, progs[k].len, progs[k].consts, ld);
+      StackVal v;
+      if (progs[k].len == 1 && (progs[k].code[0].op == OP_VAR || progs[k].code[0].op == OP_COL))
+        v = ld.var(progs[k].code[0]);
+      else
+        v = eval_prog(progs[k].code, progs[k].len, progs[k].consts, ld);
       if (v.null) break;
       if (progs[k].type == T_FLOAT || progs[k].type == T_DOUBLE) {
         double d = v.d;
