@@ -42,6 +42,17 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
 // sid[i] = stream index, or NFA_TICK (-1) for a playback heartbeat (clock advance without an event).
 // out[i] = start + i
 void iota_i64(int64_t* out, int64_t n, int64_t start, hipStream_t s);
+// Carried closed-form partials (rows of `width` int64: key, ordinal, event time, then the attributes in canonical
+// form: integers as int64, FLOAT / DOUBLE as double bits) as the columns of a stream: attribute k (type types[k]) to
+// cols[k] in its own width, event time to ts, ordinal to ord (the hand-over of the carry to the NFA kernel).
+struct CarryCols {
+  int32_t nattr, width;
+  int32_t types[kMaxAttrs];
+  void* cols[kMaxAttrs];
+  int64_t* ts;
+  int64_t* ord;
+};
+void carry_rows_to_columns(const int64_t* rows, int64_t n, const CarryCols& c, hipStream_t s);
 
 // One query's n output records (stride bytes each, OutRec first) in delivery order (runtime.cpp deliver): by
 // (pos, phase), then for timer-phase records (time, listener group, key creation ordinal); a lane's own records

@@ -866,6 +866,28 @@ __global__ void iota_kernel(int64_t* __restrict__ out, int64_t n, int64_t start)
 }
 }  // namespace
 
+namespace {
+__global__ void __launch_bounds__(256) carry_columns_kernel(const int64_t* __restrict__ rows, int64_t n, CarryCols c) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const int64_t* row = rows + r * c.width;
+  c.ord[r] = row[1];
+  c.ts[r] = row[2];
+  for (int k = 0; k < c.nattr; ++k) {
+    const int64_t v = row[3 + k];
+    const int t = c.types[k];
+    if (t == T_INT || t == T_STRING) ((int32_t*)c.cols[k])[r] = (int32_t)v;
+    else if (t == T_FLOAT) ((float*)c.cols[k])[r] = (float)__longlong_as_double(v);
+    else if (t == T_LONG || t == T_DOUBLE) ((int64_t*)c.cols[k])[r] = v;
+    else ((uint8_t*)c.cols[k])[r] = (uint8_t)(v != 0);
+  }
+}
+}  // namespace
+
+void carry_rows_to_columns(const int64_t* rows, int64_t n, const CarryCols& c, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(carry_columns_kernel, grid_for(n), dim3(256), 0, s, rows, n, c);
+}
+
 void iota_i64(int64_t* out, int64_t n, int64_t start, hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(iota_kernel, grid_for(n), dim3(256), 0, s, out, n, start);
 }

@@ -996,44 +996,18 @@ int64_t nfa_device_batch(sm_app* a, int qi, int s, size_t n, const int64_t* d_ts
   off += al((size_t)N * 4);
   a->d_rp.ensure(off);
   char* base = (char*)a->d_rp.p;
-  std::vector<std::vector<char>> hcols(nattr);
-  std::vector<int64_t> hts, hord;
-  if (nc > 0) {
-    const int w = q.carry.width;
-    std::vector<int64_t> rows((size_t)nc * w);
-    SM_HIP(hipMemcpyAsync(rows.data(), q.carry.rows, rows.size() * 8, hipMemcpyDeviceToHost, hs));
-    SM_HIP(hipStreamSynchronize(hs));
+  if (nc > 0) {  // the carried rows become the first nc entries of the columns, on the device
+    if (nattr > kMaxAttrs) throw std::runtime_error("stream has more attributes than the device path supports");
+    CarryCols cc{};
+    cc.nattr = nattr;
+    cc.width = q.carry.width;
     for (int k = 0; k < nattr; ++k) {
-      const int t = (int)attrs[k].type, cw = width_of(t);
-      hcols[k].resize((size_t)nc * cw);
-      for (int64_t r = 0; r < nc; ++r) {
-        const int64_t v = rows[(size_t)r * w + 3 + k];  // canonical: integers as int64, FLOAT / DOUBLE as double bits
-        char* d = hcols[k].data() + (size_t)r * cw;
-        if (t == T_INT || t == T_STRING) {
-          const int32_t x = (int32_t)v;
-          memcpy(d, &x, 4);
-        } else if (t == T_FLOAT) {
-          double x;
-          memcpy(&x, &v, 8);
-          const float f = (float)x;
-          memcpy(d, &f, 4);
-        } else if (t == T_LONG || t == T_DOUBLE) {
-          memcpy(d, &v, 8);
-        } else {
-          const uint8_t x = (uint8_t)(v != 0);
-          memcpy(d, &x, 1);
-        }
-      }
-      SM_HIP(hipMemcpyAsync(base + col_off[k], hcols[k].data(), hcols[k].size(), hipMemcpyHostToDevice, hs));
+      cc.types[k] = (int)attrs[k].type;
+      cc.cols[k] = base + col_off[k];
     }
-    hts.resize(nc);
-    hord.resize(nc);
-    for (int64_t r = 0; r < nc; ++r) {
-      hord[r] = rows[(size_t)r * w + 1];
-      hts[r] = rows[(size_t)r * w + 2];
-    }
-    SM_HIP(hipMemcpyAsync(base + ts_off, hts.data(), nc * 8, hipMemcpyHostToDevice, hs));
-    SM_HIP(hipMemcpyAsync(base + ord_off, hord.data(), nc * 8, hipMemcpyHostToDevice, hs));
+    cc.ts = (int64_t*)(base + ts_off);
+    cc.ord = (int64_t*)(base + ord_off);
+    carry_rows_to_columns((const int64_t*)q.carry.rows, nc, cc, hs);
   }
   for (int k = 0; k < nattr; ++k) {
     const size_t cw = width_of((int)attrs[k].type);
