@@ -176,15 +176,16 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
       const Cond c1 = make_cond(c1code, c1len, consts);
       if (c1.simple) {
         // `x CMP y`: every operand load of the tile issued before the first compare (the interpreter loop below
-        // waits on one row's loads at a time)
+        // waits on one row's loads at a time); the operand columns resolved once (ColRef)
+        const ColRef ca = c1.a.op == OP_CONST ? ColRef{nullptr, 0} : col_ref(st, c1.a.op == OP_COL ? c1.a.a : c1.a.c);
+        const ColRef cb = c1.b.op == OP_CONST ? ColRef{nullptr, 0} : col_ref(st, c1.b.op == OP_COL ? c1.b.a : c1.b.c);
         StackVal l[kItems], r[kItems];
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
           const int64_t p = base + w * 64 * kItems + k * 64 + lane;
           if (p < hi0) {
-            const RowLoader ld{st, p};
-            l[k] = c1.a.op == OP_CONST ? c1.ka : ld.var(c1.a);
-            r[k] = c1.b.op == OP_CONST ? c1.kb : ld.var(c1.b);
+            l[k] = c1.a.op == OP_CONST ? c1.ka : ca.at(p);
+            r[k] = c1.b.op == OP_CONST ? c1.kb : cb.at(p);
           }
         }
 #pragma unroll
@@ -908,6 +909,7 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
   if constexpr (!KEYED && OP < 0) c2.c = make_cond(a.c2, a.c2_len, a.consts);
   c2.vtype = a.vtype;
   C2Code<OP, FP> cc{a.exact_codes, a.vtype, a.st->cols[a.vattr], a.ord, a.obase, n};  // keyed
+  const ColRef vref = KEYED ? ColRef{nullptr, 0} : col_ref(a.st, a.vattr);  // unkeyed: the compared column
 
   // keyed: the next tile's records are loaded into registers while the current tile is scanned
   constexpr int kPre = (kWalkLds + kWalkBlock - 1) / kWalkBlock;
@@ -943,7 +945,7 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
       for (int e = threadIdx.x; e < nload; e += kWalkBlock) {
         const int64_t p = base + e;
         L.t[e] = a.ts[p];
-        L.v[e] = canon(col_value(a.st, a.vattr, p), a.vtype);
+        L.v[e] = canon(vref.at(p), a.vtype);
       }
     }
     lds_barrier();
@@ -1069,7 +1071,7 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
           if (!stp) {
             const int64_t d = a.ts[q] - t0;
             stp = a.within >= 0 && (d < 0 ? -d : d) > a.within;
-            if (!stp) hit = c2(v0, canon(col_value(a.st, a.vattr, q), a.vtype));
+            if (!stp) hit = c2(v0, canon(vref.at(q), a.vtype));
           }
           const uint64_t hb = __ballot(hit), any = __ballot(stp) | hb;
           if (any) {
@@ -1115,7 +1117,7 @@ __global__ void __launch_bounds__(kWalkBlock) __attribute__((amdgpu_waves_per_eu
             ran_out = false;
             break;
           }
-          hit = c2(L.v[luu], canon(col_value(a.st, a.vattr, p), a.vtype));
+          hit = c2(L.v[luu], canon(vref.at(p), a.vtype));
         }
         if (hit) {
           hasm |= 1u << kk;

@@ -113,6 +113,29 @@ __device__ __forceinline__ StackVal col_value(const NfaStream* st, int a, int64_
   return v;
 }
 
+// One attribute column resolved once per kernel (its pointer and type out of the NfaStream descriptor), so a loop
+// of column reads does not reload the descriptor after every store (the compiler cannot prove the stores miss it)
+struct ColRef {
+  const void* p;
+  int t;
+  __device__ __forceinline__ StackVal at(int64_t row) const {
+    StackVal v;
+    v.i = 0;
+    v.d = 0;
+    v.null = 0;
+    switch (t) {
+      case T_INT: v.i = ((const int32_t*)p)[row]; break;
+      case T_LONG: v.i = ((const int64_t*)p)[row]; break;
+      case T_FLOAT: v.d = (double)((const float*)p)[row]; break;
+      case T_DOUBLE: v.d = ((const double*)p)[row]; break;
+      case T_STRING: v.i = ((const int32_t*)p)[row]; v.null = v.i < 0; break;
+      default: v.i = ((const uint8_t*)p)[row]; break;
+    }
+    return v;
+  }
+};
+__device__ __forceinline__ ColRef col_ref(const NfaStream* st, int a) { return ColRef{st->cols[a], st->types[a]}; }
+
 // canonical 64-bit image of an attribute value (double bits for FLOAT/DOUBLE, integer otherwise)
 __device__ __forceinline__ uint64_t canon(const StackVal& v, int type) {
   return (type == T_FLOAT || type == T_DOUBLE) ? (uint64_t)__double_as_longlong(v.d) : (uint64_t)v.i;
