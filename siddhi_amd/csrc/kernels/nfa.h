@@ -111,7 +111,12 @@ __host__ __device__ inline int64_t le_node(const NfaBatch& b, const int64_t* r, 
 // LaneEv records for key_pos[0, nq) of a batch of n records: b.lane_ev must point at
 // nq * LaneEv::words(node_words, b.lane_compact) words, inv_scratch at n int32
 void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_words, int32_t* inv_scratch,
-                        hipStream_t s);
+                        int nstreams, hipStream_t s);
+// stream descriptors a kernel copies into LDS (per-record attribute reads then find column pointers and types there
+// instead of in device memory): batches with at most this many streams
+constexpr int kLdsStreams = 8;
+
+static_assert(sizeof(NfaStream) % 8 == 0, "stream descriptors are copied as 8-byte words");
 // Lane order by descending event count of the batch (stable by slot), so that the 64 lanes of a wave walk about
 // as many events each: a wave runs as long as its longest lane. perm must hold nkeys uint32.
 struct Scratch;

@@ -47,12 +47,20 @@ __global__ void lane_events_kernel(NfaBatch b, int64_t n, const int32_t* __restr
 constexpr int kLeBlock = 256;
 template <int WORDS>
 __global__ void __launch_bounds__(kLeBlock) lane_events_lds_kernel(NfaBatch b, int64_t n, const int32_t* __restrict__ inv,
-                                                                   int32_t node_words, int64_t* __restrict__ out) {
+                                                                   int32_t node_words, int nstreams,
+                                                                   int64_t* __restrict__ out) {
   constexpr int kStride = WORDS + 2;  // words per LDS row: 2 of padding (rows start on rotating banks)
   constexpr int kPieces = WORDS / 2;  // 16-byte pieces per record
   __shared__ int64_t lrec[kLeBlock * kStride];
   __shared__ int32_t lk[kLeBlock];
+  __shared__ NfaStream lst[kLdsStreams];  // the batch's stream descriptors (each record reads its stream's)
   const int tid = threadIdx.x;
+  if (nstreams <= kLdsStreams) {
+    const int words = nstreams * (int)(sizeof(NfaStream) / 8);
+    for (int q = tid; q < words; q += kLeBlock) ((uint64_t*)lst)[q] = ((const uint64_t*)b.streams)[q];
+    __syncthreads();
+    b.streams = lst;
+  }
   const int64_t p = (int64_t)blockIdx.x * kLeBlock + tid;
   const int32_t k = p < n ? inv[p] : -1;
   lk[tid] = k;
@@ -117,7 +125,7 @@ void launch_lane_balance(const int64_t* key_off, int32_t nkeys, uint32_t* perm, 
 }
 
 void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_words, int32_t* inv_scratch,
-                        hipStream_t s) {
+                        int nstreams, hipStream_t s) {
   if (nq <= 0) return;
   if (nq >= INT32_MAX) throw std::runtime_error("query batch too large for the lane-event index (>= 2^31 records)");
   // positions outside the query's records stay -1; when the query keeps every record, lane_index writes them all
@@ -126,10 +134,10 @@ void launch_lane_events(const NfaBatch& b, int64_t n, int64_t nq, int32_t node_w
                      inv_scratch);
   if (b.lane_compact)
     hipLaunchKernelGGL(lane_events_lds_kernel<8>, dim3((unsigned)((n + kLeBlock - 1) / kLeBlock)), dim3(kLeBlock), 0, s,
-                       b, n, (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
+                       b, n, (const int32_t*)inv_scratch, node_words, nstreams, (int64_t*)b.lane_ev);
   else if (LaneEv::words(node_words) == 16)
     hipLaunchKernelGGL(lane_events_lds_kernel<16>, dim3((unsigned)((n + kLeBlock - 1) / kLeBlock)), dim3(kLeBlock), 0,
-                       s, b, n, (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);
+                       s, b, n, (const int32_t*)inv_scratch, node_words, nstreams, (int64_t*)b.lane_ev);
   else
     hipLaunchKernelGGL(lane_events_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, n,
                        (const int32_t*)inv_scratch, node_words, (int64_t*)b.lane_ev);

@@ -33,7 +33,7 @@ void project_rows(const NfaStream* st_dev, const int64_t* rows, int64_t nm, cons
                   uint32_t stride, hipStream_t s);
 int64_t select_records(const int32_t* ev_stream, int64_t n, uint64_t stream_mask, bool with_start, int64_t* out_pos,
                        Scratch& sc, hipStream_t s);
-int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* ev_stream, const int64_t* ev_row,
+int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* ev_stream, const int64_t* ev_row, int nstreams,
                      const NfaStream* streams_dev, const KeyProg* progs_dev, int nprogs, int64_t** key_pos_out,
                      int64_t** key_off_out, Scratch& sc, hipStream_t s, bool pos_identity = false);
 

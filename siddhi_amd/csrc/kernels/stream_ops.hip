@@ -248,13 +248,20 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 __global__ __launch_bounds__(256) void key_lookup_kernel(const int64_t* __restrict__ pos, int64_t n,
                                                          const int32_t* __restrict__ ev_stream,
                                                          const int64_t* __restrict__ ev_row,
-                                                         const NfaStream* __restrict__ streams,
+                                                         const NfaStream* __restrict__ streams, int nstreams,
                                                          const KeyProg* __restrict__ progs, int nprogs,
                                                          const int64_t* __restrict__ tkeys,
                                                          const int32_t* __restrict__ tslots, uint64_t mask, bool empty,
                                                          int64_t* __restrict__ keys, int32_t* __restrict__ slot_out,
                                                          uint32_t* __restrict__ nmissing) {
   __shared__ uint32_t wmiss[4];
+  __shared__ NfaStream lst[kLdsStreams];  // the stream descriptors, read by every record's key load
+  if (nstreams <= kLdsStreams) {
+    const int words = nstreams * (int)(sizeof(NfaStream) / 8);
+    for (int q = threadIdx.x; q < words; q += blockDim.x) ((uint64_t*)lst)[q] = ((const uint64_t*)streams)[q];
+    __syncthreads();
+    streams = lst;
+  }
   uint32_t miss = 0;
   // grid-stride over a bounded grid: one miss-count atomic per workgroup (all on one address, they serialise in
   // the L2: a workgroup per 256 records made them 3x the kernel's own time on a batch of new keys)
@@ -728,7 +735,7 @@ int64_t select_records(const int32_t* ev_stream, int64_t n, uint64_t stream_mask
 
 // Group a query's records by partition key. Returns the number of valid records; key_pos / key_off (CSR over
 // all `*nslots` slots) are written into buffers from `sc` (valid until the caller releases the scratch).
-int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* ev_stream, const int64_t* ev_row,
+int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* ev_stream, const int64_t* ev_row, int nstreams,
                      const NfaStream* streams_dev, const KeyProg* progs_dev, int nprogs, int64_t** key_pos_out,
                      int64_t** key_off_out, Scratch& sc, hipStream_t s, bool pos_identity) {
   int64_t* keys = (int64_t*)sc.take(std::max<int64_t>(n, 1) * 8);
@@ -738,7 +745,7 @@ int64_t group_by_key(KeyTable& T, const int64_t* pos, int64_t n, const int32_t* 
   if (n > 0)
     hipLaunchKernelGGL(key_lookup_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s,
                        pos_identity ? nullptr : pos, n, ev_stream,
-                       ev_row, streams_dev, progs_dev, nprogs, T.tkeys, T.tslots, T.mask, T.nslots == 0, keys, slot,
+                       ev_row, streams_dev, nstreams, progs_dev, nprogs, T.tkeys, T.tslots, T.mask, T.nslots == 0, keys, slot,
                        nmiss);
   uint32_t hm = 0;
   SM_HIP(hipMemcpyAsync(&hm, nmiss, 4, hipMemcpyDeviceToHost, s));
