@@ -85,11 +85,16 @@ __global__ void __launch_bounds__(kP0Block) pass0_kernel(Src src, uint4* __restr
   if (len > per) len = per;
   if (len < 0) len = 0;
   src.init();
+  uint4* row = (uint4*)&wc[tid][0];  // digit tid's count row, zeroed for the first tile here, then after each
+                                     // tile's placement (its last reader), so no barrier opens a tile
   {
     const uint32_t r0 = dbase[tid] + cnt[(int64_t)tid * G + blockIdx.x];
     run[tid] = r0;
     cst[tid] = r0;
+    row[0] = make_uint4(0, 0, 0, 0);
+    row[1] = make_uint4(0, 0, 0, 0);
   }
+  lds_barrier();
   typename Src::Raw raw[kP0Items];
   auto load_tile = [&](int64_t base) {
     const int64_t rem = lo + len - base;
@@ -111,10 +116,7 @@ __global__ void __launch_bounds__(kP0Block) pass0_kernel(Src src, uint4* __restr
       const int e = w * 64 * kP0Items + k * 64 + lane;
       if (e < tile_n) rec[k] = src.record(raw[k], base + e);
     }
-    uint4* row = (uint4*)&wc[tid][0];
-    row[0] = make_uint4(0, 0, 0, 0);
-    row[1] = make_uint4(0, 0, 0, 0);
-    lds_barrier();  // also: the previous tile's readers of xb / tstart / run / cst / carry are done
+    // (the previous tile's readers of xb / tstart / run / cst / carry finished before its closing barrier)
 
     // stable rank within (wave, digit): wave64 ballot peer masks, in arrival order
     uint32_t dg[kP0Items], lp[kP0Items];
@@ -163,7 +165,9 @@ __global__ void __launch_bounds__(kP0Block) pass0_kernel(Src src, uint4* __restr
     // carried records of digit tid whose segment completes now (or the chunk ends) leave first
     if (rn != c0 && (last || lim > c0))
       for (uint32_t q = 0; q < rn - c0; ++q) drec[c0 + q] = carry[tid][q];
-    lds_barrier();  // xb complete; the carry slots read above may be refilled
+    lds_barrier();  // xb complete; the carry slots read above may be refilled; the count rows are read no more
+    row[0] = make_uint4(0, 0, 0, 0);
+    row[1] = make_uint4(0, 0, 0, 0);
 
     // one 16-byte store per record, or into the carry when its segment is not complete in this chunk yet
 #pragma unroll
