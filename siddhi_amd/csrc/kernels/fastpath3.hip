@@ -110,7 +110,9 @@ __device__ unsigned long long sm_stamps[16];
 //   * per-chunk counts of the pass-0 digit. Keys are rebased by kmin rounded down to a multiple of kBins, so
 //     the low digit of the rebased key is the low digit of the key itself and needs no kmin yet.
 // Tiles of kTile events (kItems per thread, every load of the tile issued before any is used).
-template <typename KT, bool MASK>
+// EXTRA: an ordinal column or a LONG compared attribute is read too (without them, their registers are not held:
+// 134 -> fewer VGPRs, two workgroups per CU instead of one)
+template <typename KT, bool MASK, bool EXTRA>
 __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kcol, const int64_t* __restrict__ vlong,
                                                       const int64_t* __restrict__ ts, const int64_t* __restrict__ ord,
                                                       int64_t obase, int64_t n, int64_t per, int G,
@@ -136,11 +138,11 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
       if (p < hi0) {
         if (kcol) kk[k] = __builtin_nontemporal_load(kcol + p);
         tt[k] = __builtin_nontemporal_load(ts + p);
-        if (ord) oo[k] = ord[p];
-        if (vlong) vv[k] = vlong[p];
+        if (EXTRA && ord) oo[k] = ord[p];
+        if (EXTRA && vlong) vv[k] = vlong[p];
         if (lane == 0 && p > 0) {  // the element before each wave-item (other lanes take it from lane - 1)
           tp[k] = ts[p - 1];
-          if (ord) op[k] = ord[p - 1];
+          if (EXTRA && ord) op[k] = ord[p - 1];
         }
       }
     }
@@ -151,7 +153,7 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
       int64_t pt = __shfl_up(tt[k], 1, 64);
       if (lane == 0) pt = p > 0 ? tp[k] : tt[k];
       if (in && tt[k] < pt) bad = 1;
-      if (ord) {
+      if (EXTRA && ord) {
         int64_t po = __shfl_up(oo[k], 1, 64);
         if (lane == 0) po = p > 0 ? op[k] : oo[k] - 1;
         if (in) {
@@ -166,7 +168,7 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
         hi = u > hi ? u : hi;
         atomicAdd(&h[(uint32_t)kk[k] & (kBins - 1)], 1u);
       }
-      if (in && vlong) {
+      if (EXTRA && in && vlong) {
         const unsigned long long u = (unsigned long long)vv[k] ^ 0x8000000000000000ull;
         vlo = u < vlo ? u : vlo;
         vhi = u > vhi ? u : vhi;
@@ -1593,9 +1595,16 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
 
   // column facts + c1 mask + pass-0 digit counts, one pass
   const bool mask = !keyed || !c1_inline(hi, a);
-#define SM_PREP(KT, M)                                                                                              \
-  hipLaunchKernelGGL((prep_kernel<KT, M>), dim3(G), dim3(kBlock), 0, s, (const KT*)kcol, vlong, a.ts, a.ordinals,    \
+#define SM_PREP2(KT, M, X)                                                                                          \
+  hipLaunchKernelGGL((prep_kernel<KT, M, X>), dim3(G), dim3(kBlock), 0, s, (const KT*)kcol, vlong, a.ts, a.ordinals, \
                      a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt, c)
+#define SM_PREP(KT, M)                  \
+  do {                                  \
+    if (a.ordinals || vlong)            \
+      SM_PREP2(KT, M, true);            \
+    else                                \
+      SM_PREP2(KT, M, false);           \
+  } while (0)
   if (hi.key_type == T_LONG && keyed) {
     if (mask) SM_PREP(int64_t, true);
     else SM_PREP(int64_t, false);
@@ -1604,6 +1613,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     else SM_PREP(int32_t, false);
   }
 #undef SM_PREP
+#undef SM_PREP2
   tmark("prep");
   Ctrl hc;
   SM_HIP(hipMemcpyAsync(&hc, c, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
