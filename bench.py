@@ -448,6 +448,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     path = app.get_stat("fast_path:q")
+    nfa_kernel = int(app.get_stat("nfa_kernel:q")) if args.config == 5 else 0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     m = torch.tensor([nm], dtype=torch.int64, device=dev)
     if world > 1:
@@ -513,7 +514,9 @@ def main():
                 "event_time": f"floor(i/{ts_div}) ms", "matches": total_matches,
                 "parallelism": (f"key-sharded x{world}" if args.config in (4, 5) else
                                 f"index-range-sharded x{world}" if cfg["shards"] else f"replicas x{world}"),
-                "device_path": ("general NFA (interleaved device events)" if args.config == 5 else
+                "device_path": (("general NFA (interleaved device events), " +
+                                 {1: "query-specialised kernel", 2: "interpreter"}.get(nfa_kernel, "?"))
+                                if args.config == 5 else
                                 ({1: "general closed form", 2: "sort / walk closed form", 3: "bucket-stack closed form"}
                                  if args.config in (3, 4) else {3: "filter interpreter", 4: "filter typed conjunction"})
                                 .get(int(path), str(path))),

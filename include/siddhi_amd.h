@@ -149,7 +149,8 @@ int sm_app_process_device_batch(sm_app* app, const char* stream_id, size_t n, co
  * run on the GPU (general NFA kernel, playback timers included); outputs go to the callbacks in reference
  * order before the call returns. Ordinals: d_ordinals[i] if given, else ordinal_base + i. d_stream_idx[i] = -1
  * marks a playback heartbeat (sm_app_advance_time at d_timestamps[i]; no event, no ordinal).
- * "output_events:<query>" (sm_app_get_stat) = output events of the last such batch. */
+ * "output_events:<query>" (sm_app_get_stat) = output events of the last such batch; "nfa_kernel:<query>" = which NFA
+ * kernel ran it (1 = query-specialised, 2 = interpreter, 0 = none yet). */
 int sm_app_process_device_events(sm_app* app, size_t n, const int32_t* d_stream_idx, const int64_t* d_timestamps,
                                  const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
                                  void* hip_stream);

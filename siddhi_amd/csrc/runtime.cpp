@@ -164,6 +164,7 @@ struct QueryRt {
   bool nfa_used = false;     // host-API batches ran through the NFA kernel (partials live in ks / heap)
   bool nfa_mode = false;     // a closed-form query handed to the NFA kernel for good (nfa_device_batch)
   int level = 0;             // chaining depth: 0 reads input streams only, L reads a stream a level L-1 query fills
+  int nfa_kernel_used = 0;   // 1 = query-specialised NFA kernel, 2 = interpreter (last batch this query ran on the NFA)
   int fast_path_used = 0;    // 5 = NFA kernel, 3 = bucket stack, 2 = onesweep form, 1 = general form (last device
                              // batch)
   // what sm_app_device_project needs of the last closed-form batch: its stream, event times, ordinals, and the
@@ -921,6 +922,7 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
       a->nfa_jit = 0;
     }
   }
+  q.nfa_kernel_used = jit ? 1 : 2;
   if (jit)
     launch_nfa_jit(jit, nfa_jit_lds_bytes(q.cq.blob), b, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half,
                    q.state_slots, (int32_t)nkeys, (int32_t*)a->d_err.p, hs);
@@ -2693,6 +2695,14 @@ int sm_app_get_stat(sm_app* a, const char* key, double* out) {
           return;
         }
       throw sql::ValidationError("No query with name " + k.substr(14));
+    }
+    if (k.rfind("nfa_kernel:", 0) == 0) {  // 1 = query-specialised kernel, 2 = interpreter, 0 = not run
+      for (auto& q : a->queries)
+        if (q->cq.name == k.substr(11)) {
+          *out = q->nfa_kernel_used;
+          return;
+        }
+      throw sql::ValidationError("No query with name " + k.substr(11));
     }
     if (k.rfind("fast_path:", 0) == 0) {
       for (auto& q : a->queries)
