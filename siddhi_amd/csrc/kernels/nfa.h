@@ -44,7 +44,7 @@ constexpr uint64_t kLeOrdMask = (1ull << 48) - 1;
 struct NfaBatch {
   // app batch (all records in arrival order)
   const int32_t* ev_stream;  // stream index or NFA_* marker
-  const int64_t* ev_row;     // row within the stream's columns
+  const int64_t* ev_row;     // row within the stream's columns (nullptr: the position; device batches)
   const int64_t* ev_ts;
   const int64_t* ev_clock;   // playback clock after the record's sendData
   const int64_t* ev_ord;     // global arrival ordinal of each data event (-1 for markers)

@@ -1253,7 +1253,7 @@ __device__ __forceinline__ void lane_event_record(const NfaBatch& b, int64_t p, 
   const int s = b.ev_stream[p];
   const NfaStream* st = s >= 0 ? &b.streams[s] : nullptr;
   const int na = st ? st->nattr : 0;
-  const int64_t row = st ? b.ev_row[p] : 0;
+  const int64_t row = st ? (b.ev_row ? b.ev_row[p] : p) : 0;  // no ev_row: rows are positions (device batches)
   if (SM_LE_C(b)) {
     // the compact 64-byte form (nfa.h LaneEv): at most 4 attributes
     int64_t v[8];

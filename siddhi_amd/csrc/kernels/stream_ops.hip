@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void key_lookup_kernel(const int64_t* __restri
     int64_t key = 0;
     for (int k = 0; k < nprogs; ++k) {
       if (progs[k].stream != s) continue;
-      ColLoader ld{&streams[s], ev_row[p]};
+      ColLoader ld{&streams[s], ev_row ? ev_row[p] : p};
       StackVal v;
       if (progs[k].len == 1 && (progs[k].code[0].op == OP_VAR || progs[k].code[0].op == OP_COL))
         v = ld.var(progs[k].code[0]);
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(kIxThreads) void event_index_kernel(
     if (!in) continue;
     const int32_t st = sid[i];
     if (st < NFA_TICK || st >= nstreams) *bad = 1;  // plain vector store: any offender sets the flag
-    ev_row[i] = i;
+    if (ev_row) ev_row[i] = i;  // nullptr: the caller reads rows as positions (ev_row = identity)
     ev_ord[i] = st < 0 ? -1 : ord_in ? ord_in[i] : ord_base + i;  // heartbeats carry no event ordinal
     ev_clock[i] = playback ? (t > before ? t : before) : clock_in;
   }

@@ -1051,11 +1051,11 @@ int64_t nfa_device_batch(sm_app* a, int qi, int s, size_t n, const int64_t* d_ts
   const int64_t* ts = (const int64_t*)(base + ts_off);
   int64_t clock_out = a->clock;  // the closed form leaves the playback clock alone: so does its fallback
   const int64_t nadv = build_event_index(N, sid, (int32_t)a->streams.size(), ts, (const int64_t*)(base + ord_off), 0,
-                                         a->ast.playback, a->clock, (int64_t*)a->d_ev_row.p, (int64_t*)a->d_ev_ord.p,
+                                         a->ast.playback, a->clock, nullptr /* rows = positions */, (int64_t*)a->d_ev_ord.p,
                                          (int64_t*)a->d_ev_clock.p, (int64_t*)a->d_adv_pos.p,
                                          (int64_t*)a->d_adv_clock.p, (int64_t*)a->d_adv_wall.p,
                                          (int64_t*)a->d_adv_upto.p, &clock_out, a->sc, hs);
-  const EvArrays ev{sid, (const int64_t*)a->d_ev_row.p, ts, (const int64_t*)a->d_ev_clock.p,
+  const EvArrays ev{sid, nullptr, ts, (const int64_t*)a->d_ev_clock.p,
                     (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_rp_streams.p, (const int64_t*)a->d_adv_pos.p,
                     (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p, (const int64_t*)a->d_adv_upto.p,
                     nadv, a->clock};
@@ -2331,11 +2331,11 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
     }
     int64_t clock_out = a->clock;
     const int64_t nadv = build_event_index(
-        N, d_stream_idx, (int32_t)a->streams.size(), d_ts, d_ordinals, ordinal_base, a->ast.playback, a->clock, (int64_t*)a->d_ev_row.p, (int64_t*)a->d_ev_ord.p,
+        N, d_stream_idx, (int32_t)a->streams.size(), d_ts, d_ordinals, ordinal_base, a->ast.playback, a->clock, nullptr /* rows = positions */, (int64_t*)a->d_ev_ord.p,
         (int64_t*)a->d_ev_clock.p, (int64_t*)a->d_adv_pos.p, (int64_t*)a->d_adv_clock.p, (int64_t*)a->d_adv_wall.p,
         (int64_t*)a->d_adv_upto.p, &clock_out, a->sc, hs);
     if (tm) tm->mark("event_index", hs);
-    const EvArrays ev{d_stream_idx, (const int64_t*)a->d_ev_row.p, d_ts, (const int64_t*)a->d_ev_clock.p,
+    const EvArrays ev{d_stream_idx, nullptr, d_ts, (const int64_t*)a->d_ev_clock.p,
                       (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p, (const int64_t*)a->d_adv_pos.p,
                       (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p, (const int64_t*)a->d_adv_upto.p,
                       nadv, a->clock};
