@@ -574,7 +574,8 @@ __global__ __launch_bounds__(kIxThreads) void event_index_kernel(
     const int32_t st = sid[i];
     if (st < NFA_TICK || st >= nstreams) *bad = 1;  // plain vector store: any offender sets the flag
     if (ev_row) ev_row[i] = i;  // nullptr: the caller reads rows as positions (ev_row = identity)
-    ev_ord[i] = st < 0 ? -1 : ord_in ? ord_in[i] : ord_base + i;  // heartbeats carry no event ordinal
+    // heartbeats carry no event ordinal; nullptr: the caller reads ord_in itself (its data events' ordinals)
+    if (ev_ord) ev_ord[i] = st < 0 ? -1 : ord_in ? ord_in[i] : ord_base + i;
     ev_clock[i] = playback ? (t > before ? t : before) : clock_in;
   }
   if (lane == 0) wadv[w] = nadv;

@@ -2331,12 +2331,15 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
     }
     int64_t clock_out = a->clock;
     const int64_t nadv = build_event_index(
-        N, d_stream_idx, (int32_t)a->streams.size(), d_ts, d_ordinals, ordinal_base, a->ast.playback, a->clock, nullptr /* rows = positions */, (int64_t*)a->d_ev_ord.p,
+        N, d_stream_idx, (int32_t)a->streams.size(), d_ts, d_ordinals, ordinal_base, a->ast.playback, a->clock,
+        nullptr /* rows = positions */, d_ordinals ? nullptr : (int64_t*)a->d_ev_ord.p /* given ordinals are read in place */,
         (int64_t*)a->d_ev_clock.p, (int64_t*)a->d_adv_pos.p, (int64_t*)a->d_adv_clock.p, (int64_t*)a->d_adv_wall.p,
         (int64_t*)a->d_adv_upto.p, &clock_out, a->sc, hs);
     if (tm) tm->mark("event_index", hs);
+    // the event ordinals: the caller's array when given (a heartbeat's entry is never read as an event's ordinal)
     const EvArrays ev{d_stream_idx, nullptr, d_ts, (const int64_t*)a->d_ev_clock.p,
-                      (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p, (const int64_t*)a->d_adv_pos.p,
+                      d_ordinals ? d_ordinals : (const int64_t*)a->d_ev_ord.p, (const NfaStream*)a->d_streams.p,
+                      (const int64_t*)a->d_adv_pos.p,
                       (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p, (const int64_t*)a->d_adv_upto.p,
                       nadv, a->clock};
     std::vector<HostOut> outs;
