@@ -11,7 +11,8 @@ over the whole batch: (multi-GPU) hash-by-key all-to-all of (symbol, price, ts, 
 then the closed-form pattern kernels producing the ordered (e1, e2) match tuples on every rank.
 
 Scaling is strong (N is the whole job at every GPU count). Launch: python bench.py [--gpus N --steps K
---warmup W]; for N > 1 the driver uses torch.distributed.run (one rank per GPU).
+--warmup W]; for N > 1 under torch.distributed.run (one rank per GPU; WORLD_SIZE must equal N), or without a
+launcher, in which case bench.py starts torch.distributed.run with N ranks itself (launch_command).
 
 The other §8(d) configurations are parity/measurement side lines, selected with --config:
   --config 2   filter-only `StockStream[price > 70 and volume < 1000]`, N = 1e9 (bandwidth roofline);
@@ -301,6 +302,29 @@ CONFIGS = {
 }
 
 
+def launch_command(gpus, argv, env, port=None):
+    """How `bench.py --gpus N` gets N ranks. Under a launcher (WORLD_SIZE set) the process is one rank: WORLD_SIZE
+    must equal N (a mismatch is an error, not a silently smaller run). Without one and N > 1, bench.py starts
+    torch.distributed.run itself (one process per GPU, rendezvous on 127.0.0.1) with the same arguments and exits with
+    its status: the returned command. None = run here as the only rank (N = 1) or as the launcher's rank."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws} (the launcher started a different number "
+                             "of ranks)")
+        return None
+    if gpus <= 1:
+        return None
+    if port is None:
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -320,6 +344,17 @@ def main():
     ap.add_argument("--heap-words", type=int, default=None,
                     help="NFA per-key partial-match arena (words per semispace; option heap_words)")
     args = ap.parse_args()
+    # before anything touches the GPU: N > 1 without a launcher starts one (a child process, never an exec)
+    cmd = launch_command(args.gpus, sys.argv[1:], os.environ)
+    if cmd is not None:
+        import subprocess
+        log(f"starting {args.gpus} ranks: {' '.join(cmd)}")
+        sys.exit(subprocess.call(cmd))
+    if os.environ.get("SM_BENCH_PROBE"):  # launcher test: report the rank layout and stop before any GPU call
+        sys.stdout.write(json.dumps({"rank": int(os.environ.get("RANK", "0")),
+                                     "world": int(os.environ.get("WORLD_SIZE", "1")), "gpus": args.gpus}) + "\n")
+        sys.stdout.flush()
+        return
     cfg = dict(CONFIGS[args.config])
     if args.variant:
         if args.config != 5:
@@ -334,7 +369,7 @@ def main():
     import torch.distributed as dist
     from siddhi_amd.testing import ProductApp
     from siddhi_amd.shard import (clock_ticks, concat_ordered, exchange_with_ordinals, merge_heartbeats,
-                                  return_matches, slice_starts)
+                                  partitioned_step, slice_starts)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -395,13 +430,30 @@ def main():
             return int(app.get_stat("output_events:q"))
         # a fresh runtime of the app per step: the query's open partials (carried across device batches) dropped
         app.set_option("reset", 0)
-        if args.config == 4 and world > 1:
-            (s_sym, s_price, s_ts), s_ord, _ = exchange_with_ordinals(symbol, [symbol, price, ts], world, lo,
-                                                                      starts=starts, offsets=offsets)
-        elif args.config == 4:
-            s_sym, s_price, s_ts, s_ord = symbol, price, ts, None
-        else:
-            s_sym, s_price, s_ts, s_ord = symbol, price, ts, None
+        if args.config == 4:
+            nm = [0]
+
+            def match(cols, ords):
+                # this rank's keys in global arrival order (with their global ordinals when sharded)
+                s_sym, s_price, s_ts = cols
+                n_local[0] = s_ts.numel()
+                app.process_device_batch("StockStream", s_ts, [s_sym, s_price, s_price, s_price], ordinals=ords,
+                                         hip_stream=hip_stream)
+                m = nm[0] = app.device_matches("q")[1]
+                if world == 1:
+                    return None  # the output stays in the library's device buffer, in reference order
+                if mbuf[0] is None or mbuf[0].numel() < m:
+                    mbuf[0] = torch.empty(max(m, 1) + (m >> 3), dtype=torch.int64, device=dev)
+                app.copy_device_matches("q", mbuf[0])
+                return mbuf[0][:m]
+
+            # the reference's single output order across ranks (shard.partitioned_step): key exchange, matching,
+            # every tuple returned to the rank that ingested its e2 and ordered there
+            mine = partitioned_step(symbol, [symbol, price, ts], world, lo, N, match, starts=starts, offsets=offsets)
+            if mine is not None:
+                out_local[0] = mine.numel()
+            return nm[0]
+        s_sym, s_price, s_ts, s_ord = symbol, price, ts, None
         n_local[0] = s_ts.numel()
         # columns: symbol, price, volume, timestamp (attributes the plan does not read are aliased)
         cols = [s_sym, s_price, volume if args.config == 2 else s_price, tsattr if args.config == 2 else s_price]
@@ -409,17 +461,11 @@ def main():
                                  hip_stream=hip_stream)
         m = app.device_matches("q")[1]
         if world > 1 and cfg["shards"]:
-            # the reference's single output order across ranks (shard.py): config 4 returns every tuple to the
-            # rank that ingested its e2 and orders it there; config 2's index-range outputs are concatenated
-            elem = torch.int32 if args.config == 2 else torch.int64
+            # config 2's index-range outputs are concatenated in rank order (shard.concat_ordered)
             if mbuf[0] is None or mbuf[0].numel() < m:
-                mbuf[0] = torch.empty(max(m, 1) + (m >> 3), dtype=elem, device=dev)
+                mbuf[0] = torch.empty(max(m, 1) + (m >> 3), dtype=torch.int32, device=dev)
             app.copy_device_matches("q", mbuf[0])
-            mine = mbuf[0][:m]
-            if args.config == 2:
-                out_local[0] = concat_ordered(mine.to(torch.int64) + lo, world).numel()
-            else:
-                out_local[0] = return_matches(mine, starts, N, world).numel()
+            out_local[0] = concat_ordered(mbuf[0][:m].to(torch.int64) + lo, world).numel()
         return m
 
     log(f"rank {rank}: config {args.config}, {hi - lo} events resident; warmup {args.warmup}")

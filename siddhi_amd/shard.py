@@ -270,6 +270,22 @@ def return_matches(pairs: torch.Tensor, starts, hi_last: int, world: int, group=
     return order_matches(buf, lo, hi)
 
 
+def partitioned_step(keys: torch.Tensor, columns, world: int, lo: int, n_total: int, match, starts=None,
+                     offsets=None, group=None) -> torch.Tensor:
+    """One step of a key-sharded partitioned pattern (bench.py config 4), from this rank's contiguous ingest slice
+    [lo, lo + len) to its slice of the global output: exchange_with_ordinals (one packed record per event, one
+    all-to-all-v) → `match(received columns, global ordinals or None)`, which returns this rank's match tuples (int64
+    (e2 << 32) | e1, global ordinals, reference order for its keys) → return_matches (each tuple to the rank that
+    ingested its e2, ordered there). The ranks' results in rank order are the single-process output. With world 1
+    the columns go to `match` unchanged (ordinals None: positions are the global ordinals)."""
+    if world == 1:
+        return match(list(columns), None)
+    recv, ords, _ = exchange_with_ordinals(keys, columns, world, lo, group=group, starts=starts, offsets=offsets)
+    if starts is None:
+        starts = slice_starts(lo, world, keys.device, group)
+    return return_matches(match(recv, ords), starts, n_total, world, group=group)
+
+
 def concat_ordered(rows: torch.Tensor, world: int, group=None) -> torch.Tensor:
     """Index-range shards (config 2: rank r filtered the r-th contiguous slice of the arrival order): every rank's
     kept rows (global ordinals, ordered) concatenated in rank order = the single-process output order. All-gather

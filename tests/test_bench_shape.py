@@ -1,0 +1,209 @@
+"""The benchmarked configurations at their benchmarked sizes (bench.py --config 4 / --config 3), so the numbers
+bench.py reports are for outputs that are pinned, not only for outputs that look plausible.
+
+Config 4 (N = 1e9, K = 1e6, ts_i = floor(i / 10000) ms, the automatic pipeline: bucket stack, path 3):
+  (a) the product's tuples restricted to the keys `symbol % 1009 == 5` equal the CPU oracle's output on that key
+      subsample (about 1e6 events: partition keys are independent, PartitionRuntime.java:256-309, so a key subset's
+      outputs are exactly the reference's outputs for those keys, in the same relative order);
+  (b) the whole output equals the sort / walk pipeline's (fast_stack = 2) on the same batch;
+  (c) the whole output equals a brute-force statement of the closed form, computed with torch on the GPU:
+      for every event i with c1 (price > 20), j*(i) = the first later event of i's key with price_j > price_i and
+      ts_j - ts_i <= 1000, output (i, j*) ordered by (j*, i). That is StreamPreStateProcessor.processAndReturn
+      (core/query/input/stream/state/StreamPreStateProcessor.java:274-327) for `every e1 -> e2 within T` with one
+      partial per e1: a partial leaves its pending list at its first match, or expires at the first event of its key
+      past the window.
+Config 3 (N = 1e8, ts_i = i ms, unpartitioned): the oracle on the first 1e7 events, and the whole 1e8 output against
+the brute-force statement.
+
+The synthetic stream is bench.py's own generator (gen_stock, on the device)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import bench
+
+def _dev():
+    import torch
+    return torch.device("cuda", 0)
+
+
+def closed_form_torch(key, price, ts, within, c1_min=20.0, chunk=1 << 26):
+    """Brute-force closed form of `every e1=S[price>c1_min] -> e2=S[price>e1.price] within T` on torch tensors
+    (key None = unpartitioned). Returns the packed int64 tuples (j << 32) | i in (j, i) order."""
+    import torch
+    n = price.numel()
+    dev = price.device
+    if key is not None:
+        order = torch.sort(key, stable=True).indices  # each key's events contiguous, in arrival order
+        k_s, p_s, t_s = key[order], price[order], ts[order]
+    else:
+        order, k_s, p_s, t_s = None, None, price, ts
+    starts = torch.nonzero(p_s > c1_min).flatten()
+    outs = []
+    for c0 in range(0, starts.numel(), chunk):
+        open_ = starts[c0:c0 + chunk]
+        pi, ti = p_s[open_], t_s[open_]
+        ki = k_s[open_] if k_s is not None else None
+        src = torch.arange(open_.numel(), device=dev)
+        d = 1
+        hits_i, hits_j = [], []
+        while open_.numel():
+            nxt = open_ + d
+            alive = nxt < n
+            nx = nxt.clamp(max=n - 1)
+            alive &= (t_s[nx] - ti) <= within
+            if ki is not None:
+                alive &= k_s[nx] == ki
+            hit = alive & (p_s[nx] > pi)
+            if bool(hit.any()):
+                hits_i.append(open_[hit])
+                hits_j.append(nx[hit])
+            keep = alive & ~hit
+            open_, pi, ti, src = open_[keep], pi[keep], ti[keep], src[keep]
+            if ki is not None:
+                ki = ki[keep]
+            d += 1
+        if hits_i:
+            i = torch.cat(hits_i)
+            j = torch.cat(hits_j)
+            if order is not None:
+                i, j = order[i], order[j]
+            outs.append((j << 32) | i)
+    if not outs:
+        return torch.zeros(0, dtype=torch.int64, device=dev)
+    return torch.sort(torch.cat(outs)).values  # (j, i) order: j in the high word
+
+
+def product_pairs(app, n_hint):
+    """The last device batch's tuples as one int64 device tensor ((e2 << 32) | e1)."""
+    import torch
+    m = app.device_matches("q")[1]
+    buf = torch.empty(max(m, 1), dtype=torch.int64, device=_dev())
+    assert app.copy_device_matches("q", buf) == m
+    torch.cuda.synchronize()
+    return buf[:m]
+
+
+def oracle_subsample(text, sym, price, ts, sel):
+    """CPU oracle over the selected events (global ordinals = `sel`, carried in the timestamp attribute): the
+    (e1, e2) global ordinals of its outputs, in its order."""
+    from oracle_lib import OracleApp, lib as olib
+    cols = [np.ascontiguousarray(sym), np.ascontiguousarray(price), np.zeros(len(sel), dtype=np.int64),
+            np.ascontiguousarray(sel.astype(np.int64))]
+    a = OracleApp(text)
+    a.start()
+    ptrs = (ctypes.c_void_p * 4)(*[c.ctypes.data for c in cols])
+    err = ctypes.create_string_buffer(512)
+    tsa = np.ascontiguousarray(ts, dtype=np.int64)
+    rc = olib().cr_send_columns(a.h, a.stream_index("StockStream"), len(tsa), tsa.ctypes.data, ptrs, err, 512)
+    assert rc == 0, err.value
+    out = a.outputs()["streams"].get("OutputStream", [])
+    a.close()
+    return np.array([r[1] for r in out], dtype=np.int64).reshape(-1, 2)  # the selected e1 / e2 timestamp attributes
+
+
+@pytest.fixture(scope="module")
+def config4():
+    import torch
+    cfg = bench.CONFIGS[4]
+    N, K, div = int(cfg["events"]), 1_000_000, cfg["ts_div"]
+    sym, price, vol, tsa, ts = bench.gen_stock(0, N, K, div, _dev(), bench.seed_for(4))
+    del vol, tsa
+    torch.cuda.synchronize()
+    yield dict(N=N, K=K, sym=sym, price=price, ts=ts)
+
+
+def _run4(c, stack):
+    import torch
+    from siddhi_amd.testing import ProductApp
+    app = ProductApp(bench.APP, fast_stack=stack)
+    app.set_collect(False)
+    app.process_device_batch("StockStream", c["ts"], [c["sym"], c["price"], c["price"], c["price"]])
+    path = int(app.get_stat("fast_path:q"))
+    got = product_pairs(app, c["N"]).clone()
+    app.close()
+    torch.cuda.empty_cache()
+    return got, path
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_config4_bench_shape_key_subsample_and_brute_force(config4):
+    import torch
+    c = config4
+    got, path = _run4(c, 0)
+    assert path == 3, "config 4 at the bench shape must take the bucket-stack pipeline"
+    m = got.numel()
+    assert m > 0.6 * c["N"]
+    # (a) key subsample vs the oracle
+    e1 = got & 0xFFFFFFFF
+    mine = (c["sym"][e1].to(torch.int64) % 1009) == 5
+    sub = got[mine]
+    sel = torch.nonzero((c["sym"].to(torch.int64) % 1009) == 5).flatten()
+    assert 5e5 < sel.numel() < 2e6
+    exp = oracle_subsample(bench.APP, c["sym"][sel].cpu().numpy(), c["price"][sel].cpu().numpy(),
+                           c["ts"][sel].cpu().numpy(), sel.cpu().numpy())
+    sub_h = sub.cpu().numpy()
+    gpu_pairs = np.stack([sub_h & 0xFFFFFFFF, sub_h >> 32], 1)
+    assert len(exp) > 1e5
+    np.testing.assert_array_equal(gpu_pairs, exp)
+    # (c) whole output vs the brute-force closed form
+    ref = closed_form_torch(c["sym"], c["price"], c["ts"], 1000)
+    assert ref.numel() == m, (ref.numel(), m)
+    assert torch.equal(ref, got), "bucket-stack output differs from the brute-force closed form"
+    print(f"config 4 N={c['N']}: {m} matches; key subsample {len(exp)} tuples equal to the oracle")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_config4_bench_shape_stack_equals_walk(config4):
+    import torch
+    a, pa = _run4(config4, 1)
+    b, pb = _run4(config4, 2)
+    assert (pa, pb) == (3, 2)
+    assert a.numel() == b.numel() and torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_config3_bench_shape_oracle_prefix_and_brute_force():
+    import torch
+    from siddhi_amd.testing import ProductApp
+    cfg = bench.CONFIGS[3]
+    N, div = int(cfg["events"]), cfg["ts_div"]
+    sym, price, vol, tsa, ts = bench.gen_stock(0, N, 1_000_000, div, _dev(), bench.seed_for(3))
+    del vol, tsa
+    app = ProductApp(bench.APP3)
+    app.set_collect(False)
+    # the first 1e7 events against the oracle (one batch of the prefix)
+    P = 10_000_000
+    app.process_device_batch("StockStream", ts[:P].contiguous(), [sym[:P], price[:P], price[:P], price[:P]])
+    assert int(app.get_stat("fast_path:q")) == 2
+    pre = product_pairs(app, P).cpu().numpy()
+    idx = np.arange(P, dtype=np.int64)
+    exp = oracle_subsample(bench.APP3, sym[:P].cpu().numpy(), price[:P].cpu().numpy(), ts[:P].cpu().numpy(), idx)
+    assert len(exp) > 0.5 * P
+    np.testing.assert_array_equal(np.stack([pre & 0xFFFFFFFF, pre >> 32], 1), exp)
+    # the whole 1e8-event batch (a fresh runtime) against the brute-force closed form
+    app.set_option("reset", 0)
+    app.process_device_batch("StockStream", ts, [sym, price, price, price])
+    got = product_pairs(app, N)
+    app.close()
+    ref = closed_form_torch(None, price, ts, 1000)
+    assert ref.numel() == got.numel() and torch.equal(ref, got)
+
+
+def test_brute_force_statement_matches_oracle_small():
+    """CPU check of the checker itself: the torch brute-force closed form equals the oracle (keyed and unkeyed)."""
+    import torch
+    import synth
+    from test_device_batch import app_text
+    for part, (n, K, div) in ((True, (30000, 300, 20)), (False, (20000, 10, 1))):
+        sym, price, vol, tsa, ts = synth.gen_stock(0, n, K, div, synth.seed_for(4))
+        text = app_text(partitioned=part)
+        exp = oracle_subsample(text, sym, price, ts, np.arange(n))
+        ref = closed_form_torch(torch.from_numpy(sym) if part else None, torch.from_numpy(price),
+                                torch.from_numpy(ts), 1000).numpy()
+        np.testing.assert_array_equal(np.stack([ref & 0xFFFFFFFF, ref >> 32], 1), exp)
+
