@@ -174,6 +174,7 @@ def test_config3_bench_shape_oracle_prefix_and_brute_force():
     N, div = int(cfg["events"]), cfg["ts_div"]
     sym, price, vol, tsa, ts = bench.gen_stock(0, N, 1_000_000, div, _dev(), bench.seed_for(3))
     del vol, tsa
+    torch.cuda.synchronize()  # the batch is read on the library's stream (no hip_stream passed)
     app = ProductApp(bench.APP3)
     app.set_collect(False)
     # the first 1e7 events against the oracle (one batch of the prefix)
