@@ -8,6 +8,7 @@
  *   sm_input_send                   InputHandler.send(long, Object[])       stream/input/InputHandler.java:53
  *   sm_input_send_columns           InputHandler.send(Event[])              stream/input/InputHandler.java:65 (columnar)
  *   sm_app_add_stream_callback      SiddhiAppRuntime.addCallback(String, StreamCallback)  :243
+ *   sm_count_events_callback        the counting StreamCallback of the reference's performance samples
  *   sm_app_add_query_callback       SiddhiAppRuntime.addCallback(String, QueryCallback)   :254
  *   sm_app_start / sm_app_shutdown  SiddhiAppRuntime.start / shutdown       :353 / :396
  *   sm_app_advance_time             @app:playback heartbeat (EventTimeBasedMillisTimestampGenerator.java:99)
@@ -104,7 +105,13 @@ int sm_app_shutdown(sm_app* app);
 int sm_app_input_handler(sm_app* app, const char* stream_id, sm_input** out);
 int sm_input_send(sm_input* in, int64_t timestamp, const sm_value* row, size_t n);
 /* n events of the handler's stream; cols[k] = host column of attribute k (int32 / int64 / float / double /
- * uint8 for BOOL / const char* for STRING); null_flags may be NULL or hold per-attribute uint8 arrays. */
+ * uint8 for BOOL / const char* for STRING); null_flags may be NULL or hold per-attribute uint8 arrays.
+ * Events are staged and processed at the next flush, except a batch of at least option "bulk_min" events (default
+ * 65536) with no null flags and no STRING attribute sent into an app whose queries are all filters and
+ * `every e1 -> e2 within T` patterns: it is processed inside the call, on the device-batch pipelines (closed form,
+ * carried partials shared with device batches), uploaded in chunks of option "bulk_chunk" events (default 2^24) with
+ * the upload of the next chunk overlapping the processing of the current one, and its outputs reach the callbacks
+ * chunk by chunk before the call returns. Staged events of such an app take the same pipelines at flush. */
 int sm_input_send_columns(sm_input* in, size_t n, const int64_t* timestamps, const void* const* cols,
                           const uint8_t* const* null_flags);
 
@@ -116,6 +123,9 @@ int sm_app_advance_time(sm_app* app, int64_t timestamp);
 int sm_app_advance_wallclock(sm_app* app, int64_t timestamp);
 
 int sm_app_add_stream_callback(sm_app* app, const char* stream_id, sm_stream_callback cb, void* user);
+/* A ready-made sm_stream_callback that adds each call's event count to the int64 `user` points at (the counting
+ * StreamCallback of the reference's performance samples, e.g. PartitionPerformance.java). */
+void sm_count_events_callback(void* user, const sm_event* events, size_t n);
 int sm_app_add_query_callback(sm_app* app, const char* query_name, sm_query_callback cb, void* user);
 
 /* Parity/diagnostics: collect every output as JSON

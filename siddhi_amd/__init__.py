@@ -124,6 +124,38 @@ class InputHandler:
         arr, keep = self._row(data)
         check(lib().sm_input_send(self._h, ts, arr, len(data)))
 
+    def send_columns(self, timestamps, columns, null_flags=None):
+        """send(Event[]) in columnar form: numpy arrays, int64 timestamps and one column per attribute at its native
+        width (INT int32, LONG int64, FLOAT float32, DOUBLE float64, BOOL uint8; STRING an object array of str),
+        null_flags an optional list of per-attribute uint8 arrays (or None entries). A large batch without nulls or
+        STRING attributes goes to the device in chunks and is processed inside this call (sm_input_send_columns)."""
+        import numpy as np
+        ts = np.ascontiguousarray(timestamps, dtype=np.int64)
+        n = ts.shape[0]
+        if len(columns) != len(self._types):
+            raise SiddhiTypeError(f"stream {self.stream_id} expects {len(self._types)} attributes")
+        want = {0: np.int32, 1: np.int64, 2: np.float32, 3: np.float64, 5: np.uint8}
+        keep, ptrs = [ts], []
+        for c, t in zip(columns, self._types):
+            if len(c) != n:
+                raise ValueError("every column must hold one value per timestamp")
+            if t == 4:
+                enc = [None if v is None else str(v).encode() for v in c]
+                arr = (ctypes.c_char_p * max(n, 1))(*enc)
+                keep.append((enc, arr))
+                ptrs.append(ctypes.cast(arr, ctypes.c_void_p).value)
+            else:
+                a = np.ascontiguousarray(c, dtype=want[t])
+                keep.append(a)
+                ptrs.append(a.ctypes.data)
+        cp = (ctypes.c_void_p * max(len(ptrs), 1))(*ptrs)
+        nf = None
+        if null_flags is not None and any(f is not None for f in null_flags):
+            fl = [None if f is None else np.ascontiguousarray(f, dtype=np.uint8) for f in null_flags]
+            keep.append(fl)
+            nf = (ctypes.c_void_p * len(fl))(*[None if f is None else f.ctypes.data for f in fl])
+        check(lib().sm_input_send_columns(self._h, n, ts.ctypes.data, cp, nf))
+
 
 class SiddhiAppRuntime:
     def __init__(self, handle):

@@ -22,7 +22,7 @@ EXPORTS = [
     "sm_app_set_option", "sm_app_process_device_batch", "sm_app_process_device_events", "sm_app_device_matches",
     "sm_app_snapshot", "sm_app_restore", "sm_partition_by_owner", "sm_order_matches", "sm_app_copy_device_matches",
     "sm_app_get_stat", "sm_compile_dump", "sm_nfa_jit_compile", "sm_app_device_project", "sm_merge_heartbeats",
-    "sm_unpack_records",
+    "sm_unpack_records", "sm_count_events_callback",
 ]
 
 

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <future>
 #include <limits>
 #include <map>
 #include <memory>
@@ -92,6 +93,7 @@ struct StreamStage {
   // device copies for the current flush
   std::vector<DBuf> dcols, dnulls;
   DBuf drow_pos;
+  DBuf drow_ts, drow_ord;  // flush_device: per-row event times and arrival ordinals
   void clear() {
     for (auto& c : cols) c.clear();
     for (auto& c : nulls) c.clear();
@@ -308,6 +310,14 @@ struct sm_app {
   bool outputs_unconsumed() const;
   bool need_outs = false;  // set while a caller reads the output records itself (nfa_device_batch)
   hipStream_t stream = nullptr;
+  int device = 0;  // the HIP device the app was created on (helper threads select it)
+  // bulk columnar sends (bulk_send_device): minimum events for the direct path (option "bulk_min"), events per chunk
+  // (option "bulk_chunk"), the upload stream and the two chunk buffers (attributes, then event times)
+  int64_t bulk_min = (int64_t)1 << 16;
+  int64_t bulk_chunk = (int64_t)1 << 24;
+  hipStream_t copy_stream = nullptr;
+  std::vector<sm::DBuf> bulk[2];
+  bool bulk_active = false;  // a bulk send is in progress (a callback's own large send is staged instead)
   sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_ev_ord, d_adv_pos, d_adv_clock, d_adv_wall, d_adv_upto, d_streams,
       d_err, d_count,
       d_keyoff, scratch, d_rp, d_rp_streams;
@@ -501,6 +511,7 @@ void build_app(sm_app* a) {
 }
 
 void upload_app(sm_app* a) {
+  SM_HIP(hipGetDevice(&a->device));
   SM_HIP(hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking));
   for (auto& q : a->queries) {
     q->blob.ensure(q->cq.blob.size());
@@ -1649,6 +1660,307 @@ void run_chained(sm_app* a, std::vector<HostOut>& outs) {
   outs.swap(sorted);
 }
 
+// The device-batch path of one stream (sm_app_process_device_batch, and host-API batches of apps whose queries all
+// take it: flush_device): every query reading stream s runs over the n events (columns, event times and ordinals
+// in device memory) on hs; the outputs that have consumers are appended to douts (their host copies in dkeep).
+void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const void* const* d_cols,
+                         const int64_t* d_ordinals, int64_t ordinal_base, hipStream_t hs, std::vector<HostOut>& douts,
+                         std::vector<std::vector<int64_t>>& dkeep) {
+  if (a->max_level > 0)
+    throw sql::UnsupportedError("apps whose queries read streams other queries fill run through the host API");
+  for (auto& bc : a->part_bcast)
+    if (!bc.empty()) throw sql::UnsupportedError("partitions reading unkeyed streams run through the host API");
+  for (auto& qp : a->queries)
+    if (qp->cq.hdr.kind != 0 && !qp->cq.fast_every_within &&
+        std::find(qp->cq.streams.begin(), qp->cq.streams.end(), s) != qp->cq.streams.end())
+      throw sql::UnsupportedError("device batches support filter queries and `every e1 -> e2 within T` patterns; "
+                                  "query '" + qp->cq.name + "' takes sm_app_process_device_events or the host API");
+  StreamStage& st = a->streams[s];
+  NfaStream d;
+  memset(&d, 0, sizeof(d));
+  d.nattr = (int)st.def->attrs.size();
+  for (int k = 0; k < d.nattr; ++k) {
+    d.types[k] = (int)st.def->attrs[k].type;
+    d.cols[k] = d_cols[k];
+  }
+  a->d_streams.ensure(sizeof(NfaStream));
+  SM_HIP(hipMemcpyAsync(a->d_streams.p, &d, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
+  size_t need = 64 << 20;  // filter queries: mask words + block counts; patterns: records, pairs, counts
+  for (auto& qp : a->queries) {
+    const CompiledQuery& cq = qp->cq;
+    if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
+    // patterns: records / staging / pairs (64 B per event), carry-out candidates (32 B each) and the carried
+    // partials' working arrays, plus the bucket-stack spill rings and bounded buffers
+    const size_t nc = (size_t)qp->carry.n, wc = (size_t)std::max(qp->carry.width, 4);
+    need = std::max(need, cq.hdr.kind == 0 ? n / 8 + n / 1024 + (64 << 20)
+                                           : n * 64 + std::min<size_t>(n + nc, (size_t)1 << 26) * 32 +
+                                                 nc * (160 + 8 * wc) + ((size_t)640 << 20));
+  }
+  ensure_scratch(a, need);
+  for (size_t qi = 0; qi < a->queries.size(); ++qi) {
+    QueryRt& q = *a->queries[qi];
+    const CompiledQuery& cq = q.cq;
+    if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
+    a->sc.used = 0;
+    const char* blob = (const char*)q.blob.p;
+    const bool consumed = outputs_consumed(a, q);
+    q.proj_ok = q.proj_nfa = false;
+    q.proj_desc = d;
+    q.proj_ts = d_ts;
+    q.proj_ord = d_ordinals;
+    q.proj_base = ordinal_base;
+    q.proj_n = (int64_t)n;
+    if (cq.hdr.kind == 0) {
+      q.dev_pairs.ensure(std::max<size_t>(n * 4, 16));
+      bool typed = false;
+      q.dev_n = filter_device(d, (const NfaStream*)a->d_streams.p, (int64_t)n,
+                              (const Instr*)(blob + cq.hdr.off_code) + cq.hdr.filt_off,
+                              (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.hdr.filt_off, cq.hdr.filt_len,
+                              (const DVal*)(blob + cq.hdr.off_const), (const DVal*)(cq.blob.data() + cq.hdr.off_const),
+                              d_ordinals, ordinal_base, (uint32_t*)q.dev_pairs.p, a->sc, hs,
+                              a->fast_timing ? &a->fast_tm : nullptr, &typed);
+      q.fast_path_used = typed ? 4 : 3;
+      q.prev_carry_n = 0;
+      q.proj_ok = true;
+      if (consumed) device_outputs(a, (int)qi, hs, douts, dkeep);
+      continue;
+    }
+    if (q.nfa_mode || q.nfa_used) {  // matching state held by the NFA kernel
+      q.dev_n = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs,
+                                 consumed ? &douts : nullptr);
+      q.fast_path_used = 5;
+      q.proj_nfa = true;
+      continue;
+    }
+    FastArgs fa{};
+    fa.n = (int64_t)n;
+    fa.ts = d_ts;
+    fa.st = (const NfaStream*)a->d_streams.p;
+    fa.key = cq.partition >= 0 ? (const KeyProg*)q.keyprogs.p : nullptr;
+    if (fa.key) {
+      const CompiledPartition& cp = *q.part;
+      int idx = (int)(std::find(cp.streams.begin(), cp.streams.end(), s) - cp.streams.begin());
+      fa.key = (const KeyProg*)q.keyprogs.p + idx;
+    }
+    fa.code = (const Instr*)(blob + cq.hdr.off_code);
+    fa.consts = (const DVal*)(blob + cq.hdr.off_const);
+    fa.c1_off = cq.fast_c1_off;
+    fa.c1_len = cq.fast_c1_len;
+    fa.c2_off = cq.fast_c2_off;
+    fa.c2_len = cq.fast_c2_len;
+    fa.within = cq.fast_within;
+    fa.ordinals = d_ordinals;
+    fa.ordinal_base = ordinal_base;
+    q.dev_pairs.ensure(std::max<size_t>((n + (size_t)q.carry.n) * 8, 16));
+    std::vector<int32_t> types(d.types, d.types + d.nattr);
+    FastHostInfo hi;
+    hi.cols = d_cols;
+    hi.types = types.data();
+    hi.vattr = fast_vattr(cq, types);
+    hi.c2_host = (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.fast_c2_off;
+    hi.c2_len = cq.fast_c2_len;
+    hi.c1_host = (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.fast_c1_off;
+    hi.c1_len = cq.fast_c1_len;
+    if (hi.vattr >= 0) hi.vtype = types[hi.vattr];
+    hi.nattr = d.nattr;
+    if (fa.key) {
+      const CompiledPartition& cp = *q.part;
+      int idx = (int)(std::find(cp.streams.begin(), cp.streams.end(), s) - cp.streams.begin());
+      const auto& kc = cp.key_code[idx];
+      if (kc.size() == 1 && kc[0].op == OP_COL) {
+        hi.key_col = kc[0].a;
+        hi.key_type = types[hi.key_col];
+      }
+    }
+    q.prev_carry_n = q.carry.n;
+    q.prev_carry_w = q.carry.width;
+    if (q.carry.n > 0) {
+      const size_t cb = (size_t)q.carry.n * q.carry.width * 8;
+      q.prev_carry.ensure(cb);
+      SM_HIP(hipMemcpyAsync(q.prev_carry.p, q.carry.rows, cb, hipMemcpyDeviceToDevice, hs));
+    }
+    int64_t m = FAST_OUTSIDE;
+    if (!a->force_general_fast)
+      m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
+                               a->fast_timing ? &a->fast_tm : nullptr, a->fast_stack);
+    q.fast_path_used = q.fast.last_path;
+    if (m == FAST_OUTSIDE && a->force_general_fast && q.carry.n == 0) {
+      // diagnostic (option "fast_general"): the stateless general closed form, one batch at a time
+      m = fast_every_within(fa, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs, a->fast_timing ? &a->fast_tm : nullptr);
+      q.fast_path_used = 1;
+    } else if (m < 0) {
+      // event time not monotone, or a condition outside the v2 envelope: the NFA kernel takes the query over
+      // (carried partials included) and keeps it, so later batches and host events see one matching state
+      m = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs, consumed ? &douts : nullptr);
+      q.fast_path_used = 5;
+      q.proj_nfa = true;
+    }
+    q.dev_n = m;
+    q.proj_ok = q.fast_path_used != 5 && m >= 0;
+    if (q.proj_ok && consumed) device_outputs(a, (int)qi, hs, douts, dkeep);
+  }
+}
+
+// Outputs of device-batch queries to their consumers (deliver() hands them out even when only the collect dump
+// takes them).
+void deliver_device(sm_app* a, std::vector<HostOut>& douts) {
+  if (!douts.empty()) {
+    a->need_outs = true;
+    struct Reset {
+      bool& f;
+      ~Reset() { f = false; }
+    } reset_need{a->need_outs};
+    deliver(a, douts);
+  }
+  a->out_arena.clear();
+}
+
+// Whether a host-API batch (the staged events of sm_input_send / sm_input_send_columns) can take the device-batch
+// path, stream by stream: every query is a filter or an `every e1 -> e2 within T` pattern (so no query reads the
+// playback clock or has timers, and each reads one stream), no query reads another query's output, no partition
+// broadcasts, and no staged value is null (device columns carry no null masks). The closed form then runs on the
+// host's events exactly as on a device batch, with one carry: InputHandler.send(Event[]) (InputHandler.java:64-68)
+// feeds the same receivers as any other send.
+bool app_device_ok(const sm_app* a) {
+  if (a->max_level > 0) return false;
+  for (auto& bc : a->part_bcast)
+    if (!bc.empty()) return false;
+  for (auto& q : a->queries)
+    if (q->cq.hdr.kind != 0 && !q->cq.fast_every_within) return false;
+  return true;
+}
+
+bool host_batch_device_ok(const sm_app* a) {
+  if (!app_device_ok(a)) return false;
+  for (auto& st : a->streams)
+    if (st.rows > 0)
+      for (size_t k = 0; k < st.any_null.size(); ++k)
+        if (st.any_null[k]) return false;
+  return true;
+}
+
+// A host-API batch through the device-batch path (host_batch_device_ok): per stream, its staged columns, its events'
+// times and arrival ordinals are uploaded and device_batch_stream runs every query reading it; the outputs of all
+// streams are delivered together in reference order (deliver() orders them by trigger ordinal, then query).
+// Heartbeats and the start record carry no event: no query of such an app reads them.
+void flush_device(sm_app* a) {
+  std::vector<HostOut> douts;
+  std::vector<std::vector<int64_t>> dkeep;
+  a->out_arena.clear();
+  for (size_t s = 0; s < a->streams.size(); ++s) {
+    StreamStage& st = a->streams[s];
+    if (st.rows == 0) continue;
+    bool read = false;
+    for (auto& q : a->queries) read |= std::find(q->cq.streams.begin(), q->cq.streams.end(), (int)s) != q->cq.streams.end();
+    if (!read) continue;
+    const int64_t R = st.rows;
+    std::vector<int64_t> rts(R), rord(R);
+    bool contiguous = true;
+    for (int64_t r = 0; r < R; ++r) {
+      const int64_t p = st.row_pos[r];
+      rts[r] = a->ev_ts[p];
+      rord[r] = a->ev_ord[p];
+      contiguous &= rord[r] == rord[0] + r;
+    }
+    std::vector<const void*> dc(st.cols.size());
+    for (size_t k = 0; k < st.cols.size(); ++k) {
+      upload(a, st.dcols[k], st.cols[k]);
+      dc[k] = st.dcols[k].p;
+    }
+    upload(a, st.drow_ts, rts);
+    if (!contiguous) upload(a, st.drow_ord, rord);
+    device_batch_stream(a, (int)s, (size_t)R, (const int64_t*)st.drow_ts.p, dc.data(),
+                        contiguous ? nullptr : (const int64_t*)st.drow_ord.p, rord[0], a->stream, douts, dkeep);
+  }
+  SM_HIP(hipStreamSynchronize(a->stream));
+  deliver_device(a, douts);
+}
+
+
+void flush(sm_app* a);
+
+// InputHandler.send(Event[]) (InputHandler.java:64-68) of a large columnar batch (sm_input_send_columns, at least
+// bulk_min events, no nulls, no STRING attribute) for an app whose queries all take the device-batch path
+// (app_device_ok): the columns go from the caller's memory straight to the device in chunks of bulk_chunk events,
+// without host staging, and each chunk runs through device_batch_stream with the next arrival ordinals (one carry, so
+// partials span the chunks as they span sends in the reference). A helper thread uploads chunk c + 1 on its own HIP
+// stream while chunk c is processed. Each chunk is processed under the app lock and its outputs go to the callbacks
+// before the next chunk (with the lock released, so a callback may send into the app: what it sends is staged and
+// runs before the next chunk). Returns a status like the locked entry points.
+int bulk_send_device(sm_app* a, int s, size_t n, const int64_t* ts, const void* const* cols) {
+  const int nattr = (int)a->streams[s].def->attrs.size();
+  std::vector<size_t> w(nattr);
+  for (int k = 0; k < nattr; ++k) w[k] = (size_t)width_of((int)a->streams[s].def->attrs[k].type);
+  const size_t B = std::min(n, (size_t)std::max<int64_t>(a->bulk_chunk, 1));
+  const size_t nchunks = (n + B - 1) / B;
+  const int dev = a->device;
+  std::future<void> next;
+  auto upload_chunk = [a, dev, nattr, &w, ts, cols](size_t lo, size_t len, int b) {
+    SM_HIP(hipSetDevice(dev));
+    hipStream_t cs = a->copy_stream;
+    for (int k = 0; k < nattr; ++k)
+      SM_HIP(hipMemcpyAsync(a->bulk[b][k].p, (const char*)cols[k] + lo * w[k], len * w[k], hipMemcpyHostToDevice, cs));
+    SM_HIP(hipMemcpyAsync(a->bulk[b][nattr].p, ts + lo, len * 8, hipMemcpyHostToDevice, cs));
+    SM_HIP(hipStreamSynchronize(cs));
+  };
+  struct Done {  // the upload in flight finishes before the buffers can be reused or freed
+    sm_app* a;
+    std::future<void>& f;
+    ~Done() {
+      if (f.valid()) f.wait();
+      std::lock_guard<std::mutex> g(a->mu);
+      a->bulk_active = false;
+    }
+  } done{a, next};
+  int rc = SM_OK;
+  for (size_t c = 0; c < nchunks && rc == SM_OK; ++c) {
+    std::vector<PreparedChunk> out;
+    {
+      std::lock_guard<std::mutex> g(a->mu);
+      rc = guarded([&] {
+        if (a->failed) throw std::runtime_error(a->failed_why);
+        flush(a);  // events staged before this chunk (earlier sends, or callbacks of the previous chunk) come first
+        if (c == 0) {
+          if (!a->copy_stream) SM_HIP(hipStreamCreateWithFlags(&a->copy_stream, hipStreamNonBlocking));
+          for (int b = 0; b < 2; ++b) {
+            a->bulk[b].resize(nattr + 1);
+            for (int k = 0; k < nattr; ++k) a->bulk[b][k].ensure(B * w[k]);
+            a->bulk[b][nattr].ensure(B * 8);
+          }
+          next = std::async(std::launch::async, upload_chunk, (size_t)0, B, 0);
+        }
+        const size_t lo = c * B, len = std::min(B, n - lo);
+        const int b = (int)(c & 1);
+        next.get();  // chunk c is on the device (rethrows an upload error)
+        if (c + 1 < nchunks) next = std::async(std::launch::async, upload_chunk, lo + B, std::min(B, n - lo - B), b ^ 1);
+        std::vector<const void*> dc(nattr);
+        for (int k = 0; k < nattr; ++k) dc[k] = a->bulk[b][k].p;
+        std::vector<HostOut> douts;
+        std::vector<std::vector<int64_t>> dkeep;
+        a->out_arena.clear();
+        try {
+          device_batch_stream(a, s, len, (const int64_t*)a->bulk[b][nattr].p, dc.data(), nullptr, a->next_ordinal,
+                              a->stream, douts, dkeep);
+          deliver_device(a, douts);
+        } catch (const std::exception& e) {
+          a->failed = true;
+          a->failed_why = std::string("a batch failed half-way (") + e.what() +
+                          "); the matching state is inconsistent: restore a snapshot or reset the app";
+          throw;
+        }
+        a->next_ordinal += (int64_t)len;
+        a->ordinal_base += (int64_t)len;
+        if (a->ast.playback)  // StreamJunction.sendData :232-237: the clock follows the largest event time so far
+          for (size_t i = lo; i < lo + len; ++i) a->clock = std::max(a->clock, ts[i]);
+        a->clock_batch_in = a->clock;
+      });
+      out.swap(a->pending);
+    }
+    run_callbacks(out);
+  }
+  return rc;
+}
+
 void flush(sm_app* a) {
   const int64_t N = (int64_t)a->ev_stream.size();
   if (N == 0) return;
@@ -1675,6 +1987,18 @@ void flush(sm_app* a) {
     }
   } done{a, N};
   try {
+    if (host_batch_device_ok(a)) {
+      flush_device(a);
+      return;
+    }
+    // the NFA kernel runs this batch: a closed-form query whose stream has events here hands its carried partials
+    // over first (nfa_device_batch without new events replays them into the NFA state) and stays on the NFA
+    for (size_t qi = 0; qi < a->queries.size(); ++qi) {
+      QueryRt& q = *a->queries[qi];
+      if (!q.cq.fast_every_within || q.nfa_mode || q.nfa_used || q.carry.n == 0) continue;
+      const int s = q.cq.streams.at(0);
+      if (a->streams[s].rows > 0) nfa_device_batch(a, (int)qi, s, 0, nullptr, nullptr, nullptr, 0, a->stream, nullptr);
+    }
     const EvHost e0{&a->ev_stream, &a->ev_row, &a->ev_ts, &a->ev_clock, &a->ev_ord, &a->adv_pos, &a->adv_clock,
                     &a->adv_wall};
     run_level(a, a->streams, e0, 0, outs);
@@ -1708,16 +2032,6 @@ void stage_record(sm_app* a, int32_t stream, int64_t row, int64_t ts, int wall) 
     }
   }
   a->ev_clock.push_back(a->clock);
-}
-
-// Partials of a closed-form query fed by device batches live in its carried state, which the host-API (NFA)
-// path does not read: host events for a stream such a query reads are refused instead of silently losing the
-// matches that span the two paths.
-void check_host_stream(sm_app* a, int stream) {
-  for (auto& q : a->queries)
-    if (q->carry.active && std::find(q->cq.streams.begin(), q->cq.streams.end(), stream) != q->cq.streams.end())
-      throw sql::UnsupportedError("query '" + q->cq.name + "' holds partial matches from device batches; send its "
-                                  "stream's events through sm_app_process_device_batch (or reset the app)");
 }
 
 void maybe_autoflush(sm_app* a) {
@@ -1813,6 +2127,13 @@ uint64_t fnv1a(const std::string& s) {
 extern "C" {
 
 const char* sm_last_error(void) { return sm::g_err.c_str(); }
+
+// The StreamCallback of the reference's performance samples (modules/siddhi-samples/performance-samples: receive()
+// adds events.length to a counter), as a native function: `user` points at an int64 count.
+void sm_count_events_callback(void* user, const sm_event* events, size_t n) {
+  (void)events;
+  *(int64_t*)user += (int64_t)n;
+}
 const char* sm_version(void) { return "siddhi_amd 0.1 (gfx950)"; }
 
 int sm_manager_create(sm_manager** out) {
@@ -1881,6 +2202,7 @@ void sm_app_destroy(sm_app* a) {
   if (!a) return;
   for (auto& q : a->queries) q->keys.release();
   if (a->stream) (void)hipStreamDestroy(a->stream);
+  if (a->copy_stream) (void)hipStreamDestroy(a->copy_stream);
   delete a;
 }
 
@@ -1930,7 +2252,6 @@ int sm_input_send(sm_input* in, int64_t ts, const sm_value* row, size_t n) {
     for (size_t k = 0; k < n; ++k)
       if (!row[k].is_null && row[k].type != (int)st.def->attrs[k].type)
         throw TypeError("value type does not match attribute '" + st.def->attrs[k].name + "'");
-    check_host_stream(a, in->stream);
     for (size_t k = 0; k < n; ++k) put_value(st, (int)k, row[k], a);
     st.row_pos.push_back((int64_t)a->ev_stream.size());
     stage_record(a, in->stream, st.rows, ts, 0);
@@ -1942,10 +2263,20 @@ int sm_input_send(sm_input* in, int64_t ts, const sm_value* row, size_t n) {
 int sm_input_send_columns(sm_input* in, size_t n, const int64_t* ts, const void* const* cols,
                           const uint8_t* const* null_flags) {
   sm_app* a = in->app;
-  return locked(a, [&] {
+  bool bulk = false;
+  const int rc = locked(a, [&] {
     StreamStage& st = a->streams[in->stream];
     size_t na = st.def->attrs.size();
-    check_host_stream(a, in->stream);
+    bool nulls = false, strings = false;
+    for (size_t k = 0; k < na; ++k) {
+      nulls |= null_flags && null_flags[k];
+      strings |= (int)st.def->attrs[k].type == T_STRING;
+    }
+    bulk = (int64_t)n >= a->bulk_min && !nulls && !strings && !a->bulk_active && app_device_ok(a);
+    if (bulk) {
+      a->bulk_active = true;
+      return;
+    }
     for (size_t i = 0; i < n; ++i) {
       for (size_t k = 0; k < na; ++k) {
         sm_value v{};
@@ -1968,6 +2299,8 @@ int sm_input_send_columns(sm_input* in, size_t n, const int64_t* ts, const void*
       maybe_autoflush(a);
     }
   });
+  if (rc != SM_OK || !bulk) return rc;
+  return bulk_send_device(a, in->stream, n, ts, cols);
 }
 
 int sm_app_stream_schema(sm_app* a, const char* stream_id, int32_t* types, size_t cap, size_t* n) {
@@ -2097,6 +2430,10 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       }
     } else if (k == "output_records") {
       a->out_records = std::max<int64_t>(0, value);
+    } else if (k == "bulk_min") {
+      a->bulk_min = std::max<int64_t>(1, value);
+    } else if (k == "bulk_chunk") {
+      a->bulk_chunk = std::max<int64_t>(1, value);
     } else if (k == "batch_events") {
       a->batch_events = std::max<int64_t>(1, value);
     } else {
@@ -2112,153 +2449,13 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
     int s = stream_index(a->ast, stream_id ? stream_id : "");
     if (s < 0) throw sql::ValidationError("unknown stream");
     flush(a);  // staged host events come first (arrival order)
-    if (a->max_level > 0)
-      throw sql::UnsupportedError("apps whose queries read streams other queries fill run through the host API");
-    for (auto& bc : a->part_bcast)
-      if (!bc.empty()) throw sql::UnsupportedError("partitions reading unkeyed streams run through the host API");
-    for (auto& qp : a->queries)
-      if (qp->cq.hdr.kind != 0 && !qp->cq.fast_every_within &&
-          std::find(qp->cq.streams.begin(), qp->cq.streams.end(), s) != qp->cq.streams.end())
-        throw sql::UnsupportedError("device batches support filter queries and `every e1 -> e2 within T` patterns; "
-                                    "query '" + qp->cq.name + "' takes sm_app_process_device_events or the host API");
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
-    StreamStage& st = a->streams[s];
-    NfaStream d;
-    memset(&d, 0, sizeof(d));
-    d.nattr = (int)st.def->attrs.size();
-    for (int k = 0; k < d.nattr; ++k) {
-      d.types[k] = (int)st.def->attrs[k].type;
-      d.cols[k] = d_cols[k];
-    }
-    a->d_streams.ensure(sizeof(NfaStream));
-    SM_HIP(hipMemcpyAsync(a->d_streams.p, &d, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
-    size_t need = 64 << 20;  // filter queries: mask words + block counts; patterns: records, pairs, counts
-    for (auto& qp : a->queries) {
-      const CompiledQuery& cq = qp->cq;
-      if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
-      // patterns: records / staging / pairs (64 B per event), carry-out candidates (32 B each) and the carried
-      // partials' working arrays, plus the bucket-stack spill rings and bounded buffers
-      const size_t nc = (size_t)qp->carry.n, wc = (size_t)std::max(qp->carry.width, 4);
-      need = std::max(need, cq.hdr.kind == 0 ? n / 8 + n / 1024 + (64 << 20)
-                                             : n * 64 + std::min<size_t>(n + nc, (size_t)1 << 26) * 32 +
-                                                   nc * (160 + 8 * wc) + ((size_t)640 << 20));
-    }
-    ensure_scratch(a, need);
-    std::vector<HostOut> douts;                 // this batch's outputs for their consumers, all queries
-    std::vector<std::vector<int64_t>> dkeep;    // host copies the records point into
+    std::vector<HostOut> douts;               // this batch's outputs for their consumers, all queries
+    std::vector<std::vector<int64_t>> dkeep;  // host copies the records point into
     a->out_arena.clear();
     try {
-    for (size_t qi = 0; qi < a->queries.size(); ++qi) {
-      QueryRt& q = *a->queries[qi];
-      const CompiledQuery& cq = q.cq;
-      if (std::find(cq.streams.begin(), cq.streams.end(), s) == cq.streams.end()) continue;
-      a->sc.used = 0;
-      const char* blob = (const char*)q.blob.p;
-      const bool consumed = outputs_consumed(a, q);
-      q.proj_ok = q.proj_nfa = false;
-      q.proj_desc = d;
-      q.proj_ts = d_ts;
-      q.proj_ord = d_ordinals;
-      q.proj_base = ordinal_base;
-      q.proj_n = (int64_t)n;
-      if (cq.hdr.kind == 0) {
-        q.dev_pairs.ensure(std::max<size_t>(n * 4, 16));
-        bool typed = false;
-        q.dev_n = filter_device(d, (const NfaStream*)a->d_streams.p, (int64_t)n,
-                                (const Instr*)(blob + cq.hdr.off_code) + cq.hdr.filt_off,
-                                (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.hdr.filt_off, cq.hdr.filt_len,
-                                (const DVal*)(blob + cq.hdr.off_const), (const DVal*)(cq.blob.data() + cq.hdr.off_const),
-                                d_ordinals, ordinal_base, (uint32_t*)q.dev_pairs.p, a->sc, hs,
-                                a->fast_timing ? &a->fast_tm : nullptr, &typed);
-        q.fast_path_used = typed ? 4 : 3;
-        q.prev_carry_n = 0;
-        q.proj_ok = true;
-        if (consumed) device_outputs(a, (int)qi, hs, douts, dkeep);
-        continue;
-      }
-      if (q.nfa_mode || q.nfa_used) {  // matching state held by the NFA kernel
-        q.dev_n = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs,
-                                   consumed ? &douts : nullptr);
-        q.fast_path_used = 5;
-        q.proj_nfa = true;
-        continue;
-      }
-      FastArgs fa{};
-      fa.n = (int64_t)n;
-      fa.ts = d_ts;
-      fa.st = (const NfaStream*)a->d_streams.p;
-      fa.key = cq.partition >= 0 ? (const KeyProg*)q.keyprogs.p : nullptr;
-      if (fa.key) {
-        const CompiledPartition& cp = *q.part;
-        int idx = (int)(std::find(cp.streams.begin(), cp.streams.end(), s) - cp.streams.begin());
-        fa.key = (const KeyProg*)q.keyprogs.p + idx;
-      }
-      fa.code = (const Instr*)(blob + cq.hdr.off_code);
-      fa.consts = (const DVal*)(blob + cq.hdr.off_const);
-      fa.c1_off = cq.fast_c1_off;
-      fa.c1_len = cq.fast_c1_len;
-      fa.c2_off = cq.fast_c2_off;
-      fa.c2_len = cq.fast_c2_len;
-      fa.within = cq.fast_within;
-      fa.ordinals = d_ordinals;
-      fa.ordinal_base = ordinal_base;
-      q.dev_pairs.ensure(std::max<size_t>((n + (size_t)q.carry.n) * 8, 16));
-      std::vector<int32_t> types(d.types, d.types + d.nattr);
-      FastHostInfo hi;
-      hi.cols = d_cols;
-      hi.types = types.data();
-      hi.vattr = fast_vattr(cq, types);
-      hi.c2_host = (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.fast_c2_off;
-      hi.c2_len = cq.fast_c2_len;
-      hi.c1_host = (const Instr*)(cq.blob.data() + cq.hdr.off_code) + cq.fast_c1_off;
-      hi.c1_len = cq.fast_c1_len;
-      if (hi.vattr >= 0) hi.vtype = types[hi.vattr];
-      hi.nattr = d.nattr;
-      if (fa.key) {
-        const CompiledPartition& cp = *q.part;
-        int idx = (int)(std::find(cp.streams.begin(), cp.streams.end(), s) - cp.streams.begin());
-        const auto& kc = cp.key_code[idx];
-        if (kc.size() == 1 && kc[0].op == OP_COL) {
-          hi.key_col = kc[0].a;
-          hi.key_type = types[hi.key_col];
-        }
-      }
-      q.prev_carry_n = q.carry.n;
-      q.prev_carry_w = q.carry.width;
-      if (q.carry.n > 0) {
-        const size_t cb = (size_t)q.carry.n * q.carry.width * 8;
-        q.prev_carry.ensure(cb);
-        SM_HIP(hipMemcpyAsync(q.prev_carry.p, q.carry.rows, cb, hipMemcpyDeviceToDevice, hs));
-      }
-      int64_t m = FAST_OUTSIDE;
-      if (!a->force_general_fast)
-        m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
-                                 a->fast_timing ? &a->fast_tm : nullptr, a->fast_stack);
-      q.fast_path_used = q.fast.last_path;
-      if (m == FAST_OUTSIDE && a->force_general_fast && q.carry.n == 0) {
-        // diagnostic (option "fast_general"): the stateless general closed form, one batch at a time
-        m = fast_every_within(fa, (uint32_t*)q.dev_pairs.p, (int64_t)n, a->sc, hs, a->fast_timing ? &a->fast_tm : nullptr);
-        q.fast_path_used = 1;
-      } else if (m < 0) {
-        // event time not monotone, or a condition outside the v2 envelope: the NFA kernel takes the query over
-        // (carried partials included) and keeps it, so later batches and host events see one matching state
-        m = nfa_device_batch(a, (int)qi, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs, consumed ? &douts : nullptr);
-        q.fast_path_used = 5;
-        q.proj_nfa = true;
-      }
-      q.dev_n = m;
-      q.proj_ok = q.fast_path_used != 5 && m >= 0;
-      if (q.proj_ok && consumed) device_outputs(a, (int)qi, hs, douts, dkeep);
-    }
-    if (!douts.empty()) {
-      a->need_outs = true;  // deliver() hands them out even when only the collect dump takes them
-      struct Reset {
-        bool& f;
-        ~Reset() { f = false; }
-      } reset_need{a->need_outs};
-      deliver(a, douts);
-    }
-    a->out_arena.clear();
+      device_batch_stream(a, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs, douts, dkeep);
+      deliver_device(a, douts);
     } catch (const std::exception& e) {
       a->failed = true;
       a->failed_why = std::string("a device batch failed half-way (") + e.what() +

@@ -196,9 +196,10 @@ def test_rejected_row_keeps_columns_aligned():
 
 def test_failed_batch_refuses_further_events_until_reset():
     """A batch that fails half-way (here: the output buffer option set too small) leaves the matching state
-    inconsistent; the app then refuses events instead of replaying the batch, until it is reset or restored."""
+    inconsistent; the app then refuses events instead of replaying the batch, until it is reset or restored. (A
+    sequence: an `every e1 -> e2` pattern would take the closed form, whose output has no such buffer.)"""
     from siddhi_amd.testing import EngineError, ProductApp
-    text = SCHEMA + ("@info(name='q') from every e1=S[price > 10] -> e2=S[price > e1.price] "
+    text = SCHEMA + ("@info(name='q') from every e1=S[price > 10], e2=S[price > e1.price] "
                      "select e1.price as p1, e2.price as p2 insert into O;")
     app = ProductApp(text, output_records=2)
     app.start()
