@@ -333,10 +333,15 @@ def via_input_handler(cols_dev, n, expect, chunk=None):
         best = dt if best is None else min(best, dt)
     path = ct.c_double()
     _lib.check(L.sm_app_get_stat(rt._h, b"fast_path:q", ct.byref(path)))
+    phases = {}
+    for ph in ("device", "outputs", "deliver", "callbacks", "upload_wait"):  # host time of the last run, per phase
+        v = ct.c_double()
+        _lib.check(L.sm_app_get_stat(rt._h, f"host_ms:{ph}".encode(), ct.byref(v)))
+        phases[ph] = v.value
     rt.shutdown()
     del cb
     return {"events": n, "value": n / best, "unit": "events/s", "ms": best * 1e3, "output_events": expect,
-            "fast_path": int(path.value), "host_bytes_per_event": 36,
+            "fast_path": int(path.value), "host_bytes_per_event": 36, "host_ms_last_run": phases,
             "note": "host columns -> sm_input_send_columns (InputHandler.send(Event[])) -> bucket-stack closed form in "
                     "chunks (H2D of the next chunk overlapped) -> StreamCallback counting every output Event; "
                     "best of 2, fresh runtime each"}
@@ -415,7 +420,7 @@ def main():
     import torch.distributed as dist
     from siddhi_amd.testing import ProductApp
     from siddhi_amd.shard import (clock_ticks, concat_ordered, exchange_with_ordinals, merge_heartbeats,
-                                  partitioned_step, slice_starts)
+                                  merge_outputs, partitioned_step, slice_starts)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -447,6 +452,8 @@ def main():
     torch.cuda.synchronize()
 
     opts = dict(cfg.get("options", {}))
+    if args.config == 5 and world > 1:
+        opts["keep_outputs"] = 1  # the output records of each batch stay on the device for the cross-rank merge
     if args.heap_words:
         opts["heap_words"] = args.heap_words
     app = ProductApp(cfg["app"], fast_stack=args.stack, **opts)
@@ -473,6 +480,10 @@ def main():
             # columns: symbol, price, volume (not read: aliased), timestamp attribute = global ordinal
             app.process_device_events(s_sid, s_ts, [s_sym, s_price, s_price, s_ord], ordinals=s_ord,
                                       hip_stream=hip_stream)
+            if world > 1:
+                # the reference's single output order across ranks (shard.merge_outputs): every output record to the
+                # rank that ingested its trigger, ordered there (timers of one clock advance in key creation order)
+                out_local[0] = merge_outputs(app.copy_device_outputs("q"), starts, N, world).shape[0]
             return int(app.get_stat("output_events:q"))
         # a fresh runtime of the app per step: the query's open partials (carried across device batches) dropped
         app.set_option("reset", 0)

@@ -21,6 +21,8 @@
  *                                   replayed as heartbeats among a rank's received events
  *   sm_unpack_records               multi-GPU receive side of the key exchange: packed records -> columns + global
  *                                   ordinals (no reference counterpart: one JVM has no exchange)
+ *   sm_app_copy_device_outputs      the ordered output records of the last interleaved device batch (multi-GPU merge)
+ *   sm_order_outputs                multi-GPU merge of per-rank output records into one JVM's delivery order
  *   sm_order_matches                multi-GPU merge of the per-rank outputs back into the single output order a
  *                                   query callback sees (QueryCallback.receive, query/output/callback/
  *                                   QueryCallback.java:51): no Java counterpart, one JVM has one output queue
@@ -150,7 +152,9 @@ int sm_app_set_option(sm_app* app, const char* key, int64_t value);
  * (or the collect dump is on), its outputs are also projected on the device and delivered as Events before the
  * call returns, in reference order, one callback call per input event that produced output
  * (OutputRateLimiter.sendToCallBacks :61 → StreamCallback.receive :65). `ordinals` (int64, may be NULL = base +
- * index) gives each event's global arrival ordinal (multi-GPU shards keep the ordinals of the unsharded stream). */
+ * index) gives each event's global arrival ordinal (multi-GPU shards keep the ordinals of the unsharded stream).
+ * hip_stream: the stream the batch was produced on (the call's work is ordered after it); NULL = the library waits
+ * for all work on the device first. The same holds for sm_app_process_device_events. */
 int sm_app_process_device_batch(sm_app* app, const char* stream_id, size_t n, const int64_t* d_timestamps,
                                 const void* const* d_cols, const int64_t* d_ordinals, int64_t ordinal_base,
                                 void* hip_stream);
@@ -203,12 +207,40 @@ int sm_order_matches(const uint64_t* d_pairs, size_t n, int64_t lo, int64_t hi, 
  * events (n; global ordinals d_ord ascending; stream index, event time and ncols columns of 4 or 8 bytes) merged
  * in ordinal order with the global clock-advance points (m; ordinals d_tick_ord ascending, clock d_tick_ts), a point
  * at an ordinal this rank holds dropped: the playback clock is global (StreamJunction.sendData :232-237) while a rank
- * holds only its keys' events, so it replays the other ranks' clock advances as heartbeats (stream index -1,
- * ordinal -1, zero attributes). Outputs hold n + m entries; *n_out = merged length. */
+ * holds only its keys' events, so it replays the other ranks' clock advances as heartbeats (stream index -1, zero
+ * attributes; its ordinal entry holds the ordinal of the event that advanced the clock, the trigger of the timers the
+ * heartbeat fires, see sm_app_copy_device_outputs). Outputs hold n + m entries; *n_out = merged length. */
 int sm_merge_heartbeats(size_t n, const int64_t* d_ord, const int32_t* d_sid, const int64_t* d_ts, int ncols,
                         const int32_t* widths, const void* const* d_src, size_t m, const int64_t* d_tick_ord,
                         const int64_t* d_tick_ts, int32_t* d_sid_out, int64_t* d_ts_out, int64_t* d_ord_out,
                         void* const* d_dst, size_t* n_out, void* hip_stream);
+/* The output records of the last sm_app_process_device_events batch of a query (needs option "keep_outputs" = 1 set
+ * before the batch), in the reference's delivery order: each record is *stride bytes, an sm_out_rec followed by the
+ * select values (nsel sm_dval) and the events' ordinals (int64), with pos = the ordinal of the output's trigger: the
+ * event whose processing emitted it, or for a timer the event that advanced the playback clock (a heartbeat's ordinal
+ * entry). *n = records; with d_dst == NULL only *n and *stride are set. The multi-GPU merge of config 5 sends each
+ * record to the rank whose ingest slice holds its trigger and orders the received runs with sm_order_outputs. */
+typedef struct sm_out_rec {
+  int64_t pos;     /* trigger ordinal */
+  int64_t time;    /* timer phase: the clock step; data phase: 0 (or a broadcast copy's rank + 1) */
+  int64_t create;  /* ordinal of the event that created the output's partition instance, -1 outside partitions */
+  int64_t ts;      /* output event timestamp */
+  int32_t phase;   /* 0 = fired by the clock advance before the trigger's own processing, 1 = the trigger's */
+  int32_t query;   /* query order in the app */
+  int32_t sched;
+  int32_t seq;     /* emission order within the instance */
+  int32_t key;     /* key slot (diagnostic, differs between apps) */
+  int32_t pad;
+} sm_out_rec;
+int sm_app_copy_device_outputs(sm_app* app, const char* query_name, void* d_dst, size_t cap_bytes, size_t* n,
+                               size_t* stride, void* hip_stream);
+/* Multi-GPU merge of output records (sm_app_copy_device_outputs layout, n of stride bytes): a concatenation of runs,
+ * each in delivery order, into the reference's delivery order (QueryCallback / StreamCallback order of one JVM):
+ * by trigger ordinal and phase, then for timer outputs by clock step and instance creation ordinal (the scheduler
+ * listeners' registration order, core/util/timestamp/EventTimeBasedMillisTimestampGenerator.java:99-116,
+ * core/partition/PartitionRuntime.java:256-309), records equal in all of these keeping their run order. d_out must
+ * not alias d_recs. */
+int sm_order_outputs(const void* d_recs, size_t n, size_t stride, void* d_out, void* hip_stream);
 /* Match tuples of the last device batch for a query: n pairs (e1, e2) of ordinals relative to the batch's
  * ordinal_base, uint32[2*n] in device memory, in reference output order (e2 ordinal, then e1 ordinal). */
 int sm_app_device_matches(sm_app* app, const char* query_name, const uint32_t** d_pairs, size_t* n);

@@ -554,6 +554,9 @@ struct Output {
   int64_t ts;
   std::vector<Value> vals;
   std::vector<int64_t> refs;
+  // place in the emission order (cr_output_order): trigger ordinal, phase, clock step, instance creation ordinal
+  int64_t trig = -1, step = 0, create = -1;
+  int phase = 1;
 };
 
 struct PartitionRt;
@@ -755,6 +758,7 @@ struct PartitionRt {
   std::vector<CExprP> key_owned;
   std::unordered_map<std::string, int> key_index;               // key -> instance idx
   std::vector<std::string> inst_key;                             // key of each instance, creation order
+  std::vector<int64_t> inst_create;                              // ordinal of the event that created it
   std::vector<std::vector<std::unique_ptr<QueryRt>>> instances;  // per key: one runtime per query
   // per stream the partition does not key: its receiver's cachedStreamJunctionMap (streamId + key → junction)
   std::map<std::string, JavaJunctionMap*> junction_maps;
@@ -781,6 +785,10 @@ struct OApp : cr_app {
   std::vector<std::unique_ptr<PartitionRt>> partitions;
   std::vector<Scheduler*> time_listeners;  // TimeChangeListener registration order
   int64_t next_ordinal = 0;
+  // what is being processed (cr_output_order): the trigger's ordinal, timer phase (0) or the event's own (1), the
+  // clock value of the advance that fires timers
+  int64_t cur_trig = -1, cur_step = 0;
+  int cur_phase = 1;
   bool collect = true;
   std::map<std::string, std::vector<Output>> stream_out;
   std::map<std::string, int64_t> stream_count;
@@ -1351,6 +1359,13 @@ void absent_timer(Pre* p, int64_t now) {
 }
 
 // ---------------------------------------------------------------- selector / output
+void set_order(const OApp* a, const QueryRt* q, Output& o) {
+  o.trig = a->cur_trig;
+  o.phase = a->cur_phase;
+  o.step = a->cur_phase == 0 ? a->cur_step : 0;
+  o.create = q->partitioned && q->part ? q->part->inst_create[(size_t)q->inst] : -1;
+}
+
 void selector_emit(QueryRt* q, const STP& s) {
   // QuerySelector.processNoGroupBy :124-167 → OutputRateLimiter → QueryCallback / InsertIntoStreamCallback
   OApp* a = q->app;
@@ -1368,6 +1383,7 @@ void selector_emit(QueryRt* q, const STP& s) {
   }
   c.outs = &o.vals;
   if (q->having && !truthy(eval(*q->having, c))) return;  // :138-139 complexEventChunk.remove()
+  set_order(a, q, o);
   a->stream_count[out]++;
   if (a->collect) {
     a->stream_out[out].push_back(o);
@@ -1389,6 +1405,7 @@ void selector_emit_row(QueryRt* q, const Row& row, int64_t ts) {
   }
   c.outs = &o.vals;
   if (q->having && !truthy(eval(*q->having, c))) return;  // QuerySelector.java:138-139
+  set_order(a, q, o);
   a->stream_count[out]++;
   if (a->collect) {
     a->stream_out[out].push_back(o);
@@ -1889,6 +1906,14 @@ void advance_clock(OApp* a, int64_t ts) {
   if (!a->playback) return;
   if (ts < a->clock) return;
   a->clock = ts;
+  const int phase = a->cur_phase;
+  a->cur_phase = 0;  // timers fired by this advance come before the event's own processing
+  a->cur_step = ts;
+  struct Restore {
+    OApp* a;
+    int phase;
+    ~Restore() { a->cur_phase = phase; }
+  } restore{a, phase};
   for (size_t k = 0; k < a->time_listeners.size(); ++k) {
     Scheduler* sc = a->time_listeners[k];
     if (!sc->queue.empty() && sc->queue.front() <= a->clock) {
@@ -1941,6 +1966,7 @@ void dispatch(OApp* a, int si, const RowP& row, int64_t ts) {
           inst = (int)pr->instances.size();
           pr->key_index.emplace(key, inst);
           pr->inst_key.push_back(key);
+          pr->inst_create.push_back(row->ordinal);
           pr->instances.emplace_back();
           for (size_t qi = 0; qi < pr->p->queries.size(); ++qi) {
             int order_index = 0;
@@ -1964,6 +1990,7 @@ void dispatch(OApp* a, int si, const RowP& row, int64_t ts) {
 }
 
 void send_row(OApp* a, int si, int64_t ts, RowP row) {
+  a->cur_trig = row->ordinal;
   advance_clock(a, ts);  // StreamJunction.sendData :232-237
   dispatch(a, si, row, ts);
 }
@@ -2221,6 +2248,7 @@ int cr_send_interleaved(cr_app* app, size_t n, const int32_t* stream_idx, const 
     for (size_t i = 0; i < n; ++i) {
       int si = stream_idx[i];
       if (si == -1) {  // playback heartbeat (the device batch's stream -1): clock only, no event
+        a->cur_trig = -1;
         advance_clock(a, ts[i]);
         continue;
       }
@@ -2234,9 +2262,48 @@ int cr_send_interleaved(cr_app* app, size_t n, const int32_t* stream_idx, const 
   return 0;
 }
 
+int cr_send_interleaved_ord(cr_app* app, size_t n, const int32_t* stream_idx, const int64_t* ts, const int64_t* ord,
+                            const void* const* cols, char* err, size_t errlen) {
+  OApp* a = static_cast<OApp*>(app);
+  try {
+    for (size_t i = 0; i < n; ++i) {
+      int si = stream_idx[i];
+      if (si == -1) {
+        a->cur_trig = ord[i];
+        advance_clock(a, ts[i]);
+        continue;
+      }
+      if (si < 0 || si >= (int)a->streams.size()) throw RuntimeError("bad stream index");
+      auto r = row_from_columns(a, a->streams[si].def, cols, i);
+      r->ordinal = ord[i];
+      a->next_ordinal = std::max(a->next_ordinal, ord[i] + 1);
+      send_row(a, si, ts[i], std::move(r));
+    }
+  } catch (const std::exception& e) {
+    set_err(err, errlen, e.what());
+    return 6;
+  }
+  return 0;
+}
+
+size_t cr_output_order(cr_app* app, const char* stream_id, int64_t* out, size_t cap) {
+  OApp* a = static_cast<OApp*>(app);
+  auto it = a->stream_out.find(stream_id ? stream_id : "");
+  if (it == a->stream_out.end()) return 0;
+  const auto& v = it->second;
+  for (size_t k = 0; k < v.size() && k < cap; ++k) {
+    out[4 * k] = v[k].trig;
+    out[4 * k + 1] = v[k].phase;
+    out[4 * k + 2] = v[k].step;
+    out[4 * k + 3] = v[k].create;
+  }
+  return v.size();
+}
+
 int cr_advance_time(cr_app* app, int64_t ts, char* err, size_t errlen) {
   OApp* a = static_cast<OApp*>(app);
   try {
+    a->cur_trig = -1;
     advance_clock(a, ts);
   } catch (const std::exception& e) {
     set_err(err, errlen, e.what());

@@ -42,6 +42,18 @@ int cr_send_columns(cr_app* app, int stream_index, size_t n, const int64_t* ts, 
  * stream_idx[i] == -1 is a playback heartbeat at ts[i] (as cr_advance_time; its columns are not read) */
 int cr_send_interleaved(cr_app* app, size_t n, const int32_t* stream_idx, const int64_t* ts, const void* const* cols,
                         char* err, size_t errlen);
+/* cr_send_interleaved with given arrival ordinals: event i gets ordinal ord[i] (a key-sharded rank's events keep the
+ * ordinals of the unsharded stream); a heartbeat's ord[i] is the ordinal of the event that advanced the global clock
+ * there (the trigger of the timers it fires, see cr_output_order). */
+int cr_send_interleaved_ord(cr_app* app, size_t n, const int32_t* stream_idx, const int64_t* ts, const int64_t* ord,
+                            const void* const* cols, char* err, size_t errlen);
+/* The place of each collected output of a stream in the reference's emission order, 4 int64 per output: the ordinal
+ * of its trigger (the input event whose processing emitted it; for a timer, the event whose arrival advanced the
+ * playback clock), its phase (0 = a timer fired by that clock advance, before the event itself is processed; 1 = the
+ * event's own processing), the clock value of the advance (phase 0; else 0) and the ordinal of the event that created
+ * its partition instance (-1 outside partitions). Test infrastructure for the multi-GPU output merge. Returns the
+ * output count; writes min(count, cap) entries. */
+size_t cr_output_order(cr_app* app, const char* stream_id, int64_t* out, size_t cap);
 /* Outputs collected since creation, as JSON text:
  * {"streams": {"<id>": [[ts, [values...], [refs...]], ...]},
  *  "queries": {"<name>": [[ts, [[values...], ...]], ...]}}

@@ -200,6 +200,25 @@ class SiddhiAppRuntime:
         calls (InputHandler.java:53 → StreamJunction.sendData :232). Filter queries and `every e1 -> e2 within T`
         patterns on the stream run on the GPU; their outputs reach the registered callbacks in the reference's
         order, one call per input event that produced output (sm_app_process_device_batch)."""
+        import torch
+        n = ts.numel()
+        for name, t in [("ts", ts), ("ordinals", ordinals)] + [(f"column {k}", c) for k, c in enumerate(cols)]:
+            if t is None:
+                continue
+            if not isinstance(t, torch.Tensor) or not t.is_cuda or not t.is_contiguous() or t.dim() != 1:
+                raise ValueError(f"sendDeviceBatch: {name} must be a contiguous 1-D tensor on the GPU")
+            if t.numel() != n:
+                raise ValueError(f"sendDeviceBatch: {name} holds {t.numel()} values for {n} events")
+        if ts.dtype != torch.int64 or (ordinals is not None and ordinals.dtype != torch.int64):
+            raise ValueError("sendDeviceBatch: event times and ordinals are int64 tensors")
+        schema = self.stream_schema(stream_id)
+        if len(cols) != len(schema):
+            raise ValueError(f"sendDeviceBatch: stream {stream_id} has {len(schema)} attributes, got {len(cols)}")
+        width = {0: 4, 1: 8, 2: 4, 3: 8, 4: 4, 5: 1}
+        for k, (c, t) in enumerate(zip(cols, schema)):
+            if c.element_size() != width[t]:
+                raise ValueError(f"sendDeviceBatch: column {k} has {c.element_size()}-byte elements, attribute type "
+                                 f"{_lib.TYPE_NAMES[t]} needs {width[t]}")
         ptrs = (ctypes.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
         check(lib().sm_app_process_device_batch(self._h, stream_id.encode(), ts.numel(), ts.data_ptr(), ptrs,
                                                 ordinals.data_ptr() if ordinals is not None else None,

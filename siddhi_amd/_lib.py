@@ -22,7 +22,7 @@ EXPORTS = [
     "sm_app_set_option", "sm_app_process_device_batch", "sm_app_process_device_events", "sm_app_device_matches",
     "sm_app_snapshot", "sm_app_restore", "sm_partition_by_owner", "sm_order_matches", "sm_app_copy_device_matches",
     "sm_app_get_stat", "sm_compile_dump", "sm_nfa_jit_compile", "sm_app_device_project", "sm_merge_heartbeats",
-    "sm_unpack_records", "sm_count_events_callback",
+    "sm_unpack_records", "sm_count_events_callback", "sm_app_copy_device_outputs", "sm_order_outputs",
 ]
 
 
@@ -82,6 +82,8 @@ def lib():
                                           ctypes.POINTER(vp), sz, vp, vp, vp, vp, vp, ctypes.POINTER(vp),
                                           ctypes.POINTER(sz), vp]
         L.sm_app_copy_device_matches.argtypes = [vp, cp, vp, sz, ctypes.POINTER(sz), vp]
+        L.sm_app_copy_device_outputs.argtypes = [vp, cp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz), vp]
+        L.sm_order_outputs.argtypes = [vp, sz, sz, vp, vp]
         L.sm_app_snapshot.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.sm_app_restore.argtypes = [vp, ctypes.c_char_p, sz]
         L.sm_app_device_matches.argtypes = [vp, cp, ctypes.POINTER(vp), ctypes.POINTER(sz)]

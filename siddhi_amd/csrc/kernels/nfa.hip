@@ -78,12 +78,13 @@ __global__ void __launch_bounds__(kLeBlock) lane_events_lds_kernel(NfaBatch b, i
 }
 
 // lo / hi of the data events' ordinals (markers carry -1): one atomic pair per workgroup
-__global__ void __launch_bounds__(256) ord_range_kernel(const int64_t* __restrict__ ord, int64_t n,
-                                                        unsigned long long* __restrict__ mm) {
+// range of the data events' ordinals (a heartbeat's entry, stream < 0, carries no event ordinal and is skipped)
+__global__ void __launch_bounds__(256) ord_range_kernel(const int64_t* __restrict__ ord, const int32_t* __restrict__ sid,
+                                                        int64_t n, unsigned long long* __restrict__ mm) {
   uint64_t lo = ~0ull, hi = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t o = ord[i];
-    if (o >= 0) {
+    if (o >= 0 && sid[i] >= 0) {
       lo = (uint64_t)o < lo ? (uint64_t)o : lo;
       hi = (uint64_t)o > hi ? (uint64_t)o : hi;
     }
@@ -155,7 +156,7 @@ bool lane_compact_ok(const NfaBatch& b, int64_t n, int32_t node_words, int nstre
   const unsigned long long init[2] = {~0ull, 0ull};
   SM_HIP(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(ord_range_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1024)), dim3(256), 0, s,
-                     b.ev_ord, n, mm);
+                     b.ev_ord, b.ev_stream, n, mm);
   unsigned long long h[2];
   SM_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));

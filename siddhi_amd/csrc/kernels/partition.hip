@@ -153,7 +153,7 @@ __global__ void tick_place_kernel(const int64_t* __restrict__ ord, int64_t n, co
   const int64_t p = (int64_t)kpos[j] + lower_bound_i64(ord, n, tord[j]);
   o.sid[p] = -1;
   o.ts[p] = tts[j];
-  o.ord[p] = -1;
+  o.ord[p] = tord[j];  // the ordinal of the event that advanced the clock: the trigger of the timers it fires
   for (int c = 0; c < o.ncols; ++c) {
     char* d = (char*)o.dst[c];
     if (o.width[c] == 4) ((uint32_t*)d)[p] = 0u;

@@ -56,9 +56,14 @@ void carry_rows_to_columns(const int64_t* rows, int64_t n, const CarryCols& c, h
 
 // One query's n output records (stride bytes each, OutRec first) in delivery order (runtime.cpp deliver): by
 // (pos, phase), then for timer-phase records (time, listener group, key creation ordinal); a lane's own records
-// keep their emission order (the sorts are stable and a lane's slots ascend). Returns the ordered copy (scratch).
+// keep their emission order (the sorts are stable and a lane's slots ascend). Returns the ordered copy (scratch, or
+// out_to). ev_clock null: the records' time always takes part (the multi-GPU merge: pos holds trigger ordinals of
+// pos_bits bits).
 const char* order_outputs(const char* recs, int64_t n, uint32_t stride, const int64_t* ev_clock, Scratch& sc,
-                          hipStream_t s);
+                          hipStream_t s, int pos_bits = 32, char* out_to = nullptr);
+
+// Output records' pos (batch position) -> ev_ord[pos] (the trigger's global ordinal).
+void trigger_ordinals(char* recs, int64_t n, uint32_t stride, const int64_t* ev_ord, hipStream_t s);
 
 int64_t build_event_index(int64_t n, const int32_t* sid, int32_t nstreams, const int64_t* ts, const int64_t* ord_in,
                           int64_t ord_base, bool playback, int64_t clock_in, int64_t* ev_row, int64_t* ev_ord,

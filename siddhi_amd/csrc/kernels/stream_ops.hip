@@ -915,7 +915,17 @@ __global__ void out_keys_kernel(const char* __restrict__ recs, int64_t n, uint32
   kt[i] = (uint64_t)r.time ^ 0x8000000000000000ull;
   kp[i] = ((uint64_t)r.pos << 1) | (uint64_t)(r.phase & 1);
   idx[i] = (uint32_t)i;
-  if (r.phase == 0 && r.time != ev_clock[r.pos]) atomicOr(flag, 1u);
+  if (r.phase == 0 && (!ev_clock || r.time != ev_clock[r.pos])) atomicOr(flag, 1u);
+}
+
+// pos (a batch position) -> the batch's ordinal there: the trigger's global ordinal (a heartbeat's entry is the
+// ordinal of the event that advanced the clock)
+__global__ void trigger_ordinals_kernel(char* __restrict__ recs, int64_t n, uint32_t stride,
+                                        const int64_t* __restrict__ ev_ord) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  OutRec& r = *(OutRec*)(recs + (size_t)i * stride);
+  r.pos = ev_ord[r.pos];
 }
 
 __global__ void gather_key_kernel(const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx, int64_t n,
@@ -935,8 +945,12 @@ __global__ void gather_records_kernel(const char* __restrict__ recs, const uint3
 
 }  // namespace
 
+void trigger_ordinals(char* recs, int64_t n, uint32_t stride, const int64_t* ev_ord, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(trigger_ordinals_kernel, grid_for(n), dim3(256), 0, s, recs, n, stride, ev_ord);
+}
+
 const char* order_outputs(const char* recs, int64_t n, uint32_t stride, const int64_t* ev_clock, Scratch& sc,
-                          hipStream_t s) {
+                          hipStream_t s, int pos_bits, char* out_to) {
   if (n >= (int64_t)UINT32_MAX) throw std::runtime_error("too many output records to order");
   if (stride % 8) throw std::logic_error("output record stride");
   uint64_t* kc = (uint64_t*)sc.take((size_t)n * 8);
@@ -946,7 +960,7 @@ const char* order_outputs(const char* recs, int64_t n, uint32_t stride, const in
   uint32_t* idx = (uint32_t*)sc.take((size_t)n * 4);
   uint32_t* idx2 = (uint32_t*)sc.take((size_t)n * 4);
   uint32_t* flag = (uint32_t*)sc.take(4);
-  char* out = (char*)sc.take((size_t)n * stride);
+  char* out = out_to ? out_to : (char*)sc.take((size_t)n * stride);
   SM_HIP(hipMemsetAsync(flag, 0, 4, s));
   hipLaunchKernelGGL(out_keys_kernel, grid_for(n), dim3(256), 0, s, recs, n, stride, ev_clock, kc, kt, kp, idx, flag);
   uint32_t hflag = 0;
@@ -966,7 +980,7 @@ const char* order_outputs(const char* recs, int64_t n, uint32_t stride, const in
   };
   pass(kc, 41, false);
   if (hflag) pass(kt, 64, true);
-  pass(kp, 33, true);  // positions < 2^32 (build_event_index)
+  pass(kp, pos_bits + 1, true);  // batch positions < 2^32 (build_event_index); trigger ordinals: 63 bits
   const uint32_t words = stride / 8;
   hipLaunchKernelGGL(gather_records_kernel, grid_for(n * words), dim3(256), 0, s, recs, cur, n, words, out);
   return out;

@@ -10,7 +10,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <charconv>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <deque>
@@ -21,6 +23,7 @@
 #include <memory>
 #include <mutex>
 #include <sstream>
+#include <thread>
 #include <string>
 #include <type_traits>
 #include <unordered_set>
@@ -115,33 +118,102 @@ struct HostOut {
   int64_t key_code = 0;      // partition queries: the instance's key code (an inner stream's routing key)
 };
 
+// Host copies of one query's device outputs (device_outputs), in its output order: the (e1, e2) tuples or a filter's
+// rows (ordinals relative to base), the select values and the timestamps, all in sm_app::out_arena.
+struct DevOut {
+  int qi;
+  int64_t m;
+  const uint32_t* hp;
+  const DVal* hv;
+  const int64_t* hts;
+  bool rows;
+  int64_t base;
+};
+
 struct Callback {
   sm_stream_callback scb = nullptr;
   sm_query_callback qcb = nullptr;
   void* user = nullptr;
 };
 
+// A growable array of trivially copyable elements whose growth does not initialise them (the Event arrays of a large
+// output batch are filled by several threads right after they are sized).
+template <typename T>
+struct RawVec {
+  static_assert(std::is_trivially_copyable<T>::value, "RawVec holds plain data");
+  std::unique_ptr<T[]> p;
+  size_t n = 0, cap = 0;
+  size_t size() const { return n; }
+  T* data() { return p.get(); }
+  const T* data() const { return p.get(); }
+  T& operator[](size_t i) { return p[i]; }
+  T* begin() { return p.get(); }
+  T* end() { return p.get() + n; }
+  void resize(size_t m) {
+    if (m > cap) {
+      const size_t c = std::max(m, cap + cap / 2);
+      std::unique_ptr<T[]> q(new T[c]);
+      if (n) memcpy(q.get(), p.get(), n * sizeof(T));
+      p.swap(q);
+      cap = c;
+    }
+    n = m;
+  }
+  void push_back(const T& v) {
+    resize(n + 1);
+    p[n - 1] = v;
+  }
+  void clear() { n = 0; }
+  void swap(RawVec& o) {
+    p.swap(o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+  }
+};
+
 // One output chunk ready for the callbacks: the events one trigger (an input event or a scheduler firing) made
 // one query emit, delivered as one StreamCallback.receive(Event[]) (StreamCallback.java:65-76) and one
-// QueryCallback.receive(timestamp, in, removed) (QueryCallback.java:52-74). Prepared under the app lock with
-// owned copies of everything the events point at, so the callbacks can run after the lock is released.
+// QueryCallback.receive(timestamp, in, removed) (QueryCallback.java:52-74). The chunks of one call share the arrays
+// of a Pending (no allocation per chunk or per event): its callbacks are cbs[cb_off, cb_off + n_cbs) (stream
+// callbacks of the output stream first, then query callbacks of the query), its events evs[ev_off, ev_off + n_ev).
 struct PreparedChunk {
   int64_t ts = 0;
-  std::vector<Callback> cbs;      // stream callbacks of the output stream, then query callbacks of the query
-  size_t n_stream_cbs = 0;
-  std::vector<sm_event> evs;
-  std::vector<sm_value> vals;
-  std::vector<std::unique_ptr<std::string>> strs;  // owned STRING values (stable addresses)
-  PreparedChunk() = default;
-  PreparedChunk(PreparedChunk&&) noexcept = default;
-  PreparedChunk& operator=(PreparedChunk&&) noexcept = default;
-  PreparedChunk(const PreparedChunk&) = delete;
-  PreparedChunk& operator=(const PreparedChunk&) = delete;
+  uint32_t cb_off = 0, n_cbs = 0, n_stream_cbs = 0;
+  uint64_t ev_off = 0, n_ev = 0;
 };
-// evs point into vals and vals into strs: chunks must only ever move (a vector grows by moving its elements only
-// when their move cannot throw; a copy would leave the pointers in the freed originals)
-static_assert(std::is_nothrow_move_constructible<PreparedChunk>::value && !std::is_copy_constructible<PreparedChunk>::value,
-              "PreparedChunk must move, never copy");
+
+// The outputs of one call, prepared under the app lock with owned copies of everything the events point at, so
+// the callbacks can run after the lock is released. Until finalise(), an event's data field holds the offset of its
+// values in vals (vals still grows); finalise() turns the offsets into pointers once the call's outputs are complete.
+struct Pending {
+  std::vector<PreparedChunk> chunks;
+  std::vector<Callback> cbs;
+  RawVec<sm_event> evs;
+  RawVec<sm_value> vals;
+  std::vector<std::unique_ptr<std::string>> strs;  // owned STRING values (stable addresses)
+  bool final_ = false;
+  void swap(Pending& o) {
+    chunks.swap(o.chunks);
+    cbs.swap(o.cbs);
+    evs.swap(o.evs);
+    vals.swap(o.vals);
+    strs.swap(o.strs);
+    std::swap(final_, o.final_);
+  }
+  void clear() {  // keeps the capacity (a bulk send reuses it chunk after chunk)
+    chunks.clear();
+    cbs.clear();
+    evs.clear();
+    vals.clear();
+    strs.clear();
+    final_ = false;
+  }
+  void finalise() {
+    if (final_) return;
+    for (auto& e : evs) e.data = vals.data() + (uintptr_t)e.data;
+    final_ = true;
+  }
+};
 
 struct QueryRt {
   CompiledQuery cq;
@@ -184,6 +256,11 @@ struct QueryRt {
   bool proj_nfa = false;
   DBuf nfa_proj;
   DBuf proj_out;  // device projection of a batch for its consumers (device_outputs)
+  // the last device-events batch's output records in delivery order, pos = trigger ordinal (option "keep_outputs":
+  // sm_app_copy_device_outputs, the multi-GPU merge)
+  DBuf ev_out;
+  int64_t ev_out_n = 0;
+  uint32_t ev_out_stride = 0;
   // overflow pool of per-key arenas (NfaBatch::pool, Lane::promote): allocated words, words handed out
   DBuf pool, pool_top_dev;
   int64_t pool_words = 0;
@@ -253,7 +330,8 @@ struct sm_app {
   std::vector<sm::CompiledPartition> parts;
   std::vector<std::unique_ptr<sm_input>> inputs;
   std::map<std::string, std::vector<sm::Callback>> stream_cbs, query_cbs;
-  std::vector<sm::PreparedChunk> pending;  // outputs of the current call, delivered once the lock is released
+  sm::Pending pending;  // outputs of the current call, delivered once the lock is released
+  sm::Pending bulk_spare;  // the Event arrays of bulk sends, kept for the next one
   bool failed = false;                      // a batch failed half-way: matching state is inconsistent
   std::string failed_why;
   // batch staging
@@ -275,6 +353,7 @@ struct sm_app {
   // 41.9 -> 57.8 GB of HBM traffic per launch; off by default.
   int64_t lane_balance = 0;
   int64_t out_records = 0;  // option "output_records" (0 = automatic)
+  bool keep_outputs = false;  // option "keep_outputs": device-events batches keep their ordered output records
   int nfa_jit = -1;         // option "nfa_jit": 1 = query-specialised NFA kernels (nfa_jit.cpp), 0 = the
                             // interpreter, -1 = automatic (batches of 2^20 query records or more)
   uint64_t text_hash = 0;   // FNV-1a of the SiddhiQL text (snapshots restore only into the same app)
@@ -309,6 +388,7 @@ struct sm_app {
   // no JSON dump, no callback, no chaining: outputs are copied to the host and counted, no HostOut is built
   bool outputs_unconsumed() const;
   bool need_outs = false;  // set while a caller reads the output records itself (nfa_device_batch)
+  bool in_device_events = false;  // inside sm_app_process_device_events (keep_outputs applies)
   hipStream_t stream = nullptr;
   int device = 0;  // the HIP device the app was created on (helper threads select it)
   // bulk columnar sends (bulk_send_device): minimum events for the direct path (option "bulk_min"), events per chunk
@@ -318,6 +398,10 @@ struct sm_app {
   hipStream_t copy_stream = nullptr;
   std::vector<sm::DBuf> bulk[2];
   bool bulk_active = false;  // a bulk send is in progress (a callback's own large send is staged instead)
+  // host-side time of the output path since the last reset (stat "host_ms:<phase>"): 0 device batches (including
+  // 1), 1 device projections copied out as records, 2 deliver (ordering + Event preparation), 3 callbacks of bulk
+  // sends, 4 bulk sends waiting for their next chunk's upload
+  double host_ms[5] = {0, 0, 0, 0, 0};
   sm::DBuf d_ev_stream, d_ev_row, d_ev_ts, d_ev_clock, d_ev_ord, d_adv_pos, d_adv_clock, d_adv_wall, d_adv_upto, d_streams,
       d_err, d_count,
       d_keyoff, scratch, d_rp, d_rp_streams;
@@ -350,13 +434,13 @@ int guarded(F&& f) {
   }
 }
 
-void run_callbacks(std::vector<PreparedChunk>& chunks);
+void run_callbacks(Pending& out);
 
 // Entry points that can produce outputs: run f under the app lock, then the callbacks of what it produced
 // without it.
 template <typename F>
 int locked(sm_app* a, F&& f) {
-  std::vector<PreparedChunk> out;
+  Pending out;
   int rc;
   {
     std::lock_guard<std::mutex> g(a->mu);
@@ -587,23 +671,48 @@ void json_val(std::ostringstream& o, const sm_app* a, const DVal& v, int t) {
   }
 }
 
-void to_sm_values(const sm_app* a, const HostOut& h, const CompiledQuery& cq, std::vector<sm_value>& out) {
-  out.resize(h.nvals);
-  for (int k = 0; k < h.nvals; ++k) {
+// Host threads for the output path: the process's CPU share (OMP_NUM_THREADS where the launcher sets it, e.g. 16 on
+// the GPU box, whose nproc shows the whole machine), at most 16.
+int host_threads() {
+  static const int t = [] {
+    int n = (int)std::thread::hardware_concurrency();
+    if (const char* e = getenv("OMP_NUM_THREADS")) n = std::min(n > 0 ? n : 1 << 30, std::max(1, atoi(e)));
+    return std::max(1, std::min(n, 16));
+  }();
+  return t;
+}
+
+// f(lo, hi) over [0, n) on up to host_threads() threads, at least `grain` items each.
+template <typename F>
+void parallel_for(size_t n, size_t grain, F&& f) {
+  const size_t t = std::min<size_t>((size_t)host_threads(), std::max<size_t>(n / std::max<size_t>(grain, 1), 1));
+  if (t <= 1) {
+    f((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(t - 1);
+  for (size_t w = 1; w < t; ++w) th.emplace_back([&, w] { f(n * w / t, n * (w + 1) / t); });
+  f((size_t)0, n / t);
+  for (auto& x : th) x.join();
+}
+
+void to_sm_values(const sm_app* a, const DVal* vals, int nvals, const CompiledQuery& cq, sm_value* out) {
+  for (int k = 0; k < nvals; ++k) {
     sm_value& v = out[k];
     int t = cq.sel_types[k];
     v.type = t;
-    v.is_null = h.vals[k].null;
+    v.is_null = vals[k].null;
     v.i = 0;
     v.d = 0;
     v.s = nullptr;
     if (v.is_null) continue;
-    if (t == T_FLOAT || t == T_DOUBLE) v.d = h.vals[k].d;
+    if (t == T_FLOAT || t == T_DOUBLE) v.d = vals[k].d;
     else if (t == T_STRING) {
-      int64_t id = h.vals[k].i;
+      int64_t id = vals[k].i;
       if (id < 0 || id >= (int64_t)a->dict.strs.size()) v.is_null = 1;
       else v.s = a->dict.strs[id].c_str();
-    } else v.i = h.vals[k].i;
+    } else v.i = vals[k].i;
   }
 }
 
@@ -647,11 +756,36 @@ bool out_before(const OutRec& x, const OutRec& y) {
   return x.query < y.query;
 }
 
+// The callbacks of one query as a range of pd.cbs, appended once per delivery: [offset, stream callbacks, all].
+std::array<int64_t, 3> query_callbacks(sm_app* a, const CompiledQuery& cq) {
+  Pending& pd = a->pending;
+  std::array<int64_t, 3> at{(int64_t)pd.cbs.size(), 0, 0};
+  auto it = a->stream_cbs.find(cq.insert_into);
+  if (it != a->stream_cbs.end())
+    for (auto& cb : it->second)
+      if (cb.scb) pd.cbs.push_back(cb);
+  at[1] = (int64_t)pd.cbs.size() - at[0];
+  if (cq.partition < 0) {  // partition clones do not inherit QueryCallbacks (PartitionRuntime)
+    auto qt = a->query_cbs.find(cq.name);
+    if (qt != a->query_cbs.end())
+      for (auto& cb : qt->second)
+        if (cb.qcb) pd.cbs.push_back(cb);
+  }
+  at[2] = (int64_t)pd.cbs.size() - at[0];
+  return at;
+}
+
 void deliver(sm_app* a, std::vector<HostOut>& outs) {
   if (a->outputs_unconsumed()) {  // nothing to hand out: the outputs were only counted
     a->out_arena.clear();
     return;
   }
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Tm {
+    sm_app* a;
+    std::chrono::steady_clock::time_point t0;
+    ~Tm() { a->host_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+  } tm{a, t0};
   auto key_less = [](const OutRec& x, const OutRec& y) { return out_before(x, y); };
   const auto before = [&](const HostOut& x, const HostOut& y) {
     if (key_less(x.r, y.r)) return true;
@@ -660,6 +794,13 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
   };
   // the device orders one query's records already (order_outputs); several queries' outputs still interleave here
   if (!std::is_sorted(outs.begin(), outs.end(), before)) std::stable_sort(outs.begin(), outs.end(), before);
+  std::vector<std::array<int64_t, 3>> qcb(a->queries.size(), std::array<int64_t, 3>{-1, 0, 0});
+  // pass 1 (in order): chunks, the collect dump, and each output's place in the Event arrays; pass 2 (threads): the
+  // Events themselves
+  Pending& pd = a->pending;
+  std::vector<int64_t> voff(outs.size(), -1), eoff(outs.size(), -1);
+  size_t nvals = pd.vals.size(), nevs = pd.evs.size();
+  bool strings = false;
   size_t i = 0;
   while (i < outs.size()) {
     size_t j = i + 1;  // the chunk: same trigger and emitting query instance
@@ -667,24 +808,19 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
            !key_less(outs[j].r, outs[i].r))
       ++j;
     const CompiledQuery& cq = a->queries[outs[i].qidx]->cq;
+    // this query's callbacks, appended to pd.cbs once per deliver()
+    auto& at = qcb[outs[i].qidx];
+    if (at[0] < 0) at = query_callbacks(a, cq);
+    const size_t nsel = cq.sel_types.size();
     PreparedChunk ch;
     ch.ts = outs[j - 1].r.ts;  // QueryCallback.receiveStreamEvent: the chunk's last event's timestamp
-    auto it = a->stream_cbs.find(cq.insert_into);
-    if (it != a->stream_cbs.end())
-      for (auto& cb : it->second)
-        if (cb.scb) ch.cbs.push_back(cb);
-    ch.n_stream_cbs = ch.cbs.size();
-    if (cq.partition < 0) {  // partition clones do not inherit QueryCallbacks (PartitionRuntime)
-      auto qt = a->query_cbs.find(cq.name);
-      if (qt != a->query_cbs.end())
-        for (auto& cb : qt->second)
-          if (cb.qcb) ch.cbs.push_back(cb);
-    }
-    const size_t nsel = cq.sel_types.size();
-    if (!ch.cbs.empty()) {
-      ch.vals.reserve((j - i) * nsel);
-      ch.evs.reserve(j - i);
-    }
+    ch.cb_off = (uint32_t)at[0];
+    ch.n_cbs = (uint32_t)at[2];
+    ch.n_stream_cbs = (uint32_t)at[1];
+    ch.ev_off = nevs;
+    ch.n_ev = j - i;
+    if (ch.n_cbs)
+      for (int t : cq.sel_types) strings |= t == T_STRING;
     for (size_t k = i; k < j; ++k) {
       HostOut& h = outs[k];
       if (a->collect) {
@@ -712,23 +848,33 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
           a->collected_queries[cq.name].push_back(qo.str());
         }
       }
-      if (ch.cbs.empty()) continue;
-      std::vector<sm_value> vals;
-      to_sm_values(a, h, cq, vals);
-      for (auto& v : vals)
-        if (v.type == T_STRING && !v.is_null) {
-          ch.strs.push_back(std::make_unique<std::string>(v.s));
-          v.s = ch.strs.back()->c_str();
-        }
-      ch.vals.insert(ch.vals.end(), vals.begin(), vals.end());
+      if (ch.n_cbs == 0) continue;
+      voff[k] = (int64_t)nvals;
+      eoff[k] = (int64_t)nevs++;
+      nvals += nsel;
     }
-    if (!ch.cbs.empty()) {
-      for (size_t k = i; k < j; ++k)
-        ch.evs.push_back(sm_event{outs[k].r.ts, ch.vals.data() + (k - i) * nsel, (int32_t)nsel});
-      a->pending.push_back(std::move(ch));
-    }
+    if (ch.n_cbs) pd.chunks.push_back(ch);
     i = j;
   }
+  pd.vals.resize(nvals);
+  pd.evs.resize(nevs);
+  parallel_for(outs.size(), (size_t)1 << 16, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      if (eoff[k] < 0) continue;
+      const HostOut& h = outs[k];
+      to_sm_values(a, h.vals, h.nvals, a->queries[h.qidx]->cq, pd.vals.data() + voff[k]);
+      pd.evs[eoff[k]] = sm_event{h.r.ts, (const sm_value*)(uintptr_t)voff[k], (int32_t)h.nvals};
+    }
+  });
+  if (strings)  // STRING values are owned by the pending outputs (the dictionary may change before the callbacks)
+    for (size_t k = 0; k < outs.size(); ++k)
+      for (int q = 0; eoff[k] >= 0 && q < outs[k].nvals; ++q) {
+        sm_value& v = pd.vals[voff[k] + q];
+        if (v.type == T_STRING && !v.is_null) {
+          pd.strs.push_back(std::make_unique<std::string>(v.s));
+          v.s = pd.strs.back()->c_str();
+        }
+      }
   a->out_arena.clear();  // the chunks own copies of everything they hand out
 }
 
@@ -736,12 +882,15 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
 // the same app (its outputs are delivered inside that send, as in the reference). Reference behaviour for a
 // callback that throws (caught and logged, StreamCallback.java:92-99) is the binding's business: C callbacks
 // cannot throw across the ABI.
-void run_callbacks(std::vector<PreparedChunk>& chunks) {
-  for (auto& ch : chunks) {
-    for (size_t c = 0; c < ch.cbs.size(); ++c) {
-      const Callback& cb = ch.cbs[c];
-      if (c < ch.n_stream_cbs) cb.scb(cb.user, ch.evs.data(), ch.evs.size());
-      else cb.qcb(cb.user, ch.ts, ch.evs.data(), ch.evs.size(), nullptr, 0);
+void run_callbacks(Pending& out) {
+  if (out.chunks.empty()) return;
+  out.finalise();
+  for (auto& ch : out.chunks) {
+    const sm_event* evs = out.evs.data() + ch.ev_off;
+    for (uint32_t c = 0; c < ch.n_cbs; ++c) {
+      const Callback& cb = out.cbs[ch.cb_off + c];
+      if (c < ch.n_stream_cbs) cb.scb(cb.user, evs, ch.n_ev);
+      else cb.qcb(cb.user, ch.ts, evs, ch.n_ev, nullptr, 0);
     }
   }
 }
@@ -966,9 +1115,19 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   // device (a few radix passes) instead of sorting it on the host
   const char* recs = (const char*)q.out.p;
   const size_t need = (size_t)nout * (48 + stride) + (16 << 20);  // keys, indices, ordered copy, sort passes
-  if (nout >= 2048 && a->sc.used + need <= a->sc.cap) {
+  const bool keep = a->keep_outputs && a->in_device_events;
+  if ((nout >= 2048 || (keep && nout > 1)) && a->sc.used + need <= a->sc.cap) {
     recs = order_outputs(recs, nout, (uint32_t)stride, ev.ev_clock, a->sc, hs);
     SM_HIP(hipStreamSynchronize(hs));
+  }
+  if (keep) {  // the ordered records with their triggers' global ordinals (sm_app_copy_device_outputs)
+    if (nout > 1 && recs == (const char*)q.out.p)
+      throw std::runtime_error("query '" + q.cq.name + "': too many output records to order for keep_outputs");
+    q.ev_out.ensure(std::max<size_t>((size_t)nout * stride, 16));
+    if (nout) SM_HIP(hipMemcpyAsync(q.ev_out.p, recs, (size_t)nout * stride, hipMemcpyDeviceToDevice, hs));
+    trigger_ordinals((char*)q.ev_out.p, nout, (uint32_t)stride, ev.ev_ord, hs);
+    q.ev_out_n = nout;
+    q.ev_out_stride = (uint32_t)stride;
   }
   read_outputs(a, qi, recs, nout, outs);
 }
@@ -1128,22 +1287,21 @@ bool outputs_consumed(const sm_app* a, const QueryRt& q) {
 // deliver(): QuerySelector.processNoGroupBy (:124-167) on the device (pair_project), one copy to the host, then
 // OutputRateLimiter.sendToCallBacks (:61) → StreamCallback.receive (:65) / QueryCallback through deliver(). Each
 // output's trigger is its e2 (a filter: its row), so deliver() makes one chunk per input event, as a sequence of
-// InputHandler.send calls would. `keep` owns the host copies the records point into.
-void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<HostOut>& outs,
-                    std::vector<std::vector<int64_t>>& keep) {
+// InputHandler.send calls would. The host copies the records point into live in sm_app::out_arena.
+void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<DevOut>& outs) {
+  const auto t0 = std::chrono::steady_clock::now();
   QueryRt& q = *a->queries[qi];
   const int64_t m = q.dev_n;
   if (m <= 0 || !q.proj_ok) return;
   const CompiledQuery& cq = q.cq;
   const bool rows = cq.hdr.kind == 0;
-  const int ns = cq.hdr.nsel, nr = cq.hdr.nrefs_vis;
-  const int32_t* rslots = (const int32_t*)(cq.blob.data() + cq.hdr.off_refs);
-  std::vector<uint32_t> hp((size_t)m * (rows ? 1 : 2));
-  SM_HIP(hipMemcpyAsync(hp.data(), q.dev_pairs.p, hp.size() * 4, hipMemcpyDeviceToHost, hs));
-  keep.emplace_back((size_t)m * (2 * ns + 1 + nr));  // DVal = two words each, then ts, then refs
-  int64_t* hv = keep.back().data();
-  int64_t* hts = hv + (size_t)m * 2 * ns;
-  int64_t* hrf = hts + m;
+  const int ns = cq.hdr.nsel;
+  const size_t np = (size_t)m * (rows ? 1 : 2);
+  uint32_t* hp = (uint32_t*)a->out_arena.take(np * 4);
+  SM_HIP(hipMemcpyAsync(hp, q.dev_pairs.p, np * 4, hipMemcpyDeviceToHost, hs));
+  // DVal values, then timestamps: pinned, reused across calls (sm_app::out_arena), not zero-filled
+  DVal* hv = (DVal*)a->out_arena.take((size_t)m * (ns * sizeof(DVal) + 8));
+  int64_t* hts = (int64_t*)(hv + (size_t)m * ns);
   q.proj_desc_dev.ensure(sizeof(NfaStream));
   SM_HIP(hipMemcpyAsync(q.proj_desc_dev.p, &q.proj_desc, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
   const int64_t chunk = std::min<int64_t>(m, (int64_t)1 << 22);
@@ -1156,34 +1314,110 @@ void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<HostOut>& out
     pair_project((const uint32_t*)q.dev_pairs.p + (rows ? k0 : 2 * k0), c, (const NfaStream*)q.proj_desc_dev.p,
                  q.proj_ord, q.proj_n, q.proj_base, q.proj_ts, (const int64_t*)q.prev_carry.p, q.prev_carry_n,
                  q.prev_carry_w, (const char*)q.blob.p, dv, dts, a->sc, hs, rows);
-    if (ns) SM_HIP(hipMemcpyAsync(hv + (size_t)k0 * 2 * ns, dv, (size_t)c * ns * sizeof(DVal), hipMemcpyDeviceToHost, hs));
+    if (ns) SM_HIP(hipMemcpyAsync(hv + (size_t)k0 * ns, dv, (size_t)c * ns * sizeof(DVal), hipMemcpyDeviceToHost, hs));
     SM_HIP(hipMemcpyAsync(hts + k0, dts, (size_t)c * 8, hipMemcpyDeviceToHost, hs));
   }
   SM_HIP(hipStreamSynchronize(hs));
-  outs.reserve(outs.size() + (size_t)m);
-  for (int64_t k = 0; k < m; ++k) {
-    const int64_t e1 = q.proj_base + (int32_t)hp[rows ? k : 2 * k];
-    const int64_t e2 = q.proj_base + (int32_t)hp[rows ? k : 2 * k + 1];
-    int64_t* rf = hrf + (size_t)k * nr;
-    for (int r = 0; r < nr; ++r) rf[r] = rslots[2 * r] == 0 ? e1 : e2;
-    HostOut h;
-    memset(&h.r, 0, sizeof(h.r));
-    h.r.pos = e2;
-    h.r.create = -1;
-    h.r.ts = hts[k];
-    h.r.phase = 1;
-    h.r.query = cq.hdr.query_order;
-    h.r.seq = (int32_t)k;
-    h.vals = (const DVal*)(hv + (size_t)k * 2 * ns);
-    h.nvals = ns;
-    h.refs = rf;
-    h.nrefs = nr;
-    h.qidx = qi;
-    h.e1 = e1;
-    h.e2 = e2;
-    outs.push_back(h);
-  }
+  outs.push_back(DevOut{qi, m, hp, hv, hts, rows, q.proj_base});
   q.n_out += m;
+  a->host_ms[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// HostOut records of device outputs (the general deliver(): several queries' outputs to interleave, or NFA records
+// to merge with): the trigger of each output is its e2 (a filter: its row), the hidden references its e1 / e2.
+void materialize(sm_app* a, const DevOut& d, std::vector<HostOut>& outs) {
+  const CompiledQuery& cq = a->queries[d.qi]->cq;
+  const int ns = cq.hdr.nsel, nr = cq.hdr.nrefs_vis;
+  const int32_t* rslots = (const int32_t*)(cq.blob.data() + cq.hdr.off_refs);
+  int64_t* hrf = (int64_t*)a->out_arena.take((size_t)std::max<int64_t>(d.m * nr, 1) * 8);
+  const size_t base = outs.size();
+  outs.resize(base + (size_t)d.m);
+  parallel_for((size_t)d.m, (size_t)1 << 16, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const int64_t e1 = d.base + (int32_t)d.hp[d.rows ? k : 2 * k];
+      const int64_t e2 = d.base + (int32_t)d.hp[d.rows ? k : 2 * k + 1];
+      int64_t* rf = hrf + k * nr;
+      for (int r = 0; r < nr; ++r) rf[r] = rslots[2 * r] == 0 ? e1 : e2;
+      HostOut& h = outs[base + k];
+      memset(&h.r, 0, sizeof(h.r));
+      h.r.pos = e2;
+      h.r.create = -1;
+      h.r.ts = d.hts[k];
+      h.r.phase = 1;
+      h.r.query = cq.hdr.query_order;
+      h.r.seq = (int32_t)k;
+      h.vals = d.hv + k * ns;
+      h.nvals = ns;
+      h.refs = rf;
+      h.nrefs = nr;
+      h.qidx = d.qi;
+      h.e1 = e1;
+      h.e2 = e2;
+    }
+  });
+}
+
+// One query's device outputs straight into Events (deliver_device when nothing else interleaves with them and no
+// dump is collected): they are in reference order already (e2, then e1; a filter's rows in order), one chunk per
+// trigger = per run of equal e2. No HostOut, no comparison sort; the Events are built by several threads.
+void deliver_direct(sm_app* a, const DevOut& d) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const CompiledQuery& cq = a->queries[d.qi]->cq;
+  const int ns = cq.hdr.nsel;
+  Pending& pd = a->pending;
+  const std::array<int64_t, 3> at = query_callbacks(a, cq);
+  if (at[2] == 0) return;
+  const size_t m = (size_t)d.m;
+  auto trig = [&](size_t k) { return d.rows ? d.hp[k] : d.hp[2 * k + 1]; };
+  // chunk starts: counted per thread range, then written at their ranks
+  const size_t T = std::min<size_t>((size_t)host_threads(), std::max<size_t>(m >> 16, 1));
+  std::vector<size_t> cnt(T + 1, 0);
+  parallel_for(T, 1, [&](size_t lo, size_t hi) {
+    for (size_t t = lo; t < hi; ++t) {
+      size_t c = 0;
+      for (size_t k = m * t / T; k < m * (t + 1) / T; ++k) c += k == 0 || trig(k) != trig(k - 1);
+      cnt[t + 1] = c;
+    }
+  });
+  for (size_t t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+  const size_t c0 = pd.chunks.size(), e0 = pd.evs.size(), v0 = pd.vals.size();
+  pd.chunks.resize(c0 + cnt[T]);
+  pd.evs.resize(e0 + m);
+  pd.vals.resize(v0 + m * ns);
+  parallel_for(T, 1, [&](size_t lo, size_t hi) {
+    for (size_t t = lo; t < hi; ++t) {
+      size_t c = c0 + cnt[t];
+      const size_t kb = m * t / T, ke = m * (t + 1) / T;
+      for (size_t k = kb; k < ke; ++k) {
+        to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
+        pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
+        if (k == 0 || trig(k) != trig(k - 1)) {
+          PreparedChunk& ch = pd.chunks[c++];
+          ch.cb_off = (uint32_t)at[0];
+          ch.n_cbs = (uint32_t)at[2];
+          ch.n_stream_cbs = (uint32_t)at[1];
+          ch.ev_off = e0 + k;
+        }
+      }
+    }
+  });
+  for (size_t c = c0; c < pd.chunks.size(); ++c) {  // sizes and timestamps (the chunk's last event's)
+    PreparedChunk& ch = pd.chunks[c];
+    const size_t end = c + 1 < pd.chunks.size() ? pd.chunks[c + 1].ev_off : e0 + m;
+    ch.n_ev = end - ch.ev_off;
+    ch.ts = pd.evs[end - 1].timestamp;
+  }
+  bool strings = false;
+  for (int t : cq.sel_types) strings |= t == T_STRING;
+  if (strings)  // STRING values are owned by the pending outputs (the dictionary may change before the callbacks)
+    for (size_t k = v0; k < pd.vals.size(); ++k) {
+      sm_value& v = pd.vals[k];
+      if (v.type == T_STRING && !v.is_null) {
+        pd.strs.push_back(std::make_unique<std::string>(v.s));
+        v.s = pd.strs.back()->c_str();
+      }
+    }
+  a->host_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // Host side of one batch in arrival order: the staged input (flush), or a chaining level's merged batch.
@@ -1444,6 +1678,7 @@ void run_level(sm_app* a, std::vector<StreamStage>& stages, const EvHost& e, int
     if (q.level != level || q.bcast) continue;
     const DQuery& h = q.cq.hdr;
     a->sc.used = 0;
+    q.proj_ok = q.proj_nfa = false;  // host-staged outputs: nothing for sm_app_device_project
     size_t stride = sizeof(OutRec) + h.nsel * sizeof(DVal) + h.nrefs * sizeof(int64_t);
     const size_t first = outs.size();
     if (h.kind == 0) {
@@ -1662,10 +1897,10 @@ void run_chained(sm_app* a, std::vector<HostOut>& outs) {
 
 // The device-batch path of one stream (sm_app_process_device_batch, and host-API batches of apps whose queries all
 // take it: flush_device): every query reading stream s runs over the n events (columns, event times and ordinals
-// in device memory) on hs; the outputs that have consumers are appended to douts (their host copies in dkeep).
+// in device memory) on hs; the outputs that have consumers are appended to douts (host copies in out_arena).
 void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const void* const* d_cols,
                          const int64_t* d_ordinals, int64_t ordinal_base, hipStream_t hs, std::vector<HostOut>& douts,
-                         std::vector<std::vector<int64_t>>& dkeep) {
+                         std::vector<DevOut>& draw) {
   if (a->max_level > 0)
     throw sql::UnsupportedError("apps whose queries read streams other queries fill run through the host API");
   for (auto& bc : a->part_bcast)
@@ -1722,7 +1957,7 @@ void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const 
       q.fast_path_used = typed ? 4 : 3;
       q.prev_carry_n = 0;
       q.proj_ok = true;
-      if (consumed) device_outputs(a, (int)qi, hs, douts, dkeep);
+      if (consumed) device_outputs(a, (int)qi, hs, draw);
       continue;
     }
     if (q.nfa_mode || q.nfa_used) {  // matching state held by the NFA kernel
@@ -1797,20 +2032,25 @@ void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const 
     }
     q.dev_n = m;
     q.proj_ok = q.fast_path_used != 5 && m >= 0;
-    if (q.proj_ok && consumed) device_outputs(a, (int)qi, hs, douts, dkeep);
+    if (q.proj_ok && consumed) device_outputs(a, (int)qi, hs, draw);
   }
 }
 
 // Outputs of device-batch queries to their consumers (deliver() hands them out even when only the collect dump
 // takes them).
-void deliver_device(sm_app* a, std::vector<HostOut>& douts) {
-  if (!douts.empty()) {
+void deliver_device(sm_app* a, std::vector<HostOut>& douts, std::vector<DevOut>& draw) {
+  if (!douts.empty() || !draw.empty()) {
     a->need_outs = true;
     struct Reset {
       bool& f;
       ~Reset() { f = false; }
     } reset_need{a->need_outs};
-    deliver(a, douts);
+    if (douts.empty() && draw.size() == 1 && !a->collect) {
+      deliver_direct(a, draw[0]);
+    } else {
+      for (const DevOut& d : draw) materialize(a, d, douts);
+      deliver(a, douts);
+    }
   }
   a->out_arena.clear();
 }
@@ -1845,7 +2085,7 @@ bool host_batch_device_ok(const sm_app* a) {
 // Heartbeats and the start record carry no event: no query of such an app reads them.
 void flush_device(sm_app* a) {
   std::vector<HostOut> douts;
-  std::vector<std::vector<int64_t>> dkeep;
+  std::vector<DevOut> draw;
   a->out_arena.clear();
   for (size_t s = 0; s < a->streams.size(); ++s) {
     StreamStage& st = a->streams[s];
@@ -1870,10 +2110,10 @@ void flush_device(sm_app* a) {
     upload(a, st.drow_ts, rts);
     if (!contiguous) upload(a, st.drow_ord, rord);
     device_batch_stream(a, (int)s, (size_t)R, (const int64_t*)st.drow_ts.p, dc.data(),
-                        contiguous ? nullptr : (const int64_t*)st.drow_ord.p, rord[0], a->stream, douts, dkeep);
+                        contiguous ? nullptr : (const int64_t*)st.drow_ord.p, rord[0], a->stream, douts, draw);
   }
   SM_HIP(hipStreamSynchronize(a->stream));
-  deliver_device(a, douts);
+  deliver_device(a, douts, draw);
 }
 
 
@@ -1903,20 +2143,33 @@ int bulk_send_device(sm_app* a, int s, size_t n, const int64_t* ts, const void* 
     SM_HIP(hipMemcpyAsync(a->bulk[b][nattr].p, ts + lo, len * 8, hipMemcpyHostToDevice, cs));
     SM_HIP(hipStreamSynchronize(cs));
   };
+  Pending out;  // the chunks' outputs; its arrays are reused from chunk to chunk and from call to call
+  {
+    std::lock_guard<std::mutex> g(a->mu);
+    out.swap(a->bulk_spare);
+  }
   struct Done {  // the upload in flight finishes before the buffers can be reused or freed
     sm_app* a;
     std::future<void>& f;
+    Pending& out;
     ~Done() {
       if (f.valid()) f.wait();
       std::lock_guard<std::mutex> g(a->mu);
       a->bulk_active = false;
+      out.clear();
+      a->bulk_spare.swap(out);
     }
-  } done{a, next};
+  } done{a, next, out};
   int rc = SM_OK;
+  std::vector<HostOut> douts;
+  std::vector<DevOut> draw;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   for (size_t c = 0; c < nchunks && rc == SM_OK; ++c) {
-    std::vector<PreparedChunk> out;
     {
       std::lock_guard<std::mutex> g(a->mu);
+      out.clear();
+      a->pending.swap(out);  // a->pending is empty between calls: it takes the reused arrays
       rc = guarded([&] {
         if (a->failed) throw std::runtime_error(a->failed_why);
         flush(a);  // events staged before this chunk (earlier sends, or callbacks of the previous chunk) come first
@@ -1931,17 +2184,21 @@ int bulk_send_device(sm_app* a, int s, size_t n, const int64_t* ts, const void* 
         }
         const size_t lo = c * B, len = std::min(B, n - lo);
         const int b = (int)(c & 1);
+        const auto tw = clk::now();
         next.get();  // chunk c is on the device (rethrows an upload error)
+        a->host_ms[4] += ms_since(tw);
         if (c + 1 < nchunks) next = std::async(std::launch::async, upload_chunk, lo + B, std::min(B, n - lo - B), b ^ 1);
         std::vector<const void*> dc(nattr);
         for (int k = 0; k < nattr; ++k) dc[k] = a->bulk[b][k].p;
-        std::vector<HostOut> douts;
-        std::vector<std::vector<int64_t>> dkeep;
+        douts.clear();
+        draw.clear();
         a->out_arena.clear();
         try {
+          const auto td = clk::now();
           device_batch_stream(a, s, len, (const int64_t*)a->bulk[b][nattr].p, dc.data(), nullptr, a->next_ordinal,
-                              a->stream, douts, dkeep);
-          deliver_device(a, douts);
+                              a->stream, douts, draw);
+          a->host_ms[0] += ms_since(td);
+          deliver_device(a, douts, draw);
         } catch (const std::exception& e) {
           a->failed = true;
           a->failed_why = std::string("a batch failed half-way (") + e.what() +
@@ -1956,7 +2213,9 @@ int bulk_send_device(sm_app* a, int s, size_t n, const int64_t* ts, const void* 
       });
       out.swap(a->pending);
     }
+    const auto tc = clk::now();
     run_callbacks(out);
+    a->host_ms[3] += ms_since(tc);
   }
   return rc;
 }
@@ -2417,6 +2676,7 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       SM_HIP(hipStreamSynchronize(a->stream));
       a->clock = a->clock_batch_in = 0;
       a->next_ordinal = a->ordinal_base = 0;
+      for (double& t : a->host_ms) t = 0;
       a->started = false;
       a->failed = false;
       a->failed_why.clear();
@@ -2430,6 +2690,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       }
     } else if (k == "output_records") {
       a->out_records = std::max<int64_t>(0, value);
+    } else if (k == "keep_outputs") {
+      a->keep_outputs = value != 0;
     } else if (k == "bulk_min") {
       a->bulk_min = std::max<int64_t>(1, value);
     } else if (k == "bulk_chunk") {
@@ -2450,12 +2712,15 @@ int sm_app_process_device_batch(sm_app* a, const char* stream_id, size_t n, cons
     if (s < 0) throw sql::ValidationError("unknown stream");
     flush(a);  // staged host events come first (arrival order)
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
-    std::vector<HostOut> douts;               // this batch's outputs for their consumers, all queries
-    std::vector<std::vector<int64_t>> dkeep;  // host copies the records point into
+    // no stream given: the batch may still be in the making on any stream of the caller (the app's own stream does
+    // not wait for the legacy default stream), so all device work completes before it is read
+    if (!hip_stream) SM_HIP(hipDeviceSynchronize());
+    std::vector<HostOut> douts;               // this batch's outputs for their consumers: NFA records
+    std::vector<DevOut> draw;                 // and host copies of closed-form / filter device outputs
     a->out_arena.clear();
     try {
-      device_batch_stream(a, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs, douts, dkeep);
-      deliver_device(a, douts);
+      device_batch_stream(a, s, n, d_ts, d_cols, d_ordinals, ordinal_base, hs, douts, draw);
+      deliver_device(a, douts, draw);
     } catch (const std::exception& e) {
       a->failed = true;
       a->failed_why = std::string("a device batch failed half-way (") + e.what() +
@@ -2480,6 +2745,9 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
     for (auto& bc : a->part_bcast)
       if (!bc.empty()) throw sql::UnsupportedError("partitions reading unkeyed streams run through the host API");
     hipStream_t hs = hip_stream ? (hipStream_t)hip_stream : a->stream;
+    // no stream given: the batch may still be in the making on any stream of the caller (the app's own stream does
+    // not wait for the legacy default stream), so all device work completes before it is read
+    if (!hip_stream) SM_HIP(hipDeviceSynchronize());
     // every stream a query reads must carry the batch schema (the schema of the first such stream)
     const std::vector<sql::Attribute>* schema = nullptr;
     for (auto& qp : a->queries) {
@@ -2540,9 +2808,15 @@ int sm_app_process_device_events(sm_app* a, size_t n, const int32_t* d_stream_id
                       (const int64_t*)a->d_adv_clock.p, (const int64_t*)a->d_adv_wall.p, (const int64_t*)a->d_adv_upto.p,
                       nadv, a->clock};
     std::vector<HostOut> outs;
+    a->in_device_events = true;
+    struct Reset {
+      bool& f;
+      ~Reset() { f = false; }
+    } reset_in{a->in_device_events};
     for (size_t qi = 0; qi < a->queries.size(); ++qi) {
       a->sc.used = 0;
       a->queries[qi]->n_out = 0;
+      a->queries[qi]->ev_out_n = 0;
       run_pattern_query(a, (int)qi, ev, N, outs, hs, tm);
       a->queries[qi]->dev_n = a->queries[qi]->n_out;
     }
@@ -2884,6 +3158,44 @@ int sm_order_matches(const uint64_t* d_pairs, size_t n, int64_t lo, int64_t hi, 
   });
 }
 
+// Multi-GPU output merge (siddhi_amd/shard.py order_outputs): runs of output records, each in delivery order, into
+// the reference's delivery order. Records as sm_app_copy_device_outputs writes them (pos = trigger ordinal).
+static_assert(sizeof(sm_out_rec) == sizeof(sm::OutRec) && offsetof(sm_out_rec, phase) == offsetof(sm::OutRec, phase),
+              "sm_out_rec mirrors the device output record");
+
+int sm_order_outputs(const void* d_recs, size_t n, size_t stride, void* d_out, void* hip_stream) {
+  return guarded([&] {
+    if (n == 0) return;
+    if (stride < sizeof(sm::OutRec) || stride % 8) throw std::invalid_argument("order_outputs: bad record stride");
+    if (d_recs == d_out) throw std::invalid_argument("order_outputs: output must not alias the input");
+    HelperScratch& h = helper_scratch(n * 48 + (32 << 20));
+    HelperLock lk{h};
+    sm::order_outputs((const char*)d_recs, (int64_t)n, (uint32_t)stride, nullptr, h.sc, (hipStream_t)hip_stream, 62,
+                      (char*)d_out);
+    SM_HIP(hipStreamSynchronize((hipStream_t)hip_stream));
+  });
+}
+
+int sm_app_copy_device_outputs(sm_app* a, const char* query_name, void* d_dst, size_t cap_bytes, size_t* n,
+                               size_t* stride, void* hip_stream) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    if (!a->keep_outputs) throw std::invalid_argument("copy_device_outputs needs option keep_outputs = 1");
+    for (auto& q : a->queries)
+      if (q->cq.name == query_name) {
+        const size_t st = sizeof(OutRec) + q->cq.hdr.nsel * sizeof(DVal) + q->cq.hdr.nrefs * sizeof(int64_t);
+        const size_t bytes = (size_t)q->ev_out_n * st;
+        *n = (size_t)q->ev_out_n;
+        if (stride) *stride = st;
+        if (!d_dst) return;
+        if (bytes > cap_bytes) throw std::invalid_argument("copy_device_outputs: destination too small");
+        if (bytes) SM_HIP(hipMemcpyAsync(d_dst, q->ev_out.p, bytes, hipMemcpyDeviceToDevice, (hipStream_t)hip_stream));
+        return;
+      }
+    throw sql::ValidationError(std::string("No query with name ") + query_name);
+  });
+}
+
 int sm_app_get_stat(sm_app* a, const char* key, double* out) {
   std::lock_guard<std::mutex> g(a->mu);
   return guarded([&] {
@@ -2936,6 +3248,14 @@ int sm_app_get_stat(sm_app* a, const char* key, double* out) {
         }
       *out = calls ? cnt : tot;
       return;
+    }
+    if (k.rfind("host_ms:", 0) == 0) {
+      static const char* names[5] = {"device", "outputs", "deliver", "callbacks", "upload_wait"};
+      for (int i = 0; i < 5; ++i)
+        if (k.substr(8) == names[i]) {
+          *out = a->host_ms[i];
+          return;
+        }
     }
     throw std::invalid_argument("unknown stat " + k);
   });

@@ -330,7 +330,8 @@ def clock_ticks(ts: torch.Tensor, lo: int, world: int, group=None) -> torch.Tens
 
 def merge_heartbeats(sid: torch.Tensor, ts: torch.Tensor, columns, ords: torch.Tensor, ticks: torch.Tensor):
     """A rank's received events (global ordinals `ords` ascending) merged with the global clock-advance points
-    (`ticks` from clock_ticks) in ordinal order, as heartbeats (stream index -1, ordinal -1, zero attributes) for
+    (`ticks` from clock_ticks) in ordinal order, as heartbeats (stream index -1, zero attributes, ordinal = that of the
+    event that advanced the clock there: the trigger of the timers the heartbeat fires) for
     sm_app_process_device_events; a point at an ordinal this rank holds is dropped (that event advances the clock
     itself). GPU tensors: the HIP merge of the native library (sm_merge_heartbeats: binary-search merge path, no
     sort); host tensors (gloo tests): the same merge with torch.searchsorted. Returns (sid, ts, columns, ords)."""
@@ -377,12 +378,64 @@ def merge_heartbeats(sid: torch.Tensor, ts: torch.Tensor, columns, ords: torch.T
     o_ts[ev_at] = ts
     o_ts[tick_at] = kts
     o_ord[ev_at] = ords
+    o_ord[tick_at] = kt  # a heartbeat carries the ordinal of the event that advanced the clock (its timers' trigger)
     outs = []
     for c in columns:
         o = torch.zeros(L, dtype=c.dtype)
         o[ev_at] = c
         outs.append(o)
     return o_sid, o_ts, outs, o_ord
+
+
+def route_outputs(recs: torch.Tensor, starts, n_total: int, world: int, group=None) -> torch.Tensor:
+    """Multi-GPU config 5: send every output record (int64 rows of the sm_app_copy_device_outputs
+    layout, column 0 = the trigger's global ordinal, this rank's records in delivery order, so ascending in column 0)
+    to the rank whose ingest slice holds its trigger (one all-to-all-v; split points by binary search). Returns the
+    received rows: one run per source rank, in rank order."""
+    if world == 1:
+        return recs
+    W = recs.shape[1]
+    trig = recs[:, 0].contiguous()
+    bnd = torch.searchsorted(trig, torch.tensor(starts[1:], dtype=torch.int64, device=recs.device))
+    cuts = [0] + bnd.tolist() + [recs.shape[0]]
+    sc = [(cuts[r + 1] - cuts[r]) * W for r in range(world)]
+    rc = _all_to_all_counts(sc, recs.device, group)
+    buf = torch.empty(sum(rc), dtype=torch.int64, device=recs.device)
+    dist.all_to_all_single(buf, recs.contiguous().view(-1), rc, sc, group=group)
+    return buf.view(-1, W)
+
+
+def order_outputs(recs: torch.Tensor) -> torch.Tensor:
+    """Runs of output records, each in delivery order, into the reference's delivery order for their triggers: one
+    JVM calls its callbacks per trigger event in arrival order, the clock advance's timers first, those in scheduler
+    listener registration order = partition instance creation order (EventTimeBasedMillisTimestampGenerator
+    .setCurrentTimestamp core/util/timestamp/EventTimeBasedMillisTimestampGenerator.java:99-116; instances created in
+    PartitionRuntime.cloneIfNotExist core/partition/PartitionRuntime.java:256-309). Stable sorts by the instance
+    creation ordinal (column 2), the clock step (column 1), then (trigger ordinal, phase) (column 0, low half of
+    column 4): records equal in all of them come from one instance and keep their run order. GPU: sm_order_outputs
+    (radix passes); host tensors: the same passes with torch's stable sort."""
+    if recs.shape[0] <= 1:
+        return recs
+    if recs.is_cuda:
+        import ctypes
+        from siddhi_amd import _lib
+        out = torch.empty_like(recs)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(recs.device).cuda_stream)
+        rc = _lib.lib().sm_order_outputs(recs.data_ptr(), recs.shape[0], recs.shape[1] * 8, out.data_ptr(), stream)
+        if rc != _lib.SM_OK:
+            raise RuntimeError(_lib.lib().sm_last_error().decode(errors="replace"))
+        return out
+    idx = torch.arange(recs.shape[0])
+    phase = recs[:, 4] & 0xFFFFFFFF
+    for key in (recs[:, 2] + 1, recs[:, 1], recs[:, 0] * 2 + phase):  # least significant first
+        idx = idx[torch.sort(key[idx], stable=True).indices]
+    return recs[idx]
+
+
+def merge_outputs(recs: torch.Tensor, starts, n_total: int, world: int, group=None) -> torch.Tensor:
+    """route_outputs + order_outputs: this rank's slice of the single-process output sequence (the ranks' results
+    concatenated in rank order are the one-JVM delivery order)."""
+    return order_outputs(route_outputs(recs, starts, n_total, world, group))
 
 
 def merge_matches(parts):

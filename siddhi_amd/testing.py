@@ -158,6 +158,22 @@ class ProductApp:
                                                dst.numel() * dst.element_size(), ctypes.byref(n), s))
         return n.value
 
+    def copy_device_outputs(self, query):
+        """The last interleaved device batch's output records (option keep_outputs) as an int64 device tensor
+        (n, stride / 8) in delivery order: sm_out_rec (pos = trigger ordinal) + select values + ordinals."""
+        import torch
+        n = ctypes.c_size_t()
+        st = ctypes.c_size_t()
+        _call(lib().sm_app_copy_device_outputs(self.h, query.encode(), None, 0, ctypes.byref(n), ctypes.byref(st),
+                                               None))
+        dev = torch.device("cuda", torch.cuda.current_device())
+        out = torch.empty((max(n.value, 1), st.value // 8), dtype=torch.int64, device=dev)
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _call(lib().sm_app_copy_device_outputs(self.h, query.encode(), ctypes.c_void_p(out.data_ptr()),
+                                               out.numel() * 8, ctypes.byref(n), ctypes.byref(st), s))
+        torch.cuda.synchronize()
+        return out[:n.value]
+
     def get_stat(self, key):
         v = ctypes.c_double()
         _call(lib().sm_app_get_stat(self.h, key.encode(), ctypes.byref(v)))

@@ -33,6 +33,11 @@ def lib():
                                       ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_size_t]
         L.cr_send_interleaved.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_size_t]
+        L.cr_send_interleaved_ord.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p,
+                                              ctypes.c_size_t]
+        L.cr_output_order.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t]
+        L.cr_output_order.restype = ctypes.c_size_t
         L.cr_advance_time.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_size_t]
         L.cr_advance_wallclock.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_size_t]
         L.cr_dump_outputs.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
@@ -118,6 +123,29 @@ class OracleApp:
         rc = lib().cr_send_interleaved(self.h, len(ts), sidx.ctypes.data, ts.ctypes.data, ptrs, err, 512)
         if rc != 0:
             raise EngineError(rc, err.value.decode())
+
+    def send_interleaved_ord(self, stream_idx, ts, ords, cols):
+        """send_interleaved with given arrival ordinals (a heartbeat's entry: its trigger's ordinal)."""
+        import numpy as np
+        sidx = np.ascontiguousarray(stream_idx, dtype=np.int32)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        ords = np.ascontiguousarray(ords, dtype=np.int64)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        ptrs = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        err = ctypes.create_string_buffer(512)
+        rc = lib().cr_send_interleaved_ord(self.h, len(ts), sidx.ctypes.data, ts.ctypes.data, ords.ctypes.data, ptrs,
+                                           err, 512)
+        if rc != 0:
+            raise EngineError(rc, err.value.decode())
+
+    def output_order(self, sid):
+        """(n, 4) int64: trigger ordinal, phase, clock step, instance creation ordinal of each collected output."""
+        import numpy as np
+        n = lib().cr_output_order(self.h, sid.encode(), None, 0)
+        out = np.zeros((n, 4), dtype=np.int64)
+        if n:
+            lib().cr_output_order(self.h, sid.encode(), out.ctypes.data, n)
+        return out
 
     def advance_time(self, ts):
         err = ctypes.create_string_buffer(2048)

@@ -120,12 +120,22 @@ def test_projection_of_filter_queries():
     np.testing.assert_array_equal(ots.cpu().numpy(), ts[sel])
 
 
-def test_projection_refused_after_host_events():
-    """Outputs of host-API events reach the callbacks as Events; there is no device batch to project."""
+def test_projection_after_host_events():
+    """Host-API events of an app whose queries all take the device-batch path run there (flush_device), so their
+    outputs can be projected like a device batch's; a host batch the device path cannot take (a null value) runs on
+    the host-staged path and leaves nothing to project."""
+    import torch
     from siddhi_amd.testing import EngineError, ProductApp
     app = ProductApp(SCHEMA.format(kt="int") + "@info(name='q') from StockStream[price > 50] select price insert into O;")
     app.start()
-    app.send("StockStream", 1, [1, 60.0, 1, 0], ["INT", "DOUBLE", "LONG", "LONG"])
+    types = ["INT", "DOUBLE", "LONG", "LONG"]
+    app.send("StockStream", 1, [1, 60.0, 1, 0], types)
+    app.send("StockStream", 2, [1, 40.0, 1, 0], types)
+    app.send("StockStream", 3, [1, 70.5, 1, 0], types)
+    app.flush()
+    vals, nulls, ts = app.device_project("q")
+    assert vals[:, 0].cpu().view(torch.float64).tolist() == [60.0, 70.5] and ts.tolist() == [1, 3]
+    app.send("StockStream", 4, [1, 80.0, None, 0], types)
     app.flush()
     with pytest.raises(EngineError):
         app.device_project("q")

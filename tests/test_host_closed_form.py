@@ -154,3 +154,25 @@ def test_filter_and_pattern_bulk_interleave():
     rt.shutdown()
     assert len(exp) > 1000
     assert got == [[r[0], r[1]] for r in exp]
+
+
+def test_send_device_batch_validates_tensors():
+    """SiddhiAppRuntime.sendDeviceBatch refuses tensors the device pipeline would misread: host
+    tensors, int32 event times or ordinals, misaligned lengths, a column whose width is not its attribute's."""
+    import torch
+    from siddhi_amd import SiddhiManager
+    d = torch.device("cuda", 0)
+    rt = SiddhiManager().createSiddhiAppRuntime(SCHEMA + part(PAT.format(within=" within 1 sec")))
+    n = 100
+    ts = torch.arange(n, dtype=torch.int64, device=d)
+    good = [torch.zeros(n, dtype=torch.int32, device=d), torch.zeros(n, dtype=torch.float64, device=d),
+            torch.zeros(n, dtype=torch.int64, device=d), torch.zeros(n, dtype=torch.int64, device=d)]
+    bad = [
+        dict(ts=ts.cpu()), dict(ts=ts.to(torch.int32)), dict(ordinals=ts.to(torch.int32)),
+        dict(cols=[good[0][:50]] + good[1:]), dict(cols=[good[0].to(torch.int64)] + good[1:]), dict(cols=good[:3]),
+    ]
+    for b in bad:
+        with pytest.raises(ValueError):
+            rt.sendDeviceBatch("StockStream", b.get("ts", ts), b.get("cols", good), ordinals=b.get("ordinals"))
+    rt.sendDeviceBatch("StockStream", ts, good, ordinals=ts)
+    rt.shutdown()

@@ -106,3 +106,53 @@ def test_unpack_with_ordinals_hip_equals_torch(n, world):
         assert torch.equal(a, b)
     base = torch.repeat_interleave(torch.tensor(starts, dtype=torch.int64), torch.tensor(counts, dtype=torch.int64))
     assert torch.equal(got_ord.cpu(), base + exp[-1].cpu().to(torch.int64) % 2**32)
+
+
+# ---- config 5 across ranks: each rank's device-events batch (its keys' events with their global
+# ordinals, plus the global clock advances as heartbeats) exports its output records with their triggers' global
+# ordinals (sm_app_copy_device_outputs); sending each record to its trigger's slice and ordering there
+# (sm_order_outputs) must give exactly the single app's records, in its order. Ranks are simulated on one GPU.
+BODIES5 = ["every e1=A -> e2=B[price>e1.price]<2:5> -> (e3=C or e4=D) -> not E for 1 sec",
+           "every e1=A, e2=B[price>e1.price]<1:3>, (e3=C or e4=D), not E for 1 sec"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("body", BODIES5)
+def test_config5_rank_outputs_merge_to_single_app(world, body):
+    import synth
+    from siddhi_amd.shard import clock_ticks, merge_heartbeats, order_outputs, owner_of
+    from siddhi_amd.testing import ProductApp
+    d = torch.device("cuda", 0)
+    N, K = 30000, 500
+    sid, cols, ts = synth.gen5(0, N, K, 1)
+    text = synth.app5(body)
+    t_sid = torch.from_numpy(sid).to(d)
+    t_ts = torch.from_numpy(ts).to(d)
+    t_cols = [torch.from_numpy(c).to(d) for c in cols]
+    ords = torch.arange(N, dtype=torch.int64, device=d)
+
+    def run(s, t, c, o):
+        app = ProductApp(text, keep_outputs=1)
+        app.start()
+        torch.cuda.synchronize()
+        app.process_device_events(s, t, c, ordinals=o)
+        recs = app.copy_device_outputs("q")
+        app.close()
+        return recs
+
+    full = run(t_sid, t_ts, t_cols, ords)
+    assert full.shape[0] > 30 and bool(((full[:, 4] & 0xFFFFFFFF) == 0).any()), "the stream must fire timers"
+    ticks = clock_ticks(t_ts, 0, 1)
+    per_rank = []
+    for r in range(world):
+        mine = owner_of(t_cols[0], world) == r
+        m = merge_heartbeats(t_sid[mine], t_ts[mine], [c[mine] for c in t_cols], ords[mine], ticks)
+        per_rank.append(run(m[0], m[1], m[2], m[3]))
+    starts = [N * r // world for r in range(world)] + [N]
+    got = []
+    for dst in range(world):  # what rank dst receives: each source's records of its slice, in rank order
+        runs = [rec[(rec[:, 0] >= starts[dst]) & (rec[:, 0] < starts[dst + 1])] for rec in per_rank]
+        got.append(order_outputs(torch.cat(runs)))
+    got = torch.cat(got)
+    keep = [c for c in range(full.shape[1]) if c != 6]  # column 6: key slot (differs between apps) | pad
+    assert torch.equal(got[:, keep], full[:, keep])

@@ -208,36 +208,39 @@ def test_merge_keeps_same_trigger_order():
 
 
 # ---- config 5 (five streams, playback timers): key exchange + global clock-advance heartbeats (shard.py
-# clock_ticks / merge_heartbeats) must reproduce every output of the single-process run, with the same timestamps,
-# and each rank's outputs in the global relative order.
+# clock_ticks / merge_heartbeats), then the output merge (shard.merge_outputs: every output to the rank that ingested
+# its trigger, ordered there by trigger, timers before the event, timers in instance creation order): the ranks'
+# outputs concatenated in rank order must be the single-process output list exactly.
 N5, K5 = 20000, 400
 BODIES5 = ["every e1=A -> e2=B[price>e1.price]<2:5> -> (e3=C or e4=D) -> not E for 1 sec",
            "every e1=A, e2=B[price>e1.price]<1:3>, (e3=C or e4=D), not E for 1 sec"]
 
 
 def replay5(text, sid, ts, cols):
-    """Oracle over a rank's merged sequence: events (stream >= 0) and heartbeats (-1 -> advance_time)."""
+    """The single-process reference: one oracle app over the whole stream."""
     a = OracleApp(text)
     a.start()
-    i, n = 0, len(ts)
-    while i < n:
-        if sid[i] < 0:
-            a.advance_time(int(ts[i]))
-            i += 1
-            continue
-        j = i
-        while j < n and sid[j] >= 0:
-            j += 1
-        a.send_interleaved(sid[i:j], ts[i:j], [c[i:j] for c in cols])
-        i = j
-    a.flush()
+    a.send_interleaved(sid, ts, cols)
     out = a.outputs()["streams"].get("Out", [])
+    order = a.output_order("Out")
     a.close()
-    return [[r[0], r[1]] for r in out]
+    return [[r[0], r[1]] for r in out], order
+
+
+def out_records(order, rank):
+    """Output records in the sm_app_copy_device_outputs layout (trigger ordinal, clock step, creation ordinal, ts,
+    phase | query << 32, sched | seq << 32, key | pad << 32) + one payload column: (rank << 32) | index."""
+    m = len(order)
+    rec = torch.zeros((m, 8), dtype=torch.int64)
+    if m:
+        o = torch.from_numpy(order)
+        rec[:, 0], rec[:, 4], rec[:, 1], rec[:, 2] = o[:, 0], o[:, 1], o[:, 2], o[:, 3]
+        rec[:, 7] = (rank << 32) | torch.arange(m, dtype=torch.int64)
+    return rec
 
 
 def _worker5(rank, world, port, outfile, body):
-    from siddhi_amd.shard import clock_ticks, exchange_by_key, merge_heartbeats
+    from siddhi_amd.shard import clock_ticks, exchange_by_key, merge_heartbeats, merge_outputs, slice_starts
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -252,9 +255,17 @@ def _worker5(rank, world, port, outfile, body):
         (r_sym, r_price, r_vol, r_tsa, r_ts, r_ord, r_sid), _ = exchange_by_key(t[0], t + [tts, ords, tsid], world)
         m_sid, m_ts, m_cols, m_ord = merge_heartbeats(r_sid, r_ts, [r_sym, r_price, r_vol, r_tsa], r_ord, ticks)
         assert (np.diff(m_ts.numpy()) >= 0).all()
-        local = replay5(synth.app5(body), m_sid.numpy(), m_ts.numpy(), [c.numpy() for c in m_cols])
+        assert (m_ord.numpy()[m_sid.numpy() < 0] >= 0).all(), "a heartbeat carries its trigger's ordinal"
+        a = OracleApp(synth.app5(body))
+        a.start()
+        a.send_interleaved_ord(m_sid.numpy(), m_ts.numpy(), m_ord.numpy(), [c.numpy() for c in m_cols])
+        rows = [[r[0], r[1]] for r in a.outputs()["streams"].get("Out", [])]
+        order = a.output_order("Out")
+        a.close()
+        mine = merge_outputs(out_records(order, rank), slice_starts(lo, world, torch.device("cpu")), N5, world)
+        assert ((mine[:, 0] >= lo) & (mine[:, 0] < hi)).all(), "an output merged away from its trigger's slice"
         parts = [None] * world
-        dist.all_gather_object(parts, local)
+        dist.all_gather_object(parts, [rows, mine[:, 7].tolist()])
         if rank == 0:
             with open(outfile, "w") as f:
                 json.dump(parts, f)
@@ -265,22 +276,30 @@ def _worker5(rank, world, port, outfile, body):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("body", BODIES5)
-def test_config5_sharded_with_heartbeats_equal_single_process(world, body, tmp_path):
+def test_config5_sharded_outputs_merge_to_single_process_order(world, body, tmp_path):
     out = str(tmp_path / "parts5.json")
     mp.start_processes(_worker5, args=(world, _free_port(), out, body), nprocs=world, join=True,
                        start_method="spawn")
     parts = json.load(open(out))
     sid, cols, ts = synth.gen5(0, N5, K5, 1)
-    full = replay5(synth.app5(body), sid, ts, cols)
-    assert len(full) > 30
-    key = lambda r: json.dumps(r)  # noqa: E731
-    assert sorted(map(key, full)) == sorted(key(r) for p in parts for r in p)
-    pos = {}
-    for k, r in enumerate(full):
-        pos.setdefault(key(r), []).append(k)
-    for p in parts:
-        idx = [pos[key(r)].pop(0) for r in p]
-        assert idx == sorted(idx), "a rank's outputs are out of the global order"
+    full, order = replay5(synth.app5(body), sid, ts, cols)
+    assert len(full) > 30 and (order[:, 1] == 0).any(), "the stream must fire timers"
+    merged = [parts[p >> 32][0][p & 0xFFFFFFFF] for r in range(world) for p in parts[r][1]]
+    assert merged == full
+
+
+def test_output_order_key_sorts_single_process_output():
+    """The order key itself: the single-process output list is already sorted by (trigger, phase, step, creation)
+    with its own records, so order_outputs leaves it unchanged (also on records fed in a shuffled run split)."""
+    from siddhi_amd.shard import order_outputs
+    sid, cols, ts = synth.gen5(0, N5, K5, 1)
+    full, order = replay5(synth.app5(BODIES5[0]), sid, ts, cols)
+    rec = out_records(order, 0)
+    assert torch.equal(order_outputs(rec)[:, 7], rec[:, 7])
+    # two runs (every other creation ordinal's outputs first), each in order: merged back to the single order
+    odd = (rec[:, 2] % 2) == 1
+    runs = torch.cat([rec[odd], rec[~odd]])
+    assert torch.equal(order_outputs(runs)[:, 7], rec[:, 7])
 
 
 def test_narrow_keys_rejected_consistently():
