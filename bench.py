@@ -392,6 +392,7 @@ def main():
                     help="config 4: run the input-handler variant on all --events")
     ap.add_argument("--no-ih", action="store_true", help="config 4: skip the input-handler variant")
     ap.add_argument("--ih-chunk", type=float, default=None, help="input-handler variant: option bulk_chunk")
+    ap.add_argument("--no-sparse", action="store_true", help="config 4: skip the sparse 64-bit key variant")
     ap.add_argument("--heap-words", type=int, default=None,
                     help="NFA per-key partial-match arena (words per semispace; option heap_words)")
     args = ap.parse_args()
@@ -591,6 +592,35 @@ def main():
                "h2d_GBps": 20 * N / best[0] / 1e9,
                "note": "H2D of symbol + price + event time from pinned host memory over PCIe, then the step; "
                        "not overlapped (best of 2)"}
+    sparse = None
+    if args.config == 4 and world == 1 and not args.no_sparse:
+        # the same stream keyed by sparse 64-bit ids (splitmix64 of the dense symbol: K ids over the whole int64
+        # range), `symbol long`: the keys become dense ids on the device (remap_keys) before key pass 0
+        log("sparse-key variant")
+        key64 = splitmix_torch(symbol.to(torch.int64) * 7919 + 11)
+        app_s = ProductApp(APP.replace("symbol int", "symbol long"), fast_stack=args.stack)
+        app_s.set_collect(False)
+
+        def step_s():
+            app_s.set_option("reset", 0)
+            app_s.process_device_batch("StockStream", ts, [key64, price, price, price], hip_stream=hip_stream)
+            return app_s.device_matches("q")[1]
+
+        for _ in range(args.warmup):
+            step_s()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            ms_ = step_s()
+        torch.cuda.synchronize()
+        dts = (time.perf_counter() - t1) / args.steps
+        if ms_ != nm:
+            raise RuntimeError(f"sparse-key run found {ms_} matches, the dense one {nm}")
+        sparse = {"ms_per_step": dts * 1e3, "value": N / dts, "unit": "events/s",
+                  "ratio_to_dense": dts * 1e3 / ms_per_step, "fast_path": int(app_s.get_stat("fast_path:q")),
+                  "keys": "1e6 splitmix64 ids over the int64 range (symbol long), remapped to dense ids on the device"}
+        app_s.close()
+        del key64
     ih = None
     if args.config == 4 and world == 1 and not args.no_ih:
         n_ih = N if args.via_input_handler else min(N, int(args.ih_events))
@@ -650,6 +680,8 @@ def main():
             line["e2e_with_h2d"] = e2e
         if ih:
             line["via_input_handler"] = ih
+        if sparse:
+            line["sparse_keys"] = sparse
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -33,6 +33,7 @@ struct FastHostInfo {
   const Instr* c1_host = nullptr;  // host copy of the c1 program (c1 on the compared attribute: no bit mask)
   int c1_len = 0;
   int nattr = 0;              // attributes of the stream (carried partial rows)
+  const int32_t* dense_keys = nullptr;  // device: the key column as dense ids (remap_keys), read instead of the column
 };
 
 // Device facts cached across batches by the v2 kernels.

@@ -1548,7 +1548,8 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     init.vmin = ~0ull;
     SM_HIP(hipMemcpyAsync(c, &init, sizeof(Ctrl), hipMemcpyHostToDevice, s));
   }
-  const void* kcol = keyed ? hi.cols[hi.key_col] : nullptr;
+  const void* kcol = keyed ? (hi.dense_keys ? (const void*)hi.dense_keys : hi.cols[hi.key_col]) : nullptr;
+  const int key_type = hi.dense_keys ? T_INT : hi.key_type;
   const int64_t* vlong = (keyed && hi.vtype == T_LONG) ? (const int64_t*)hi.cols[hi.vattr] : nullptr;
   if (tm) {
     SM_HIP(hipEventRecord(tm->ev[0], s));
@@ -1605,7 +1606,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     else                                \
       SM_PREP2(KT, M, false);           \
   } while (0)
-  if (hi.key_type == T_LONG && keyed) {
+  if (key_type == T_LONG && keyed) {
     if (mask) SM_PREP(int64_t, true);
     else SM_PREP(int64_t, false);
   } else {
@@ -1697,7 +1698,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     uint4* B = (uint4*)sc.take(n * 16);
     // key pass 0 from the original columns (its digit counts came from prep)
     scan_counts(G);
-    if (hi.key_type == T_INT)
+    if (key_type == T_INT)
       launch_down0_k<int32_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
     else launch_down0_k<int64_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
     tmark("key_pass0");

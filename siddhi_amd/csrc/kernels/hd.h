@@ -30,6 +30,11 @@ inline int atomicOr(int* p, int v) {
   *p |= v;
   return o;
 }
+inline unsigned long long atomicCAS(unsigned long long* p, unsigned long long cmp, unsigned long long v) {
+  unsigned long long o = *p;
+  if (o == cmp) *p = v;
+  return o;
+}
 #else
 // Wave emulator (tests/native/stack_emu.cpp, test infrastructure): every GPU thread of a workgroup is a fiber of one
 // host thread; wave64 operations and __syncthreads are barriers of the fibers of a wave / the workgroup (the
@@ -98,6 +103,10 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
 }
 inline unsigned atomicOr(unsigned* p, unsigned v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ_CST); }
 inline int atomicOr(int* p, int v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ_CST); }
+inline unsigned long long atomicCAS(unsigned long long* p, unsigned long long cmp, unsigned long long v) {
+  __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
+  return cmp;
+}
 inline unsigned __float_as_uint(float f) {
   unsigned u;
   memcpy(&u, &f, 4);

@@ -130,4 +130,10 @@ bool lane_compact_ok(const NfaBatch& b, int64_t n, int32_t node_words, int nstre
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
                 int32_t nkeys, int32_t* err_dev, hipStream_t s);
 
+// One pass of the overflow-pool compaction over nkeys key slots (nfa_impl.h nfa_pool_lane): pass 0 writes each key's
+// new home to new_off (-2 none, -1 its own arena, else an offset claimed from new_top), pass 1 moves the live objects.
+void launch_pool_compact(int pass, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
+                         int32_t nkeys, int64_t* old_pool, int64_t* new_pool, unsigned long long* new_top,
+                         int64_t* new_off, hipStream_t s);
+
 }  // namespace sm

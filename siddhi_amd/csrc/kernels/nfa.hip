@@ -23,6 +23,14 @@ __global__ SM_NFA_ATTR void nfa_kernel(NfaBatch b, const char* __restrict__ blob
   nfa_lane(b, blob, ks_all, heap_all, heap_half, lanes, key, err_out);
 }
 
+__global__ void pool_compact_kernel(int pass, const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all,
+                                    int32_t heap_half, int64_t lanes, int32_t nkeys, int64_t* old_pool,
+                                    int64_t* new_pool, unsigned long long* new_top, int64_t* new_off) {
+  const int key = blockIdx.x * blockDim.x + threadIdx.x;
+  if (key >= nkeys) return;
+  nfa_pool_lane(blob, ks_all, heap_all, heap_half, lanes, key, pass, old_pool, new_pool, new_top, new_off);
+}
+
 // Gather each record of the query's batch, in key order, into its LaneEv record: a lane then reads one
 // contiguous record per event instead of chasing key_pos -> stream / row / ts / clock / ordinal / columns.
 // Key order -> batch position is a permutation (key_pos); build the records in batch-position order instead, so
@@ -165,6 +173,14 @@ bool lane_compact_ok(const NfaBatch& b, int64_t n, int32_t node_words, int nstre
   if (h[1] - h[0] >= kLeOrdMask) return false;
   *ord_base = (int64_t)h[0];
   return true;
+}
+
+void launch_pool_compact(int pass, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half, int64_t lanes,
+                         int32_t nkeys, int64_t* old_pool, int64_t* new_pool, unsigned long long* new_top,
+                         int64_t* new_off, hipStream_t s) {
+  if (nkeys <= 0) return;
+  hipLaunchKernelGGL(pool_compact_kernel, dim3((unsigned)((nkeys + 255) / 256)), dim3(256), 0, s, pass, blob_dev, ks,
+                     heap, heap_half, lanes, nkeys, old_pool, new_pool, new_top, new_off);
 }
 
 void launch_nfa(const NfaBatch& b, const char* blob_dev, int64_t* ks, int64_t* heap, int32_t heap_half,

@@ -1033,16 +1033,9 @@ struct Lane {
     heap[o] = K_FWD | ((int64_t)(uint32_t)n << 32);
     return n;
   }
-  __device__ void promote(int64_t live) {
-    int64_t nh = 2 * (int64_t)half;
-    if (nh < 8 * live) nh = 8 * live;
-    nh = (nh + 63) & ~(int64_t)63;
-    if (nh > ((int64_t)1 << 30)) return;  // heap offsets are 32-bit: stay (alloc reports an arena overflow)
-    const int64_t words = 2 * nh + 64;
-    if (!b->pool) return;
-    const int64_t off = (int64_t)atomicAdd(b->pool_top, (unsigned long long)words);
-    if (off + words > b->pool_cap) return;  // pool full: the host grows it after the batch
-    const LaneWords dst{b->pool + off, 1};
+  // Cheney copy of the live objects (reachable from the pending / newAndEvery lists, the collector's roots) into
+  // semispace 0 of dst; returns the words copied. The source is left holding forwarding words.
+  __device__ int64_t copy_live(const LaneWords& dst) {
     auto hi_of = [&](int64_t w) { return (int32_t)(w >> 32); };
     auto with_hi = [&](int64_t w, int32_t v) { return (w & 0xFFFFFFFFll) | ((int64_t)(uint32_t)v << 32); };
     int64_t top = 0, scan = 0;
@@ -1073,6 +1066,34 @@ struct Lane {
         scan += PQ->node_words;
       }
     }
+    return top;
+  }
+  // words per semispace of a pool region for `live` live words: at least twice the own arena, 8x the live data
+  __device__ static int64_t pool_half(int64_t live, int32_t own_half) {
+    int64_t nh = 2 * (int64_t)own_half;
+    if (nh < 8 * live) nh = 8 * live;
+    return (nh + 63) & ~(int64_t)63;
+  }
+  // `words` of the overflow pool, or -1 when it is full (a failed request claims nothing: the host sizes the pool
+  // from pool_top after the batch)
+  __device__ int64_t pool_claim(int64_t words) {
+    unsigned long long cur = *(volatile unsigned long long*)b->pool_top;
+    for (;;) {
+      if ((int64_t)cur + words > b->pool_cap) return -1;
+      const unsigned long long prev = atomicCAS(b->pool_top, cur, cur + (unsigned long long)words);
+      if (prev == cur) return (int64_t)cur;
+      cur = prev;
+    }
+  }
+  __device__ void promote(int64_t live) {
+    const int64_t nh = pool_half(live, half);
+    if (nh > ((int64_t)1 << 30)) return;  // heap offsets are 32-bit: stay (alloc reports an arena overflow)
+    const int64_t words = 2 * nh + 64;
+    if (!b->pool) return;
+    const int64_t off = pool_claim(words);
+    if (off < 0) return;  // pool full: the host grows it after the batch
+    const LaneWords dst{b->pool + off, 1};
+    const int64_t top = copy_live(dst);
     heap = dst;
     half = (int32_t)nh;
     misc(2) = 0;
@@ -1485,6 +1506,54 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
   }
   if (L.err) atomicOr(err_out, L.err);
 }
+
+#if !defined(SM_NFA_JIT) && !defined(SM_NFA_LDS)
+// Batch-boundary compaction of a query's overflow pool (runtime.cpp compact_pool): pass 0 sizes each promoted key's
+// new home, pass 1 moves its live objects there (the collector's copy). A key whose live data fits a quarter of its own
+// arena goes back to it (misc(5) = 0); every other promoted key gets a pool region sized for its live data in the new
+// pool. Nothing of the old pool stays reachable afterwards: regions abandoned by keys promoted again, and regions of
+// keys whose hot phase is over, are reclaimed, so the pool holds what the live partial matches need.
+__device__ void nfa_pool_lane(const char* __restrict__ blob, int64_t* ks_all, int64_t* heap_all, int32_t heap_half,
+                              int64_t lanes, int32_t key, int pass, int64_t* old_pool, int64_t* new_pool,
+                              unsigned long long* new_top, int64_t* new_off) {
+  Lane L;
+  L.PQ = (const DQuery*)blob;
+  L.PPRE = (const DPre*)(blob + L.PQ->off_pre);
+  L.PPOST = (const DPost*)(blob + L.PQ->off_post);
+  L.PRECV = (const DReceiver*)(blob + L.PQ->off_recv);
+  L.PWITHIN = (const DWithin*)(blob + L.PQ->off_within);
+  L.PCODE = (const Instr*)(blob + L.PQ->off_code);
+  L.PCONSTS = (const DVal*)(blob + L.PQ->off_const);
+  L.PSEL = (const int32_t*)(blob + L.PQ->off_sel);
+  L.PREFS = (const int32_t*)(blob + L.PQ->off_refs);
+  L.ks = LaneWords{ks_all + key, lanes};
+  L.ksh = L.ks;
+  L.b = nullptr;
+  L.err = 0;
+  if (L.misc(4) == 0 || L.misc(5) <= 0) {  // no lane yet, or its heap is its own arena
+    if (pass == 0) new_off[key] = -2;
+    return;
+  }
+  L.heap = LaneWords{old_pool + (L.misc(5) - 1), 1};
+  L.half = (int32_t)L.misc(6);
+  if (pass == 0) L.gc();  // in place: what is in use afterwards is exactly the live data
+  const int64_t live = L.misc(1) - L.misc(2) * L.half;
+  if (pass == 0) {
+    new_off[key] = live * 4 <= heap_half ? -1
+                                         : (int64_t)atomicAdd(new_top, (unsigned long long)(2 * Lane::pool_half(live, heap_half) + 64));
+    return;
+  }
+  const int64_t o = new_off[key];
+  if (o == -2) return;
+  const LaneWords dst = o == -1 ? LaneWords{heap_all + (int64_t)key * (2 * (int64_t)heap_half + 64), 1}
+                                : LaneWords{new_pool + o, 1};
+  const int64_t top = L.copy_live(dst);
+  L.misc(2) = 0;
+  L.misc(1) = top;
+  L.misc(5) = o == -1 ? 0 : o + 1;
+  L.misc(6) = o == -1 ? 0 : Lane::pool_half(live, heap_half);
+}
+#endif
 
 }  // namespace
 }  // namespace sm

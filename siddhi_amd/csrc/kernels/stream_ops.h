@@ -25,6 +25,26 @@ struct KeyTable {
   void release();
 };
 
+// Dense ids of a closed-form query's partition keys (remap_keys): any int32 / int64 key domain (sparse 64-bit ids,
+// spans of 2^40 ...) becomes ids 0 .. nslots-1, so the keyed pipelines see a key span of the number of distinct keys.
+// An open-addressing table of 16-byte entries {key, id + 1 | busy}, filled by the lookup kernel itself (an event whose
+// key is missing claims an entry and the next id), persistent across batches: carried partials hold dense ids.
+struct DenseKeys {
+  int64_t* table = nullptr;      // cap entries of two words: key, state (0 empty, -1 being inserted, else id + 1)
+  int64_t* slot_keys = nullptr;  // id -> key
+  uint32_t* counter = nullptr;   // device: ids handed out
+  int64_t cap = 0, slot_cap = 0;
+  int64_t nslots = 0;
+  void reserve(int64_t slots, hipStream_t s);
+  void load(const int64_t* keys_host, int64_t n, hipStream_t s);  // restore: ids 0 .. n-1 = keys_host
+  void clear(hipStream_t s);
+  void release();
+};
+// smallest and largest key of an int32 / int64 key column
+void key_range(const void* col, int key_type, int64_t n, int64_t* lo, int64_t* hi, Scratch& sc, hipStream_t s);
+// out[i] = dense id of key column col[i] (key_type T_INT or T_LONG), new keys added; n events.
+void remap_keys(DenseKeys& D, const void* col, int key_type, int64_t n, int32_t* out, hipStream_t s);
+
 // FilterProcessor over rows [0, n) of one stream; writes matching row indices (ascending), returns the count.
 int64_t filter_rows(const NfaStream* st_dev, int64_t n, const Instr* code, int len, const DVal* consts,
                     int64_t* out_rows, Scratch& sc, hipStream_t s);

@@ -473,6 +473,89 @@ __global__ void rehash_kernel(const int64_t* __restrict__ slot_keys, int64_t nsl
 
 inline dim3 grid_for(int64_t n, int t = 256) { return dim3((unsigned)((n + t - 1) / t)); }
 
+// ---- dense key ids (remap_keys)
+constexpr int64_t kDkBusy = -1;
+
+// Lookup-or-insert of each event's key. An entry is claimed with a CAS from empty to busy, filled, then published
+// with its id; a reader meeting a busy entry reads it again (the claiming lane fills it in the same loop iteration,
+// so no lane waits on work another lane of its wave has not done yet). An id beyond the id capacity releases the
+// entry and flags an overflow: the host grows the table and runs the batch again (found keys are found again).
+template <typename KT>
+__global__ void __launch_bounds__(256) remap_kernel(const KT* __restrict__ col, int64_t n, int64_t* __restrict__ table,
+                                                    uint64_t mask, int64_t* __restrict__ slot_keys, int64_t limit,
+                                                    uint32_t* __restrict__ counter, int32_t* __restrict__ out,
+                                                    uint32_t* __restrict__ overflow) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = (int64_t)col[i];
+    uint64_t h = mix64((uint64_t)k) & mask;
+    int32_t res = -1;
+    uint64_t probes = 0;
+    while (probes <= mask) {
+      unsigned long long* st = (unsigned long long*)&table[2 * h + 1];
+      const int64_t sv = (int64_t)__hip_atomic_load(st, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (sv == kDkBusy) continue;
+      if (sv == 0) {
+        if (atomicCAS(st, 0ull, (unsigned long long)kDkBusy) != 0ull) continue;
+        const uint32_t id = atomicAdd(counter, 1u);
+        if ((int64_t)id >= limit) {
+          __hip_atomic_store(st, 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          atomicOr(overflow, 1u);
+          break;
+        }
+        table[2 * h] = k;
+        slot_keys[id] = k;
+        __hip_atomic_store(st, (unsigned long long)id + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        res = (int32_t)id;
+        break;
+      }
+      if (table[2 * h] == k) {
+        res = (int32_t)(sv - 1);
+        break;
+      }
+      h = (h + 1) & mask;
+      ++probes;
+    }
+    out[i] = res;
+  }
+}
+
+template <typename KT>
+__global__ void __launch_bounds__(256) key_minmax_kernel(const KT* __restrict__ col, int64_t n,
+                                                         unsigned long long* __restrict__ mm) {
+  uint64_t lo = ~0ull, hi = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t u = (uint64_t)(int64_t)col[i] ^ 0x8000000000000000ull;
+    lo = u < lo ? u : lo;
+    hi = u > hi ? u : hi;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t l2 = __shfl_xor(lo, off, 64), h2 = __shfl_xor(hi, off, 64);
+    lo = l2 < lo ? l2 : lo;
+    hi = h2 > hi ? h2 : hi;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&mm[0], (unsigned long long)lo);
+    atomicMax(&mm[1], (unsigned long long)hi);
+  }
+}
+
+__global__ void dk_rehash_kernel(const int64_t* __restrict__ slot_keys, int64_t n, int64_t* __restrict__ table,
+                                 uint64_t mask) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t k = slot_keys[i];
+  uint64_t h = mix64((uint64_t)k) & mask;
+  for (;;) {
+    unsigned long long* st = (unsigned long long*)&table[2 * h + 1];
+    if (atomicCAS(st, 0ull, (unsigned long long)i + 1) == 0ull) {
+      table[2 * h] = k;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+
 
 // ---- device-resident interleaved batch (sm_app_process_device_events): the per-event arrays the host path
 // builds record by record in stage_record (runtime.cpp) — row, ordinal, playback clock after sendData and the
@@ -654,6 +737,112 @@ void KeyTable::load(const int64_t* keys_host, int32_t n, hipStream_t s) {
   }
   nslots = n;
   SM_HIP(hipStreamSynchronize(s));
+}
+
+void DenseKeys::reserve(int64_t slots, hipStream_t s) {
+  if (slots > INT32_MAX - 1) throw std::runtime_error("too many partition keys");
+  if (slots > slot_cap) {
+    int64_t nc = std::max<int64_t>(1 << 16, slot_cap);
+    while (nc < slots) nc *= 2;
+    int64_t* nk = nullptr;
+    SM_HIP(hipMalloc(&nk, nc * 8));
+    if (slot_keys && nslots) SM_HIP(hipMemcpyAsync(nk, slot_keys, (size_t)nslots * 8, hipMemcpyDeviceToDevice, s));
+    SM_HIP(hipStreamSynchronize(s));
+    if (slot_keys) SM_HIP(hipFree(slot_keys));
+    slot_keys = nk;
+    slot_cap = nc;
+  }
+  if (!counter) {
+    SM_HIP(hipMalloc(&counter, 8));
+    SM_HIP(hipMemsetAsync(counter, 0, 8, s));
+  }
+  if (slot_cap * 2 > cap) {  // load factor at most 1/2 when every id is handed out
+    int64_t nc = std::max<int64_t>(1 << 17, cap);
+    while (nc < slot_cap * 2) nc *= 2;
+    if (table) SM_HIP(hipFree(table));
+    SM_HIP(hipMalloc(&table, (size_t)nc * 16));
+    SM_HIP(hipMemsetAsync(table, 0, (size_t)nc * 16, s));
+    cap = nc;
+    if (nslots > 0)
+      hipLaunchKernelGGL(dk_rehash_kernel, grid_for(nslots), dim3(256), 0, s, slot_keys, nslots, table,
+                         (uint64_t)cap - 1);
+  }
+}
+
+void DenseKeys::load(const int64_t* keys_host, int64_t n, hipStream_t s) {
+  clear(s);
+  reserve(std::max<int64_t>(n, 1), s);
+  if (n) SM_HIP(hipMemcpyAsync(slot_keys, keys_host, (size_t)n * 8, hipMemcpyHostToDevice, s));
+  nslots = n;
+  const uint32_t c = (uint32_t)n;
+  SM_HIP(hipMemcpyAsync(counter, &c, 4, hipMemcpyHostToDevice, s));
+  if (n) hipLaunchKernelGGL(dk_rehash_kernel, grid_for(n), dim3(256), 0, s, slot_keys, n, table, (uint64_t)cap - 1);
+  SM_HIP(hipStreamSynchronize(s));
+}
+
+void DenseKeys::clear(hipStream_t s) {
+  if (table) SM_HIP(hipMemsetAsync(table, 0, (size_t)cap * 16, s));
+  if (counter) SM_HIP(hipMemsetAsync(counter, 0, 8, s));
+  nslots = 0;
+}
+
+void DenseKeys::release() {
+  if (table) (void)hipFree(table);
+  if (slot_keys) (void)hipFree(slot_keys);
+  if (counter) (void)hipFree(counter);
+  table = slot_keys = nullptr;
+  counter = nullptr;
+  cap = slot_cap = nslots = 0;
+}
+
+void key_range(const void* col, int key_type, int64_t n, int64_t* lo, int64_t* hi, Scratch& sc, hipStream_t s) {
+  const size_t mark = sc.used;
+  unsigned long long* mm = (unsigned long long*)sc.take(16);
+  const unsigned long long init[2] = {~0ull, 0ull};
+  SM_HIP(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, s));
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048));
+  if (key_type == T_LONG)
+    hipLaunchKernelGGL(key_minmax_kernel<int64_t>, dim3(g), dim3(256), 0, s, (const int64_t*)col, n, mm);
+  else
+    hipLaunchKernelGGL(key_minmax_kernel<int32_t>, dim3(g), dim3(256), 0, s, (const int32_t*)col, n, mm);
+  unsigned long long h[2];
+  SM_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, s));
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+  *lo = (int64_t)(h[0] ^ 0x8000000000000000ull);
+  *hi = (int64_t)(h[1] ^ 0x8000000000000000ull);
+}
+
+void remap_keys(DenseKeys& D, const void* col, int key_type, int64_t n, int32_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  // room for the ids seen so far plus up to 2^20 new ones; more new keys overflow and grow the table
+  D.reserve(D.nslots + std::min<int64_t>(n, (int64_t)1 << 20), s);
+  uint32_t* ovf = nullptr;
+  SM_HIP(hipMalloc(&ovf, 4));
+  struct Free {
+    uint32_t* p;
+    ~Free() { (void)hipFree(p); }
+  } fr{ovf};
+  for (;;) {
+    SM_HIP(hipMemsetAsync(ovf, 0, 4, s));
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 16384);
+    if (key_type == T_LONG)
+      hipLaunchKernelGGL(remap_kernel<int64_t>, dim3(g), dim3(256), 0, s, (const int64_t*)col, n, D.table,
+                         (uint64_t)D.cap - 1, D.slot_keys, D.slot_cap, D.counter, out, ovf);
+    else
+      hipLaunchKernelGGL(remap_kernel<int32_t>, dim3(g), dim3(256), 0, s, (const int32_t*)col, n, D.table,
+                         (uint64_t)D.cap - 1, D.slot_keys, D.slot_cap, D.counter, out, ovf);
+    uint32_t h[2] = {0, 0};
+    SM_HIP(hipMemcpyAsync(&h[0], ovf, 4, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipMemcpyAsync(&h[1], D.counter, 4, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    D.nslots = std::min<int64_t>(h[1], D.slot_cap);
+    if (!h[0]) return;
+    // ids ran out: the counter went past the capacity; keep the ids handed out, grow, and run the batch again
+    const uint32_t c = (uint32_t)D.nslots;
+    SM_HIP(hipMemcpyAsync(D.counter, &c, 4, hipMemcpyHostToDevice, s));
+    D.reserve(D.slot_cap * 4, s);
+  }
 }
 
 void KeyTable::reserve(int64_t total, hipStream_t s) {

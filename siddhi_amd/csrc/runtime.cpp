@@ -235,6 +235,10 @@ struct QueryRt {
   int64_t n_out = 0;         // output records read back since the counter was last taken
   FastState fast;            // v2 kernels' persistent look-back state
   FastCarry carry;           // open partials carried across device batches (closed-form queries)
+  // dense partition-key ids for the closed form (remap_keys): 0 = not decided yet, 1 = keys become dense ids (the
+  // carry holds ids), 2 = the raw key column is used
+  int remap = 0;
+  DenseKeys dense;
   bool nfa_used = false;     // host-API batches ran through the NFA kernel (partials live in ks / heap)
   bool nfa_mode = false;     // a closed-form query handed to the NFA kernel for good (nfa_device_batch)
   int level = 0;             // chaining depth: 0 reads input streams only, L reads a stream a level L-1 query fills
@@ -265,7 +269,11 @@ struct QueryRt {
   DBuf pool, pool_top_dev;
   int64_t pool_words = 0;
   uint64_t pool_used = 0;
-  ~QueryRt() { carry.release(); }
+  int64_t pool_compactions = 0;
+  ~QueryRt() {
+    carry.release();
+    dense.release();
+  }
 };
 
 // v2 eligibility: c2 may read one attribute only (of e1 / e2 slots), c1 only e1, no timestamp reads.
@@ -309,6 +317,8 @@ struct sm_app {
   // device-batch fast path knobs (sm_app_set_option "fast_general" / "fast_timing") and the last timings
   bool force_general_fast = false;
   int fast_stack = 0;  // option "fast_stack": 0 = automatic, 1 = always the bucket-stack kernels, 2 = never
+  int key_remap = -1;  // option "key_remap": 1 = closed-form keys always become dense ids, 0 = never, -1 = when the
+                       // first batch's key span exceeds the bucket-stack window (2^20)
   int max_level = 0;   // deepest query chaining level (0: no query reads a stream another query fills)
   std::vector<char> stream_fed;  // per stream: some query reads it and some query inserts into it
   // per partition: the streams it does not key that its queries read (broadcast to every instance), and the key
@@ -1000,6 +1010,37 @@ struct EvArrays {
   int64_t clock_in;
 };
 
+// Reclaim the overflow pool at a batch boundary: Lane::promote claims a fresh region whenever a key
+// outgrows its current heap and abandons the old one, so a pool that only grew would keep every region a key ever
+// used. Every promoted key's live objects move to a new pool region sized for them, or back to the key's own arena
+// when they fit a quarter of it (nfa_pool_lane, two passes); the old pool is then entirely dead and freed.
+void compact_pool(sm_app* a, QueryRt& q, int64_t nkeys, hipStream_t hs) {
+  if (!q.pool.p || q.pool_used == 0 || nkeys <= 0) return;
+  DBuf off, top;
+  off.ensure((size_t)nkeys * 8);
+  top.ensure(8);
+  SM_HIP(hipMemsetAsync(top.p, 0, 8, hs));
+  launch_pool_compact(0, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
+                      (int32_t)nkeys, (int64_t*)q.pool.p, nullptr, (unsigned long long*)top.p, (int64_t*)off.p, hs);
+  uint64_t need = 0;
+  SM_HIP(hipMemcpyAsync(&need, top.p, 8, hipMemcpyDeviceToHost, hs));
+  SM_HIP(hipStreamSynchronize(hs));
+  const int64_t words = std::max<int64_t>(2 * (int64_t)need + 4096, (int64_t)1 << 16);
+  void* np = nullptr;
+  SM_HIP(hipMalloc(&np, (size_t)words * 8));
+  launch_pool_compact(1, (const char*)q.blob.p, (int64_t*)q.ks.p, (int64_t*)q.heap.p, a->heap_half, q.state_slots,
+                      (int32_t)nkeys, (int64_t*)q.pool.p, (int64_t*)np, nullptr, (int64_t*)off.p, hs);
+  SM_HIP(hipGetLastError());
+  SM_HIP(hipMemcpyAsync(q.pool_top_dev.p, &need, 8, hipMemcpyHostToDevice, hs));
+  SM_HIP(hipStreamSynchronize(hs));
+  q.pool.release();
+  q.pool.p = np;
+  q.pool.cap = (size_t)words * 8;
+  q.pool_words = words;
+  q.pool_used = need;
+  ++q.pool_compactions;
+}
+
 // One pattern / sequence query over a batch: select its streams' records, group them by partition key, run the
 // NFA kernel (one lane per key) and read its output records back for ordered delivery.
 void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::vector<HostOut>& outs, hipStream_t hs,
@@ -1056,7 +1097,12 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.out_count = (uint32_t*)a->d_count.p;
   b.out_cap = (uint32_t)cap;
   b.out_stride = (uint32_t)stride;
-  ensure_pool(a, q, std::max<int64_t>(q.pool_words, a->pool_init), (int64_t)q.pool_used);
+  {  // room for every promotion this batch can make: a promoted region holds at most ~32x the words the batch
+     // allocates (8x live per semispace, two semispaces, keys promoted at a quarter of their arena), and a batch
+     // allocates at most a record, a chain node and a list node per event; capped at option pool_words
+    const int64_t bound = (int64_t)q.pool_used + 32 * nq * (int64_t)(h.rec_words + h.node_words + 2) + 4096;
+    ensure_pool(a, q, std::max<int64_t>(q.pool_words, std::min<int64_t>(bound, a->pool_init)), (int64_t)q.pool_used);
+  }
   b.pool = (int64_t*)q.pool.p;
   b.pool_top = (unsigned long long*)q.pool_top_dev.p;
   b.pool_cap = q.pool_words;
@@ -1097,7 +1143,9 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   SM_HIP(hipMemcpyAsync(&he, a->d_err.p, 4, hipMemcpyDeviceToHost, hs));
   SM_HIP(hipMemcpyAsync(&q.pool_used, q.pool_top_dev.p, 8, hipMemcpyDeviceToHost, hs));
   SM_HIP(hipStreamSynchronize(hs));
-  // keep the pool at most half full for the next batch's promotions
+  // keep the pool at most half full for the next batch's promotions: reclaim dead regions first (compact_pool), grow
+  // only if the live partial matches need it
+  if ((int64_t)q.pool_used * 2 > q.pool_words) compact_pool(a, q, nkeys, hs);
   if ((int64_t)q.pool_used * 2 > q.pool_words)
     ensure_pool(a, q, std::max<int64_t>(2 * q.pool_words, 2 * (int64_t)q.pool_used), (int64_t)q.pool_used);
   if (he) {
@@ -1928,7 +1976,7 @@ void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const 
     // partials' working arrays, plus the bucket-stack spill rings and bounded buffers
     const size_t nc = (size_t)qp->carry.n, wc = (size_t)std::max(qp->carry.width, 4);
     need = std::max(need, cq.hdr.kind == 0 ? n / 8 + n / 1024 + (64 << 20)
-                                           : n * 64 + std::min<size_t>(n + nc, (size_t)1 << 26) * 32 +
+                                           : n * 68 + std::min<size_t>(n + nc, (size_t)1 << 26) * 32 +
                                                  nc * (160 + 8 * wc) + ((size_t)640 << 20));
   }
   ensure_scratch(a, need);
@@ -2005,6 +2053,25 @@ void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const 
       if (kc.size() == 1 && kc[0].op == OP_COL) {
         hi.key_col = kc[0].a;
         hi.key_type = types[hi.key_col];
+      }
+    }
+    // partition keys as dense ids (any key domain): decided at the query's first closed-form batch, then kept, since
+    // the carried partials hold ids; ValuePartitionExecutor (core/partition/executor/ValuePartitionExecutor.java:34-39)
+    // keys by any value, so a sparse 64-bit id must not leave the closed form
+    if (fa.key && hi.key_col >= 0 && !a->force_general_fast && n > 0) {
+      if (q.remap == 0 && !q.carry.active) {
+        if (a->key_remap >= 0) {
+          q.remap = a->key_remap ? 1 : 2;
+        } else {
+          int64_t lo = 0, hi_k = 0;
+          key_range(hi.cols[hi.key_col], hi.key_type, (int64_t)n, &lo, &hi_k, a->sc, hs);
+          q.remap = (uint64_t)hi_k - (uint64_t)lo > ((uint64_t)1 << 20) ? 1 : 2;
+        }
+      }
+      if (q.remap == 1) {  // the pipelines read the ids instead of the key column (the column keeps its values)
+        int32_t* dk = (int32_t*)a->sc.take(n * 4);
+        remap_keys(q.dense, hi.cols[hi.key_col], hi.key_type, (int64_t)n, dk, hs);
+        hi.dense_keys = dk;
       }
     }
     q.prev_carry_n = q.carry.n;
@@ -2354,7 +2421,7 @@ using namespace sm;
 
 // snapshot encoding helpers (sm_app_snapshot / sm_app_restore)
 namespace {
-constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '4'};
+constexpr char kSnapMagic[8] = {'S', 'M', 'S', 'N', 'A', 'P', '0', '5'};
 
 struct SnapWriter {
   std::vector<uint8_t> b;
@@ -2672,6 +2739,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
         q->pool_used = 0;
         q->dev_n = 0;
         q->carry.reset();
+        q->dense.clear(a->stream);
+        q->remap = 0;
       }
       SM_HIP(hipStreamSynchronize(a->stream));
       a->clock = a->clock_batch_in = 0;
@@ -2690,6 +2759,8 @@ int sm_app_set_option(sm_app* a, const char* key, int64_t value) {
       }
     } else if (k == "output_records") {
       a->out_records = std::max<int64_t>(0, value);
+    } else if (k == "key_remap") {
+      a->key_remap = value < 0 ? -1 : (value != 0);
     } else if (k == "keep_outputs") {
       a->keep_outputs = value != 0;
     } else if (k == "bulk_min") {
@@ -2893,6 +2964,13 @@ int sm_app_snapshot(sm_app* a, uint8_t* buf, size_t cap, size_t* len) {
         w.raw(pool.data(), pu * 8);
       }
       w.put<uint8_t>((uint8_t)(q.nfa_used | (q.nfa_mode << 1) | (q.carry.active << 2)));
+      w.put<int32_t>(q.remap);  // dense key ids: the id -> key array (the carry's keys are ids)
+      w.put<int64_t>(q.dense.nslots);
+      if (q.dense.nslots) {
+        std::vector<int64_t> keys((size_t)q.dense.nslots);
+        SM_HIP(hipMemcpy(keys.data(), q.dense.slot_keys, keys.size() * 8, hipMemcpyDeviceToHost));
+        w.raw(keys.data(), keys.size() * 8);
+      }
       w.put<int64_t>(q.carry.ts_last);
       w.put<int64_t>(q.carry.n);
       w.put<int32_t>(q.carry.width);
@@ -3002,6 +3080,13 @@ int sm_app_restore(sm_app* a, const uint8_t* buf, size_t len) {
       q.nfa_mode = (fl >> 1) & 1;
       q.carry.reset();
       q.carry.active = (fl >> 2) & 1;
+      q.remap = r.get<int32_t>();
+      const int64_t nd = r.get<int64_t>();
+      if (q.remap < 0 || q.remap > 2 || nd < 0 || nd > INT32_MAX)
+        throw std::runtime_error("CannotRestoreSiddhiAppStateException: bad key ids");
+      std::vector<int64_t> dkeys((size_t)nd);
+      if (nd) r.raw(dkeys.data(), (size_t)nd * 8);
+      q.dense.load(dkeys.data(), nd, a->stream);
       q.carry.ts_last = r.get<int64_t>();
       const int64_t cn = r.get<int64_t>();
       const int32_t cw = r.get<int32_t>();
@@ -3215,6 +3300,19 @@ int sm_app_get_stat(sm_app* a, const char* key, double* out) {
           return;
         }
       throw sql::ValidationError("No query with name " + k.substr(11));
+    }
+    for (const char* pk : {"pool_words:", "pool_used:", "pool_compactions:"}) {  // overflow pool of a pattern query
+      const std::string pre = pk;
+      if (k.rfind(pre, 0) == 0) {
+        for (auto& q : a->queries)
+          if (q->cq.name == k.substr(pre.size())) {
+            *out = pre == "pool_words:" ? (double)q->pool_words
+                 : pre == "pool_used:"  ? (double)q->pool_used
+                                        : (double)q->pool_compactions;
+            return;
+          }
+        throw sql::ValidationError("No query with name " + k.substr(pre.size()));
+      }
     }
     if (k.rfind("fast_path:", 0) == 0) {
       for (auto& q : a->queries)

@@ -207,3 +207,55 @@ def test_hot_key_overflow_pool_default_arena():
     out = exp["streams"].get("Out", [])
     assert sum(1 for r in out if r[1][1] == n - 1) >= n_hot * 0.9
     assert got == exp
+
+
+def test_rotating_hot_keys_keep_the_pool_bounded():
+    """a stream whose hot key changes batch after batch. Each batch, a new key collects 3000 open partials
+    (its heap moves to the overflow pool) and a final B matches them all; the key is never seen again. The pool is
+    compacted at batch boundaries (dead regions reclaimed, drained keys back in their own arenas), so its size stays
+    bounded instead of growing with every key that was ever hot, and the outputs equal the oracle's."""
+    rng = np.random.default_rng(5)
+    text = synth.app5("every e1=A -> e2=B[price > e1.price]", playback=False,
+                      select="select e1.timestamp as a, e2.timestamp as b insert into Out;")
+    batches, per = 14, 3000
+    sid_l, sym_l, price_l = [], [], []
+    for b in range(batches):
+        hot = np.full(per, 100_000 + b, np.int32)
+        other = rng.integers(0, 2000, 2 * per).astype(np.int32)
+        sym = np.concatenate([hot, other])
+        sid = np.concatenate([np.zeros(per, np.int32), rng.integers(0, 2, 2 * per).astype(np.int32)])
+        price = np.concatenate([rng.random(per) * 50, rng.random(2 * per) * 100])
+        perm = rng.permutation(len(sym))
+        sym_l += [sym[perm], np.array([100_000 + b], np.int32)]
+        sid_l += [sid[perm], np.array([1], np.int32)]
+        price_l += [price[perm], np.array([99.0])]
+    sizes = [len(x) for x in sym_l]
+    bounds = np.cumsum([0] + [sizes[2 * b] + sizes[2 * b + 1] for b in range(batches)])
+    sym, sid, price = np.concatenate(sym_l), np.concatenate(sid_l), np.concatenate(price_l)
+    n = len(sym)
+    cols = [sym, price, np.zeros(n, np.int64), np.arange(n, dtype=np.int64)]
+    ts = np.arange(n, dtype=np.int64)
+    exp = oracle_out(text, sid, cols, ts)
+    import torch
+    from siddhi_amd.testing import ProductApp
+    dev = torch.device("cuda", 0)
+    a = ProductApp(text)
+    a.start()
+    words, used = [], []
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        tsid = torch.from_numpy(np.ascontiguousarray(sid[lo:hi])).to(dev)
+        tts = torch.from_numpy(np.ascontiguousarray(ts[lo:hi])).to(dev)
+        tcols = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
+        torch.cuda.synchronize()
+        a.process_device_events(tsid, tts, tcols, ordinal_base=int(lo))
+        words.append(int(a.get_stat("pool_words:q")))
+        used.append(int(a.get_stat("pool_used:q")))
+    compactions = int(a.get_stat("pool_compactions:q"))
+    a.flush()
+    got = a.outputs()
+    a.close()
+    print("pool words per batch", words, "used", used, "compactions", compactions)
+    assert sum(1 for r in exp["streams"]["Out"] if r[1][1] in set(bounds[1:] - 1)) >= batches * per * 0.9
+    assert got == exp
+    assert compactions > 0
+    assert max(words[batches // 2:]) <= 2 * max(words[:4]), "the pool keeps growing with every hot key"
