@@ -668,12 +668,29 @@ struct Lane {
       case PK_ABSENT_STREAM: {
         if (P.kind == PK_ABSENT_STREAM && !fl(p, F_ACTIVE)) return;
         int32_t prev = -1;
+        // A non-sequence partial whose filter fails keeps nothing of this event (its copy is garbage): the filter is
+        // tried first against one shared copy of the event, and only a partial that passes gets its own copy
+        // (StreamEventCloner.copyStreamEvent), as the reference's per-partial clone would give it.
+        const bool trial = P.kind == PK_STREAM && !P.sequence && P.progLen != 0;
+        int32_t shared = -1;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
           int32_t s = ln_rec(ln);
           if (P.withinCnt > 0 && expired(p, s, now)) {
             ln = lerase(p, 0, prev, ln);
             continue;
+          }
+          if (trial) {
+            if (shared < 0) shared = copy_event(evr);
+            set_slot(s, sid, shared);
+            const bool pass = filter_pass(p, s);
+            set_slot(s, sid, -1);
+            if (!pass) {
+              setfl(p, F_STATE_CHANGED, false);
+              prev = ln;
+              ln = ln_next(ln);
+              continue;
+            }
           }
           set_slot(s, sid, copy_event(evr));
           pre_process(p, s);
@@ -700,12 +717,27 @@ struct Lane {
       }
       case PK_COUNT: {  // CountPreStateProcessor.processAndReturn :58-93
         int32_t prev = -1;
+        const bool trial = !P.sequence && P.progLen != 0;  // as for PK_STREAM: a failing partial keeps nothing
+        int32_t shared = -1;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
           int32_t s = ln_rec(ln);
           if ((PQ->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (PQ->nslots > sid + 2 && slot(s, sid + 2) >= 0)) {
             ln = lerase(p, 0, prev, ln);
             continue;
+          }
+          if (trial) {
+            if (shared < 0) shared = copy_event(evr);
+            add_event(s, sid, shared);
+            const bool pass = filter_pass(p, s);
+            remove_last_event(s, sid);
+            if (!pass) {
+              setfl(p, F_SUCCESS, false);
+              setfl(p, F_STATE_CHANGED, false);
+              prev = ln;
+              ln = ln_next(ln);
+              continue;
+            }
           }
           add_event(s, sid, copy_event(evr));
           setfl(p, F_SUCCESS, false);
