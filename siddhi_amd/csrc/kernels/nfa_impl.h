@@ -668,10 +668,10 @@ struct Lane {
       case PK_ABSENT_STREAM: {
         if (P.kind == PK_ABSENT_STREAM && !fl(p, F_ACTIVE)) return;
         int32_t prev = -1;
-        // A non-sequence partial whose filter fails keeps nothing of this event (its copy is garbage): the filter is
-        // tried first against one shared copy of the event, and only a partial that passes gets its own copy
+        // A partial whose filter fails keeps nothing of this event (its copy is garbage): the filter is tried first
+        // against one shared copy of the event, and only a partial that passes gets its own copy
         // (StreamEventCloner.copyStreamEvent), as the reference's per-partial clone would give it.
-        const bool trial = P.kind == PK_STREAM && !P.sequence && P.progLen != 0;
+        const bool trial = P.kind == PK_STREAM && P.progLen != 0;
         int32_t shared = -1;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
@@ -685,10 +685,16 @@ struct Lane {
             set_slot(s, sid, shared);
             const bool pass = filter_pass(p, s);
             set_slot(s, sid, -1);
-            if (!pass) {
+            if (!pass) {  // what the loop below does for a partial the filter rejects
               setfl(p, F_STATE_CHANGED, false);
-              prev = ln;
-              ln = ln_next(ln);
+              if (!P.sequence) {
+                prev = ln;
+                ln = ln_next(ln);
+              } else {
+                ln = lerase(p, 0, prev, ln);
+                int cb = PPOST[P.post].callbackPre;
+                if (cb >= 0) count_startStateReset(cb);
+              }
               continue;
             }
           }
@@ -717,7 +723,7 @@ struct Lane {
       }
       case PK_COUNT: {  // CountPreStateProcessor.processAndReturn :58-93
         int32_t prev = -1;
-        const bool trial = !P.sequence && P.progLen != 0;  // as for PK_STREAM: a failing partial keeps nothing
+        const bool trial = P.progLen != 0;  // as for PK_STREAM: a failing partial keeps nothing of the event
         int32_t shared = -1;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
@@ -731,11 +737,15 @@ struct Lane {
             add_event(s, sid, shared);
             const bool pass = filter_pass(p, s);
             remove_last_event(s, sid);
-            if (!pass) {
+            if (!pass) {  // what the loop below does for a partial the filter rejects
               setfl(p, F_SUCCESS, false);
               setfl(p, F_STATE_CHANGED, false);
-              prev = ln;
-              ln = ln_next(ln);
+              if (!P.sequence) {
+                prev = ln;
+                ln = ln_next(ln);
+              } else {
+                ln = lerase(p, 0, prev, ln);
+              }
               continue;
             }
           }
