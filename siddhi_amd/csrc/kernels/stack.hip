@@ -53,7 +53,10 @@ constexpr int kOvf = 1024;     // ... and a shared overflow (more: the batch tak
 // matches of a tile staged in LDS before one coalesced write (what the tile counts leave of the LDS; none for tiles of
 // 2^15 ordinals, whose direct writes land in a ~190 KB window that the L2 combines)
 constexpr int kOCap = kOT * 4 + 12288 * 8 <= 160 * 1024 ? 12288 : 0;
-constexpr int kGT = kTB >= 15 ? 4 : 16;  // consecutive tiles per order workgroup
+#ifndef SM_ORDER_GT
+#define SM_ORDER_GT (SM_ORDER_TB >= 15 ? 4 : 16)  // A/B build flag
+#endif
+constexpr int kGT = SM_ORDER_GT;  // consecutive tiles per order workgroup
 
 static_assert(kBins == kKeys && kKeys == kKPT * kSB && kBins == kOB && (kKPT == 1 || kKPT == 2),
               "one or two in-bucket keys per thread, one bucket per order thread");
