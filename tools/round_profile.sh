@@ -24,8 +24,8 @@ cd "$ROOT"
 step bench_full 600 python -u bench.py "$@"
 cd /tmp
 step prof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_stats" -o run -- \
-  python3 "$ROOT/bench.py" --no-cpu --no-e2e --steps 3 --warmup 1 "$@"
+  python3 "$ROOT/bench.py" --no-cpu --no-e2e --no-ih --no-sparse --steps 3 --warmup 1 "$@"
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-  python3 "$ROOT/bench.py" --no-cpu --no-e2e --steps 1 --warmup 0 "$@"
+  python3 "$ROOT/bench.py" --no-cpu --no-e2e --no-ih --no-sparse --steps 1 --warmup 0 "$@"
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-  python3 "$ROOT/bench.py" --no-cpu --no-e2e --steps 1 --warmup 0 "$@"
+  python3 "$ROOT/bench.py" --no-cpu --no-e2e --no-ih --no-sparse --steps 1 --warmup 0 "$@"

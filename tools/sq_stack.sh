@@ -10,7 +10,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   i=$((i+1))
   echo "== pass $i: $grp"
   rm -rf "$ROOT/gpurun_out/sq_$i"
-  timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-stack_kernel}" --output-format csv -d "$ROOT/gpurun_out/sq_$i" -o run -- python3 "$ROOT/bench.py" --no-cpu ${SQ_ARGS:---no-e2e --events 1e9} --steps 1 --warmup 0 > "$ROOT/gpurun_out/sq_$i.log" 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-stack4_kernel}" --output-format csv -d "$ROOT/gpurun_out/sq_$i" -o run -- python3 "$ROOT/bench.py" --no-cpu ${SQ_ARGS:---no-e2e --no-ih --no-sparse --events 1e9} --steps 1 --warmup 0 > "$ROOT/gpurun_out/sq_$i.log" 2>&1
   rc=$?
   echo "rc=$rc"
   [ $rc -ne 0 ] && tail -5 "$ROOT/gpurun_out/sq_$i.log" && exit $rc
