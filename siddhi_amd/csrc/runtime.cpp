@@ -395,7 +395,7 @@ struct sm_app {
         if (b.p) (void)hipHostFree(b.p);
     }
   } out_arena;
-  // no JSON dump, no callback, no chaining: outputs are copied to the host and counted, no HostOut is built
+  // no JSON dump, no callback, no chaining: outputs are counted and stay in device memory, no HostOut is built
   bool outputs_unconsumed() const;
   bool need_outs = false;  // set while a caller reads the output records itself (nfa_device_batch)
   bool in_device_events = false;  // inside sm_app_process_device_events (keep_outputs applies)
@@ -907,13 +907,14 @@ void run_callbacks(Pending& out) {
 
 void read_outputs(sm_app* a, int qidx, const void* dev, int64_t n, std::vector<HostOut>& outs) {
   if (n <= 0) return;
+  a->queries[qidx]->n_out += n;
+  // no callback, no dump, no chaining: the records stay in device memory (sm_app_copy_device_outputs), counted
+  if (a->outputs_unconsumed()) return;
   const CompiledQuery& cq = a->queries[qidx]->cq;
   size_t stride = sizeof(OutRec) + cq.hdr.nsel * sizeof(DVal) + cq.hdr.nrefs * sizeof(int64_t);
   char* host = a->out_arena.take((size_t)n * stride);
   SM_HIP(hipMemcpyAsync(host, dev, (size_t)n * stride, hipMemcpyDeviceToHost, a->stream));
   SM_HIP(hipStreamSynchronize(a->stream));
-  a->queries[qidx]->n_out += n;
-  if (a->outputs_unconsumed()) return;
   outs.reserve(outs.size() + (size_t)n);
   for (int64_t k = 0; k < n; ++k) {
     const char* b = host + (size_t)k * stride;
