@@ -44,6 +44,9 @@ struct DenseKeys {
 void key_range(const void* col, int key_type, int64_t n, int64_t* lo, int64_t* hi, Scratch& sc, hipStream_t s);
 // out[i] = dense id of key column col[i] (key_type T_INT or T_LONG), new keys added; n events.
 void remap_keys(DenseKeys& D, const void* col, int key_type, int64_t n, int32_t* out, hipStream_t s);
+// the key word (word 0) of n carried closed-form rows of `width` words, in place: raw key -> dense id (a query that
+// starts giving its keys dense ids after partials were carried under their values)
+void remap_carry_keys(DenseKeys& D, int64_t* rows, int64_t n, int width, Scratch& sc, hipStream_t s);
 
 // FilterProcessor over rows [0, n) of one stream; writes matching row indices (ascending), returns the count.
 int64_t filter_rows(const NfaStream* st_dev, int64_t n, const Instr* code, int len, const DVal* consts,

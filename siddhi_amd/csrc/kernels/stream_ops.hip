@@ -1081,6 +1081,29 @@ __global__ void __launch_bounds__(256) carry_columns_kernel(const int64_t* __res
 }
 }  // namespace
 
+namespace {
+__global__ void strided_get_kernel(const int64_t* __restrict__ rows, int64_t n, int w, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = rows[i * w];
+}
+__global__ void strided_put_kernel(const int32_t* __restrict__ ids, int64_t n, int w, int64_t* __restrict__ rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) rows[i * w] = ids[i];
+}
+}  // namespace
+
+void remap_carry_keys(DenseKeys& D, int64_t* rows, int64_t n, int width, Scratch& sc, hipStream_t s) {
+  if (n <= 0) return;
+  const size_t mark = sc.used;
+  int64_t* k = (int64_t*)sc.take((size_t)n * 8);
+  int32_t* ids = (int32_t*)sc.take((size_t)n * 4);
+  hipLaunchKernelGGL(strided_get_kernel, grid_for(n), dim3(256), 0, s, (const int64_t*)rows, n, width, k);
+  remap_keys(D, k, T_LONG, n, ids, s);  // an INT key's carried value is its sign extension: the same table entry
+  hipLaunchKernelGGL(strided_put_kernel, grid_for(n), dim3(256), 0, s, (const int32_t*)ids, n, width, rows);
+  SM_HIP(hipStreamSynchronize(s));
+  sc.used = mark;
+}
+
 void carry_rows_to_columns(const int64_t* rows, int64_t n, const CarryCols& c, hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(carry_columns_kernel, grid_for(n), dim3(256), 0, s, rows, n, c);
 }

@@ -2086,6 +2086,20 @@ void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const 
     if (!a->force_general_fast)
       m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
                                a->fast_timing ? &a->fast_tm : nullptr, a->fast_stack);
+    if (m == FAST_KEY_SPAN && q.remap == 2 && a->key_remap < 0) {
+      // the first batch's keys fitted their values, this one's do not: dense ids from here on, for the carried
+      // partials' keys too (each key's rows stay one run, so the carry keeps its grouping)
+      q.remap = 1;
+      remap_carry_keys(q.dense, q.carry.rows, q.carry.n, q.carry.width, a->sc, hs);
+      if (q.carry.n > 0)
+        SM_HIP(hipMemcpyAsync(q.prev_carry.p, q.carry.rows, (size_t)q.carry.n * q.carry.width * 8,
+                              hipMemcpyDeviceToDevice, hs));
+      int32_t* dk = (int32_t*)a->sc.take(n * 4);
+      remap_keys(q.dense, hi.cols[hi.key_col], hi.key_type, (int64_t)n, dk, hs);
+      hi.dense_keys = dk;
+      m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
+                               a->fast_timing ? &a->fast_tm : nullptr, a->fast_stack);
+    }
     q.fast_path_used = q.fast.last_path;
     if (m == FAST_OUTSIDE && a->force_general_fast && q.carry.n == 0) {
       // diagnostic (option "fast_general"): the stateless general closed form, one batch at a time

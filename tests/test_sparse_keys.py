@@ -71,14 +71,15 @@ def test_million_sparse_64bit_keys_take_bucket_stack():
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("logk", [10, 16, 20, 22, 24])
 def test_key_counts_stay_on_closed_form(logk):
-    """2^10 .. 2^24 sparse keys: bucket stack or sort / walk (never the NFA hand-over), equal to the brute force."""
+    """2^10 .. 2^24 sparse keys: bucket stack or sort / walk (never the NFA hand-over), the same pipeline the dense
+    symbols of the same stream take (sort / walk up to 2^19 keys in a batch, bucket stack above), equal to the brute
+    force."""
     import torch
     N = 8_000_000
     sym, key, price, ts = sparse_stream(N, 1 << logk, 100)
     got, paths = run(LONG_APP, key, price, ts)
-    assert paths[0] in (2, 3), paths
-    if logk <= 20:
-        assert paths[0] == 3
+    _, dense_paths = run(bench.APP, sym, price, ts)
+    assert paths[0] in (2, 3) and paths == dense_paths, (paths, dense_paths)
     ref = closed_form_torch(key, price, ts, 1000)
     assert torch.equal(ref, got)
 
