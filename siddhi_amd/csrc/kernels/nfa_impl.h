@@ -668,9 +668,10 @@ struct Lane {
       case PK_ABSENT_STREAM: {
         if (P.kind == PK_ABSENT_STREAM && !fl(p, F_ACTIVE)) return;
         int32_t prev = -1;
-        // A partial whose filter fails keeps nothing of this event (its copy is garbage): the filter is tried first
-        // against one shared copy of the event, and only a partial that passes gets its own copy
-        // (StreamEventCloner.copyStreamEvent), as the reference's per-partial clone would give it.
+        // A partial whose filter fails keeps nothing of this event (its copy is garbage): the filter is tried
+        // against one copy of the event shared by the failing partials; the first partial that passes keeps that
+        // copy as its own (StreamEventCloner.copyStreamEvent: one clone per partial) and the next trial makes a
+        // fresh one.
         const bool trial = P.kind == PK_STREAM && P.progLen != 0;
         int32_t shared = -1;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
@@ -683,10 +684,9 @@ struct Lane {
           if (trial) {
             if (shared < 0) shared = copy_event(evr);
             set_slot(s, sid, shared);
-            const bool pass = filter_pass(p, s);
-            set_slot(s, sid, -1);
-            if (!pass) {  // what the loop below does for a partial the filter rejects
-              setfl(p, F_STATE_CHANGED, false);
+            setfl(p, F_STATE_CHANGED, false);
+            if (!filter_pass(p, s)) {  // what the loop below does for a partial the filter rejects
+              set_slot(s, sid, -1);
               if (!P.sequence) {
                 prev = ln;
                 ln = ln_next(ln);
@@ -697,9 +697,12 @@ struct Lane {
               }
               continue;
             }
+            shared = -1;
+            post_process(P.post, s);  // pre_process after its filter
+          } else {
+            set_slot(s, sid, copy_event(evr));
+            pre_process(p, s);
           }
-          set_slot(s, sid, copy_event(evr));
-          pre_process(p, s);
           int tl = P.thisLast;
           if (returned(tl)) {
             set_returned(tl, 0);
@@ -735,11 +738,10 @@ struct Lane {
           if (trial) {
             if (shared < 0) shared = copy_event(evr);
             add_event(s, sid, shared);
-            const bool pass = filter_pass(p, s);
-            remove_last_event(s, sid);
-            if (!pass) {  // what the loop below does for a partial the filter rejects
-              setfl(p, F_SUCCESS, false);
-              setfl(p, F_STATE_CHANGED, false);
+            setfl(p, F_SUCCESS, false);
+            setfl(p, F_STATE_CHANGED, false);
+            if (!filter_pass(p, s)) {  // what the loop below does for a partial the filter rejects
+              remove_last_event(s, sid);
               if (!P.sequence) {
                 prev = ln;
                 ln = ln_next(ln);
@@ -748,10 +750,13 @@ struct Lane {
               }
               continue;
             }
+            shared = -1;  // the partial keeps the copy
+            post_process(P.post, s);  // pre_process after its filter
+          } else {
+            add_event(s, sid, copy_event(evr));
+            setfl(p, F_SUCCESS, false);
+            pre_process(p, s);
           }
-          add_event(s, sid, copy_event(evr));
-          setfl(p, F_SUCCESS, false);
-          pre_process(p, s);
           int tl = P.thisLast;
           if (returned(tl)) {
             set_returned(tl, 0);

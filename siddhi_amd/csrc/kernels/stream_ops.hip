@@ -480,42 +480,82 @@ constexpr int64_t kDkBusy = -1;
 // with its id; a reader meeting a busy entry reads it again (the claiming lane fills it in the same loop iteration,
 // so no lane waits on work another lane of its wave has not done yet). An id beyond the id capacity releases the
 // entry and flags an overflow: the host grows the table and runs the batch again (found keys are found again).
+// One key from entry h on: plain reads while they decide, then the atomic protocol.
+__device__ __noinline__ int32_t dk_lookup(int64_t k, uint64_t h, int64_t* __restrict__ table, uint64_t mask,
+                                          int64_t* __restrict__ slot_keys, int64_t limit, uint32_t* __restrict__ counter,
+                                          uint32_t* __restrict__ overflow) {
+  int32_t res = -1;
+  uint64_t probes = 0;
+  // found keys (all but the first sighting of each) with plain 16-byte reads: a non-zero key word is final (written
+  // once, before its entry is published), so an entry holding another key is passed over and one holding this key
+  // with a published id is a hit; an empty or busy entry, an entry whose key word is not visible yet, or the key 0
+  // go on at that entry with the atomic protocol
+  if (k != 0) {
+    while (probes <= mask) {
+      const longlong2 e = *(const longlong2*)&table[2 * h];
+      if (e.x == k && e.y > 0) return (int32_t)(e.y - 1);
+      if (e.x == 0 || e.x == k) break;
+      h = (h + 1) & mask;
+      ++probes;
+    }
+  }
+  while (probes <= mask) {
+    unsigned long long* st = (unsigned long long*)&table[2 * h + 1];
+    const int64_t sv = (int64_t)__hip_atomic_load(st, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (sv == kDkBusy) continue;
+    if (sv == 0) {
+      if (atomicCAS(st, 0ull, (unsigned long long)kDkBusy) != 0ull) continue;
+      const uint32_t id = atomicAdd(counter, 1u);
+      if ((int64_t)id >= limit) {
+        __hip_atomic_store(st, 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        atomicOr(overflow, 1u);
+        break;
+      }
+      table[2 * h] = k;
+      slot_keys[id] = k;
+      __hip_atomic_store(st, (unsigned long long)id + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      res = (int32_t)id;
+      break;
+    }
+    if (table[2 * h] == k) {
+      res = (int32_t)(sv - 1);
+      break;
+    }
+    h = (h + 1) & mask;
+    ++probes;
+  }
+  return res;
+}
+
+// Each thread resolves kDkU keys at a time: their first entries are read together (kDkU independent random reads in
+// flight per lane), and the keys not found at their first entry go through dk_lookup.
+constexpr int kDkU = 4;
 template <typename KT>
 __global__ void __launch_bounds__(256) remap_kernel(const KT* __restrict__ col, int64_t n, int64_t* __restrict__ table,
                                                     uint64_t mask, int64_t* __restrict__ slot_keys, int64_t limit,
                                                     uint32_t* __restrict__ counter, int32_t* __restrict__ out,
                                                     uint32_t* __restrict__ overflow) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = (int64_t)col[i];
-    uint64_t h = mix64((uint64_t)k) & mask;
-    int32_t res = -1;
-    uint64_t probes = 0;
-    while (probes <= mask) {
-      unsigned long long* st = (unsigned long long*)&table[2 * h + 1];
-      const int64_t sv = (int64_t)__hip_atomic_load(st, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      if (sv == kDkBusy) continue;
-      if (sv == 0) {
-        if (atomicCAS(st, 0ull, (unsigned long long)kDkBusy) != 0ull) continue;
-        const uint32_t id = atomicAdd(counter, 1u);
-        if ((int64_t)id >= limit) {
-          __hip_atomic_store(st, 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          atomicOr(overflow, 1u);
-          break;
-        }
-        table[2 * h] = k;
-        slot_keys[id] = k;
-        __hip_atomic_store(st, (unsigned long long)id + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        res = (int32_t)id;
-        break;
-      }
-      if (table[2 * h] == k) {
-        res = (int32_t)(sv - 1);
-        break;
-      }
-      h = (h + 1) & mask;
-      ++probes;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * kDkU) {
+    int64_t k[kDkU];
+    uint64_t h[kDkU];
+    longlong2 e[kDkU];
+#pragma unroll
+    for (int u = 0; u < kDkU; ++u) {
+      const int64_t i = i0 + u * stride;
+      k[u] = i < n ? (int64_t)col[i] : 0;
+      h[u] = mix64((uint64_t)k[u]) & mask;
     }
-    out[i] = res;
+#pragma unroll
+    for (int u = 0; u < kDkU; ++u) e[u] = *(const longlong2*)&table[2 * h[u]];
+#pragma unroll
+    for (int u = 0; u < kDkU; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n) break;
+      out[i] = (k[u] != 0 && e[u].x == k[u] && e[u].y > 0)
+                   ? (int32_t)(e[u].y - 1)
+                   : dk_lookup(k[u], h[u], table, mask, slot_keys, limit, counter, overflow);
+    }
   }
 }
 

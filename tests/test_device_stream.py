@@ -278,7 +278,8 @@ def test_outside_envelope_streams_through_nfa(c2):
 
 
 def test_host_events_then_device_batches():
-    """Partials opened by host-API events (NFA state) continue into device batches."""
+    """Partials opened by host-API events continue into device batches: the host events take the closed form too
+    (the app's only query is eligible, §1d), so the device batches continue its carry."""
     import torch
     from siddhi_amd.testing import ProductApp
     n, K, div = 20000, 80, 5
@@ -297,7 +298,7 @@ def test_host_events_then_device_batches():
         tcols = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
         tts = torch.from_numpy(np.ascontiguousarray(ts[lo:hi])).to(dev)
         app.process_device_batch("StockStream", tts, tcols, ordinal_base=lo)
-        assert app.get_stat("fast_path:q") == 5
+        assert app.get_stat("fast_path:q") in (2, 3)
         got.append(app.device_matches_host("q").view(np.int32).astype(np.int64) + lo)
     app.close()
     np.testing.assert_array_equal(np.concatenate(got), exp)

@@ -94,7 +94,7 @@ def test_dense_ids_persist_across_batches_and_snapshots():
     whole, _ = run(LONG_APP, key, price, ts)
     cuts = [0, 1, 77_777, 1_000_003, 1_000_004, 2_222_222, N]
     split, paths = run(LONG_APP, key, price, ts, ranges=list(zip(cuts[:-1], cuts[1:])))
-    assert set(paths[2:]) == {3}
+    assert set(paths) <= {2, 3}  # closed form throughout (sort / walk: about 2e5 keys per batch)
     assert torch.equal(split, whole)
     # snapshot after 1e6 events, restore into a fresh runtime, continue
     a = ProductApp(LONG_APP)
