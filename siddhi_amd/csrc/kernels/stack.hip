@@ -494,7 +494,6 @@ __global__ void __launch_bounds__(256) transpose_kernel(const uint32_t* __restri
 
 struct OrderArgs {
   const uint64_t* stage;
-  uint32_t nstage;     // entries allocated for stage (reads of whole lines stay below)
   const uint32_t* sbase;
   const uint32_t* mt;  // [t][d]: matches of bucket d whose j precedes tile t
   int64_t ntiles;
@@ -599,140 +598,6 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
           const bool valid = c + l16 < lenr[r];
           place(valid ? a.stage[s0r[r] + c + l16] : 0ull, valid, c, cj, cstart);
         }
-    }
-    lds_barrier();
-    if (staged)
-      for (uint32_t k = tid; k < tot; k += kOB) a.out[out + k] = obuf[k];
-    out += tot;
-  }
-}
-
-// order_kernel reading each bucket's staging run once. A tile's segment of a bucket ends inside a 128-byte line that
-// the next tile's segment starts in; order_kernel fetched that line again per tile (config 4: 21.3 GB read for
-// 5.6 GB staged, the lines evicted from L2 between a workgroup's tiles). Here each 16-lane group keeps, per bucket it
-// serves, the line holding the bucket's cursor (line A) in registers from tile to tile, aligned to lines: lane l holds
-// entry (line start + l); a segment that goes on past line A reads the next line (B), which becomes line A of the next
-// tile when the segment ends inside it. Entries beyond line B (segments of more than 17 .. 32 entries, rare) are read
-// directly as in order_kernel.
-__global__ void __launch_bounds__(kOB) order_lines_kernel(OrderArgs a) {
-  __shared__ uint32_t cnt[kOT];
-  __shared__ uint64_t obuf[kOCap > 0 ? kOCap : 1];
-  __shared__ uint32_t sst[kBins], slen[kBins];
-  __shared__ uint32_t lw[kOB / 64];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int l16 = lane & 15, g = lane >> 4;
-  const uint64_t gmask = 0xffffull << (g * 16);
-  const int64_t tb = (int64_t)blockIdx.x * kGT;
-  const int64_t te = tb + kGT < a.ntiles ? tb + kGT : a.ntiles;
-  uint32_t ms = a.mt[tb * kBins + tid];
-  uint32_t tot;
-  (void)block_excl(ms, lw, &tot);
-  int64_t out = tot;  // matches whose j precedes the tile
-  auto ld = [&](uint32_t i) -> uint64_t { return i < a.nstage ? a.stage[i] : 0ull; };
-  uint64_t la[16];
-  uint32_t hasa = 0;  // bit r: la[r] holds the line of bucket w * 64 + r * 4 + g's cursor
-#pragma unroll
-  for (int r = 0; r < 16; ++r) la[r] = 0ull;
-  for (int64_t t = tb; t < te; ++t) {
-    const uint32_t me = a.mt[(t + 1) * kBins + tid];
-    const uint32_t j0 = (uint32_t)(t << kTB);
-    lds_barrier();  // previous tile's readers are done
-    sst[tid] = a.sbase[tid] + ms;
-    slen[tid] = me - ms;
-    for (int e = tid; e < kOT; e += kOB) cnt[e] = 0;
-    ms = me;
-    lds_barrier();
-    bool more = false;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int d = w * 64 + r * 4 + g;
-      const uint32_t s0 = sst[d], e = s0 + slen[d], base = s0 & ~15u;
-      if (e != s0) {
-        if (!((hasa >> r) & 1u)) la[r] = ld(base + l16);
-        more |= e > base + 32u;
-      }
-    }
-    // pass A: matches per ordinal
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int d = w * 64 + r * 4 + g;
-      const uint32_t s0 = sst[d], e = s0 + slen[d], ia = (s0 & ~15u) + l16;
-      if (ia >= s0 && ia < e) atomicAdd(&cnt[(uint32_t)(la[r] >> 32) - j0], 1u);
-      if (ia + 16u < e) atomicAdd(&cnt[(uint32_t)(ld(ia + 16u) >> 32) - j0], 1u);
-    }
-    if (__any(more))
-      for (int r = 0; r < 16; ++r) {
-        const int d = w * 64 + r * 4 + g;
-        const uint32_t s0 = sst[d], e = s0 + slen[d];
-        for (uint32_t c = (s0 & ~15u) + 32u; __any(c < e); c += 16)
-          if (c + l16 < e) atomicAdd(&cnt[(uint32_t)(ld(c + l16) >> 32) - j0], 1u);
-      }
-    lds_barrier();
-    {
-      constexpr int kPer = kOT / kOB;
-      uint32_t v[kPer], sum = 0;
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        v[k] = cnt[tid * kPer + k];
-        sum += v[k];
-      }
-      uint32_t r = block_excl(sum, lw, &tot);
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        cnt[tid * kPer + k] = r;
-        r += v[k];
-      }
-    }
-    lds_barrier();
-    const bool staged = kOCap > 0 && tot <= (uint32_t)kOCap;
-    // pass B: as in order_kernel, with chunk positions relative to the segment start (line A starts before it: its
-    // lanes below the start are not valid, and the first valid lane always starts a run, since the entry before it
-    // is an earlier tile's or another bucket's, whose j differs)
-    auto place = [&](uint64_t v, bool valid, uint32_t c, uint32_t& cj, uint32_t& cstart) {
-      const uint32_t j = (uint32_t)(v >> 32);
-      uint32_t jp = __shfl_up(j, 1, 16);
-      if (l16 == 0) jp = cj;
-      const bool start = valid && j != jp;
-      const uint32_t sm = (uint32_t)((__ballot(start) & gmask) >> (g * 16));
-      const uint32_t upto = sm & ((2u << l16) - 1u);
-      const uint32_t rs = upto ? c + 31u - (uint32_t)__clz(upto) : cstart;
-      if (valid) {
-        const uint32_t pos = cnt[j - j0] + (c + l16 - rs);
-        if (staged) obuf[pos] = v;
-        else a.out[out + pos] = v;
-      }
-      const uint32_t vm = (uint32_t)((__ballot(valid) & gmask) >> (g * 16));
-      const int last = vm ? 31 - __clz(vm) : 0;
-      cj = __shfl(j, last, 16);
-      cstart = __shfl(rs, last, 16);
-    };
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int d = w * 64 + r * 4 + g;
-      const uint32_t s0 = sst[d], e = s0 + slen[d], base = s0 & ~15u, ia = base + l16;
-      uint32_t cj = 0xffffffffu, cstart = 0;
-      place(la[r], ia >= s0 && ia < e, base - s0, cj, cstart);
-      uint64_t lb = 0ull;  // line B again (read in pass A moments ago: an L2 hit)
-      if (__any(base + 16u < e)) {
-        if (e > base + 16u) lb = ld(ia + 16u);
-        place(lb, ia + 16u < e, base + 16u - s0, cj, cstart);
-      }
-      if (__any(base + 32u < e))
-        for (uint32_t c = base + 32u; __any(c < e); c += 16) {
-          const bool valid = c + l16 < e;
-          place(valid ? ld(c + l16) : 0ull, valid, c - s0, cj, cstart);
-        }
-      if (e != s0) {  // the next tile's segment starts at e: keep its line when it is held
-        const uint32_t nb = e & ~15u;
-        if (nb == base) {
-          hasa |= 1u << r;
-        } else if (nb == base + 16u && e > base + 16u) {
-          la[r] = lb;
-          hasa |= 1u << r;
-        } else {
-          hasa &= ~(1u << r);
-        }
-      }
     }
     lds_barrier();
     if (staged)
@@ -1106,7 +971,6 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
     }
     OrderArgs oa{};
     oa.stage = sa.stage;
-    oa.nstage = (uint32_t)std::min<int64_t>(n + extra, 0xffffffffll);
     oa.sbase = sbase;
     oa.out = (uint64_t*)pairs_out;
     if (M > 0) {
@@ -1115,11 +979,10 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
                          sa.mstart, sa.ntiles + 1, mt);
       oa.mt = mt;
       oa.ntiles = sa.ntiles;
-      static const bool per_tile = !(getenv("SM_ORDER_LINES") && atoi(getenv("SM_ORDER_LINES")) != 0);  // A/B
-      if (per_tile)
-        hipLaunchKernelGGL(order_kernel, dim3((unsigned)((sa.ntiles + kGT - 1) / kGT)), dim3(kOB), 0, s, oa);
-      else
-        hipLaunchKernelGGL(order_lines_kernel, dim3((unsigned)((sa.ntiles + kGT - 1) / kGT)), dim3(kOB), 0, s, oa);
+      // (a variant keeping each bucket's cursor line in registers from tile to tile, so that the line shared by
+      // consecutive tiles' segments is fetched once, was exact but slower, 15.5 against 6.6 ms: the held lines
+      // spill at 1024 threads x 128 VGPRs, and line B's reads then wait one by one)
+      hipLaunchKernelGGL(order_kernel, dim3((unsigned)((sa.ntiles + kGT - 1) / kGT)), dim3(kOB), 0, s, oa);
     }
   }
   tmark("order");
