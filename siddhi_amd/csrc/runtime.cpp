@@ -144,6 +144,7 @@ struct RawVec {
   std::unique_ptr<T[]> p;
   size_t n = 0, cap = 0;
   size_t size() const { return n; }
+  bool empty() const { return n == 0; }
   T* data() { return p.get(); }
   const T* data() const { return p.get(); }
   T& operator[](size_t i) { return p[i]; }
@@ -186,7 +187,7 @@ struct PreparedChunk {
 // the callbacks can run after the lock is released. Until finalise(), an event's data field holds the offset of its
 // values in vals (vals still grows); finalise() turns the offsets into pointers once the call's outputs are complete.
 struct Pending {
-  std::vector<PreparedChunk> chunks;
+  RawVec<PreparedChunk> chunks;
   std::vector<Callback> cbs;
   RawVec<sm_event> evs;
   RawVec<sm_value> vals;
@@ -894,7 +895,14 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
 // cannot throw across the ABI.
 void run_callbacks(Pending& out) {
   if (out.chunks.empty()) return;
-  out.finalise();
+  if (!out.final_) {  // Pending::finalise on the host threads
+    sm_value* vals = out.vals.data();
+    sm_event* evs = out.evs.data();
+    parallel_for(out.evs.size(), (size_t)1 << 16, [&](size_t lo, size_t hi) {
+      for (size_t k = lo; k < hi; ++k) evs[k].data = vals + (uintptr_t)evs[k].data;
+    });
+    out.final_ = true;
+  }
   for (auto& ch : out.chunks) {
     const sm_event* evs = out.evs.data() + ch.ev_off;
     for (uint32_t c = 0; c < ch.n_cbs; ++c) {
@@ -1450,12 +1458,15 @@ void deliver_direct(sm_app* a, const DevOut& d) {
       }
     }
   });
-  for (size_t c = c0; c < pd.chunks.size(); ++c) {  // sizes and timestamps (the chunk's last event's)
-    PreparedChunk& ch = pd.chunks[c];
-    const size_t end = c + 1 < pd.chunks.size() ? pd.chunks[c + 1].ev_off : e0 + m;
-    ch.n_ev = end - ch.ev_off;
-    ch.ts = pd.evs[end - 1].timestamp;
-  }
+  const size_t nch = pd.chunks.size();
+  parallel_for(nch - c0, (size_t)1 << 16, [&](size_t lo, size_t hi) {  // sizes and timestamps (the last event's)
+    for (size_t c = c0 + lo; c < c0 + hi; ++c) {
+      PreparedChunk& ch = pd.chunks[c];
+      const size_t end = c + 1 < nch ? pd.chunks[c + 1].ev_off : e0 + m;
+      ch.n_ev = end - ch.ev_off;
+      ch.ts = pd.evs[end - 1].timestamp;
+    }
+  });
   bool strings = false;
   for (int t : cq.sel_types) strings |= t == T_STRING;
   if (strings)  // STRING values are owned by the pending outputs (the dictionary may change before the callbacks)
