@@ -34,6 +34,7 @@ struct FastHostInfo {
   int c1_len = 0;
   int nattr = 0;              // attributes of the stream (carried partial rows)
   const int32_t* dense_keys = nullptr;  // device: the key column as dense ids (remap_keys), read instead of the column
+  int64_t remap_span = 0;  // > 0: a key span above it returns FAST_KEY_SPAN (the caller gives the keys dense ids)
 };
 
 // Device facts cached across batches by the v2 kernels.
@@ -89,8 +90,9 @@ enum : int64_t { FAST_OUTSIDE = -1, FAST_NON_MONOTONE = -2, FAST_KEY_SPAN = -3 }
 
 // FAST_OUTSIDE: outside the v2 envelope (caller falls back to fast_every_within); FAST_NON_MONOTONE: event time
 // decreases inside the batch or against the carried state (the closed form does not apply: the caller takes the
-// general NFA path); FAST_KEY_SPAN: the partition keys (carried ones included) span more than 2^30 values (the
-// caller may give them dense ids and run the batch again; nothing was changed). Match pairs are relative to a.ordinal_base; an e1 carried from an earlier batch has a
+// general NFA path); FAST_KEY_SPAN: the partition keys (carried ones included) span more than 2^30 values, or more
+// than hi.remap_span when that is set (the caller may give them dense ids and run the batch again; nothing was
+// changed). Match pairs are relative to a.ordinal_base; an e1 carried from an earlier batch has a
 // negative (int32) relative ordinal. The carry is read and replaced.
 int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastState& fs, FastCarry& carry,
                              uint32_t* pairs_out, int64_t pairs_cap, Scratch& sc, hipStream_t s,

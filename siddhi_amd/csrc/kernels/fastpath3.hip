@@ -1636,7 +1636,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     kmin &= ~(int64_t)(kBins - 1);  // rebase on a digit boundary (prep counted digit 0 of the raw key)
     kspan = (uint64_t)((int64_t)(hc.kmax ^ 0x8000000000000000ull) - kmin);
     kbits = std::max(1, bits_for(kspan));
-    if (kbits > 30) {
+    if (kbits > 30 || (hi.remap_span > 0 && kspan > (uint64_t)hi.remap_span)) {
       sc.used = mark;
       return FAST_KEY_SPAN;
     }

@@ -475,6 +475,9 @@ inline dim3 grid_for(int64_t n, int t = 256) { return dim3((unsigned)((n + t - 1
 
 // ---- dense key ids (remap_keys)
 constexpr int64_t kDkBusy = -1;
+#ifndef SM_DK_LOAD_SHIFT
+#define SM_DK_LOAD_SHIFT 1  // A/B build flag: table entries = id capacity << shift
+#endif
 
 // Lookup-or-insert of each event's key. An entry is claimed with a CAS from empty to busy, filled, then published
 // with its id; a reader meeting a busy entry reads it again (the claiming lane fills it in the same loop iteration,
@@ -776,9 +779,11 @@ void DenseKeys::reserve(int64_t slots, hipStream_t s) {
     SM_HIP(hipMalloc(&counter, 8));
     SM_HIP(hipMemsetAsync(counter, 0, 8, s));
   }
-  if (slot_cap * 2 > cap) {  // load factor at most 1/2 when every id is handed out
+  // load factor at most 2^-SM_DK_LOAD_SHIFT when every id is handed out: a wave's lookup takes as many dependent
+  // rounds as its longest probe chain among 64 lanes
+  if ((slot_cap << SM_DK_LOAD_SHIFT) > cap) {
     int64_t nc = std::max<int64_t>(1 << 17, cap);
-    while (nc < slot_cap * 2) nc *= 2;
+    while (nc < (slot_cap << SM_DK_LOAD_SHIFT)) nc *= 2;
     if (table) SM_HIP(hipFree(table));
     SM_HIP(hipMalloc(&table, (size_t)nc * 16));
     SM_HIP(hipMemsetAsync(table, 0, (size_t)nc * 16, s));

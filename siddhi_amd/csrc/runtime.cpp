@@ -2072,13 +2072,11 @@ void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const 
     // keys by any value, so a sparse 64-bit id must not leave the closed form
     if (fa.key && hi.key_col >= 0 && !a->force_general_fast && n > 0) {
       if (q.remap == 0 && !q.carry.active) {
-        if (a->key_remap >= 0) {
-          q.remap = a->key_remap ? 1 : 2;
-        } else {
-          int64_t lo = 0, hi_k = 0;
-          key_range(hi.cols[hi.key_col], hi.key_type, (int64_t)n, &lo, &hi_k, a->sc, hs);
-          q.remap = (uint64_t)hi_k - (uint64_t)lo > ((uint64_t)1 << 20) ? 1 : 2;
-        }
+        // option "key_remap", or (automatic) ids when the first batch's key span exceeds the bucket-stack window
+        // (2^20): the batch runs on the values with remap_span set, and its prep pass reports a wider span
+        // (FAST_KEY_SPAN) before anything changes
+        if (a->key_remap >= 0) q.remap = a->key_remap ? 1 : 2;
+        else hi.remap_span = (int64_t)1 << 20;
       }
       if (q.remap == 1) {  // the pipelines read the ids instead of the key column (the column keeps its values)
         int32_t* dk = (int32_t*)a->sc.take(n * 4);
@@ -2097,10 +2095,12 @@ void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const 
     if (!a->force_general_fast)
       m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
                                a->fast_timing ? &a->fast_tm : nullptr, a->fast_stack);
-    if (m == FAST_KEY_SPAN && q.remap == 2 && a->key_remap < 0) {
-      // the first batch's keys fitted their values, this one's do not: dense ids from here on, for the carried
-      // partials' keys too (each key's rows stay one run, so the carry keeps its grouping)
+    if (m == FAST_KEY_SPAN && q.remap != 1 && a->key_remap < 0 && fa.key && hi.key_col >= 0) {
+      // the first batch's keys span more than the bucket-stack window, or a later batch's keys leave the span the
+      // first batch showed: dense ids from here on, for the carried partials' keys too (each key's rows stay one
+      // run, so the carry keeps its grouping)
       q.remap = 1;
+      hi.remap_span = 0;
       remap_carry_keys(q.dense, q.carry.rows, q.carry.n, q.carry.width, a->sc, hs);
       if (q.carry.n > 0)
         SM_HIP(hipMemcpyAsync(q.prev_carry.p, q.carry.rows, (size_t)q.carry.n * q.carry.width * 8,
@@ -2111,6 +2111,7 @@ void device_batch_stream(sm_app* a, int s, size_t n, const int64_t* d_ts, const 
       m = fast_every_within_v2(fa, hi, q.fast, q.carry, (uint32_t*)q.dev_pairs.p, (int64_t)(n + q.carry.n), a->sc, hs,
                                a->fast_timing ? &a->fast_tm : nullptr, a->fast_stack);
     }
+    if (q.remap == 0 && hi.remap_span > 0 && m != FAST_OUTSIDE) q.remap = 2;  // the span fitted: values from here on
     q.fast_path_used = q.fast.last_path;
     if (m == FAST_OUTSIDE && a->force_general_fast && q.carry.n == 0) {
       // diagnostic (option "fast_general"): the stateless general closed form, one batch at a time
