@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const uint64_t gmask = 0xffffull << (g * 16);
-  // groups of kGT tiles: one per workgroup, or (a smaller grid) several per persistent workgroup
+  // groups of kGT tiles, one per workgroup
   for (int64_t tb = (int64_t)blockIdx.x * kGT; tb < a.ntiles; tb += (int64_t)gridDim.x * kGT) {
   const int64_t te = tb + kGT < a.ntiles ? tb + kGT : a.ntiles;
   uint32_t ms = a.mt[tb * kBins + tid];
@@ -984,12 +984,10 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
       // (a variant keeping each bucket's cursor line in registers from tile to tile, so that the line shared by
       // consecutive tiles' segments is fetched once, was exact but slower, 15.5 against 6.6 ms: the held lines
       // spill at 1024 threads x 128 VGPRs, and line B's reads then wait one by one)
-      // A/B (SM_ORDER_WGS): a persistent grid of fewer workgroups, so fewer tiles' segment lines compete for each
-      // XCD's L2 between a workgroup's consecutive tiles (their shared boundary lines are fetched again otherwise)
-      static const int64_t wgs = getenv("SM_ORDER_WGS") ? atoll(getenv("SM_ORDER_WGS")) : 0;
-      const int64_t groups = (sa.ntiles + kGT - 1) / kGT;
-      const int64_t grid = wgs > 0 ? std::min<int64_t>(groups, wgs) : groups;
-      hipLaunchKernelGGL(order_kernel, dim3((unsigned)grid), dim3(kOB), 0, s, oa);
+      // (a persistent grid of 128 or 64 workgroups, so that fewer tiles' segment lines compete for each XCD's L2,
+      // ran 12.2 / 24.2 ms against 6.7: the kernel is bound by its concurrency, one workgroup per CU, not by the
+      // boundary lines it fetches again)
+      hipLaunchKernelGGL(order_kernel, dim3((unsigned)((sa.ntiles + kGT - 1) / kGT)), dim3(kOB), 0, s, oa);
     }
   }
   tmark("order");
