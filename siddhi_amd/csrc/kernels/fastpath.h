@@ -137,6 +137,7 @@ void build_carry(const int64_t* cand, int64_t ncand, const NfaStream* st, int na
 // kept rows (m u32, ordinal - base), each output reading its own row.
 void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, const int64_t* ord, int64_t n,
                   int64_t base, const int64_t* ts, const int64_t* prev_carry, int64_t nc, int cw, const char* blob_dev,
-                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s, bool rows = false);
+                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s, bool rows = false,
+                  int64_t* words = nullptr, uint8_t* nulls = nullptr);  // words / nulls: compact form (nsel <= 8)
 
 }  // namespace sm

@@ -1049,7 +1049,8 @@ __global__ void pair_project_kernel(const uint32_t* __restrict__ pairs, int64_t 
                                     const int64_t* __restrict__ ts, const int64_t* __restrict__ crow, int cw,
                                     const uint32_t* __restrict__ ckey, const uint32_t* __restrict__ cidx, int64_t nc,
                                     const char* __restrict__ blob, bool rows, DVal* __restrict__ out,
-                                    int64_t* __restrict__ ts_out) {
+                                    int64_t* __restrict__ ts_out, int64_t* __restrict__ words,
+                                    uint8_t* __restrict__ nulls) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= m) return;
   const DQuery* q = (const DQuery*)blob;
@@ -1071,15 +1072,29 @@ __global__ void pair_project_kernel(const uint32_t* __restrict__ pairs, int64_t 
   } else {
     ld.r1 = batch_row(ord, n, base, e1);
   }
-  DVal* o = out + k * q->nsel;
-  for (int a = 0; a < q->nsel; ++a) {
-    const StackVal v = eval_prog(code + sel[3 * a], sel[3 * a + 1], consts, ld);
-    DVal d;
-    if (sel[3 * a + 2] == T_FLOAT || sel[3 * a + 2] == T_DOUBLE) d.d = v.d;
-    else d.i = v.i;
-    d.null = v.null;
-    d.pad = 0;
-    o[a] = d;
+  if (words) {  // compact form (nsel <= 8): one 64-bit word per value, the null flags as bits of one byte
+    int64_t* o = words + k * q->nsel;
+    uint32_t nb = 0;
+    for (int a = 0; a < q->nsel; ++a) {
+      const StackVal v = eval_prog(code + sel[3 * a], sel[3 * a + 1], consts, ld);
+      DVal d;
+      if (sel[3 * a + 2] == T_FLOAT || sel[3 * a + 2] == T_DOUBLE) d.d = v.d;
+      else d.i = v.i;
+      o[a] = d.i;
+      nb |= (v.null ? 1u : 0u) << a;
+    }
+    nulls[k] = (uint8_t)nb;
+  } else {
+    DVal* o = out + k * q->nsel;
+    for (int a = 0; a < q->nsel; ++a) {
+      const StackVal v = eval_prog(code + sel[3 * a], sel[3 * a + 1], consts, ld);
+      DVal d;
+      if (sel[3 * a + 2] == T_FLOAT || sel[3 * a + 2] == T_DOUBLE) d.d = v.d;
+      else d.i = v.i;
+      d.null = v.null;
+      d.pad = 0;
+      o[a] = d;
+    }
   }
   if (ts_out) ts_out[k] = ts[ld.r2];  // StateEvent.timestamp: the last event's (e2's) event time
 }
@@ -1087,7 +1102,8 @@ __global__ void pair_project_kernel(const uint32_t* __restrict__ pairs, int64_t 
 
 void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, const int64_t* ord, int64_t n,
                   int64_t base, const int64_t* ts, const int64_t* prev_carry, int64_t nc, int cw, const char* blob_dev,
-                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s, bool rows) {
+                  DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s, bool rows, int64_t* words,
+                  uint8_t* nulls) {
   if (m <= 0) return;
   const size_t mark = sc.used;
   uint32_t *ck = nullptr, *ci = nullptr;
@@ -1103,7 +1119,7 @@ void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, con
     }
   }
   hipLaunchKernelGGL(pair_project_kernel, grid_of(m), dim3(256), 0, s, pairs, m, st_dev, ord, n, base, ts, prev_carry,
-                     cw, ck, ci, nc, blob_dev, rows, out, ts_out);
+                     cw, ck, ci, nc, blob_dev, rows, out, ts_out, words, nulls);
   SM_HIP(hipGetLastError());
   SM_HIP(hipStreamSynchronize(s));
   sc.used = mark;

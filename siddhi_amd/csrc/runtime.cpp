@@ -124,10 +124,12 @@ struct DevOut {
   int qi;
   int64_t m;
   const uint32_t* hp;
-  const DVal* hv;
+  const DVal* hv;       // values as DVal (nullptr in the compact form)
   const int64_t* hts;
   bool rows;
   int64_t base;
+  const int64_t* hw = nullptr;  // compact form: one 64-bit word per value ...
+  const uint8_t* hn = nullptr;  // ... and one byte of null flags per output (bit a: value a)
 };
 
 struct Callback {
@@ -724,6 +726,27 @@ void to_sm_values(const sm_app* a, const DVal* vals, int nvals, const CompiledQu
       if (id < 0 || id >= (int64_t)a->dict.strs.size()) v.is_null = 1;
       else v.s = a->dict.strs[id].c_str();
     } else v.i = vals[k].i;
+  }
+}
+
+// the same from the compact device form: raw 64-bit words and a byte of null flags (bit k: value k)
+void to_sm_values_compact(const sm_app* a, const int64_t* w, uint8_t nulls, int nvals, const CompiledQuery& cq,
+                          sm_value* out) {
+  for (int k = 0; k < nvals; ++k) {
+    sm_value& v = out[k];
+    const int t = cq.sel_types[k];
+    v.type = t;
+    v.is_null = (nulls >> k) & 1;
+    v.i = 0;
+    v.d = 0;
+    v.s = nullptr;
+    if (v.is_null) continue;
+    if (t == T_FLOAT || t == T_DOUBLE) memcpy(&v.d, &w[k], 8);
+    else if (t == T_STRING) {
+      const int64_t id = w[k];
+      if (id < 0 || id >= (int64_t)a->dict.strs.size()) v.is_null = 1;
+      else v.s = a->dict.strs[id].c_str();
+    } else v.i = w[k];
   }
 }
 
@@ -1356,26 +1379,44 @@ void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<DevOut>& outs
   const size_t np = (size_t)m * (rows ? 1 : 2);
   uint32_t* hp = (uint32_t*)a->out_arena.take(np * 4);
   SM_HIP(hipMemcpyAsync(hp, q.dev_pairs.p, np * 4, hipMemcpyDeviceToHost, hs));
-  // DVal values, then timestamps: pinned, reused across calls (sm_app::out_arena), not zero-filled
-  DVal* hv = (DVal*)a->out_arena.take((size_t)m * (ns * sizeof(DVal) + 8));
-  int64_t* hts = (int64_t*)(hv + (size_t)m * ns);
+  // values, then timestamps: pinned, reused across calls (sm_app::out_arena), not zero-filled. Up to 8 select
+  // values cross PCIe in the compact form (8 bytes per value + one byte of null flags per output instead of a
+  // 16-byte DVal per value)
+  const bool compact = ns > 0 && ns <= 8;
+  const size_t vbytes = compact ? (size_t)ns * 8 + 1 : (size_t)ns * sizeof(DVal);
+  char* hb = (char*)a->out_arena.take((size_t)m * (vbytes + 8) + 16);
+  int64_t* hts = (int64_t*)hb;
+  char* hvals = hb + (size_t)m * 8;  // DVal array, or words then null bytes
   q.proj_desc_dev.ensure(sizeof(NfaStream));
   SM_HIP(hipMemcpyAsync(q.proj_desc_dev.p, &q.proj_desc, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
   const int64_t chunk = std::min<int64_t>(m, (int64_t)1 << 22);
-  q.proj_out.ensure((size_t)chunk * (ns * sizeof(DVal) + 8) + 16);
-  DVal* dv = (DVal*)q.proj_out.p;
-  int64_t* dts = (int64_t*)((char*)q.proj_out.p + (size_t)chunk * ns * sizeof(DVal));
+  q.proj_out.ensure((size_t)chunk * (vbytes + 8) + 16);
+  int64_t* dts = (int64_t*)q.proj_out.p;
+  char* dvals = (char*)q.proj_out.p + (size_t)chunk * 8;
   for (int64_t k0 = 0; k0 < m; k0 += chunk) {
     const int64_t c = std::min(chunk, m - k0);
     a->sc.used = 0;
+    int64_t* dw = compact ? (int64_t*)dvals : nullptr;
+    uint8_t* dn = compact ? (uint8_t*)(dvals + (size_t)chunk * ns * 8) : nullptr;
     pair_project((const uint32_t*)q.dev_pairs.p + (rows ? k0 : 2 * k0), c, (const NfaStream*)q.proj_desc_dev.p,
                  q.proj_ord, q.proj_n, q.proj_base, q.proj_ts, (const int64_t*)q.prev_carry.p, q.prev_carry_n,
-                 q.prev_carry_w, (const char*)q.blob.p, dv, dts, a->sc, hs, rows);
-    if (ns) SM_HIP(hipMemcpyAsync(hv + (size_t)k0 * ns, dv, (size_t)c * ns * sizeof(DVal), hipMemcpyDeviceToHost, hs));
+                 q.prev_carry_w, (const char*)q.blob.p, compact ? nullptr : (DVal*)dvals, dts, a->sc, hs, rows, dw, dn);
+    if (compact) {
+      SM_HIP(hipMemcpyAsync(hvals + (size_t)k0 * ns * 8, dw, (size_t)c * ns * 8, hipMemcpyDeviceToHost, hs));
+      SM_HIP(hipMemcpyAsync(hvals + (size_t)m * ns * 8 + k0, dn, (size_t)c, hipMemcpyDeviceToHost, hs));
+    } else if (ns) {
+      SM_HIP(hipMemcpyAsync(hvals + (size_t)k0 * ns * sizeof(DVal), dvals, (size_t)c * ns * sizeof(DVal),
+                            hipMemcpyDeviceToHost, hs));
+    }
     SM_HIP(hipMemcpyAsync(hts + k0, dts, (size_t)c * 8, hipMemcpyDeviceToHost, hs));
   }
   SM_HIP(hipStreamSynchronize(hs));
-  outs.push_back(DevOut{qi, m, hp, hv, hts, rows, q.proj_base});
+  DevOut d{qi, m, hp, compact ? nullptr : (const DVal*)hvals, hts, rows, q.proj_base};
+  if (compact) {
+    d.hw = (const int64_t*)hvals;
+    d.hn = (const uint8_t*)(hvals + (size_t)m * ns * 8);
+  }
+  outs.push_back(d);
   q.n_out += m;
   a->host_ms[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -1387,6 +1428,20 @@ void materialize(sm_app* a, const DevOut& d, std::vector<HostOut>& outs) {
   const int ns = cq.hdr.nsel, nr = cq.hdr.nrefs_vis;
   const int32_t* rslots = (const int32_t*)(cq.blob.data() + cq.hdr.off_refs);
   int64_t* hrf = (int64_t*)a->out_arena.take((size_t)std::max<int64_t>(d.m * nr, 1) * 8);
+  const DVal* hv = d.hv;
+  if (d.hw) {  // compact form: HostOut points at DVals
+    DVal* v = (DVal*)a->out_arena.take((size_t)std::max<int64_t>(d.m * ns, 1) * sizeof(DVal));
+    parallel_for((size_t)d.m, (size_t)1 << 16, [&](size_t lo, size_t hi) {
+      for (size_t k = lo; k < hi; ++k)
+        for (int j = 0; j < ns; ++j) {
+          DVal& x = v[k * ns + j];
+          x.i = d.hw[k * ns + j];
+          x.null = (d.hn[k] >> j) & 1;
+          x.pad = 0;
+        }
+    });
+    hv = v;
+  }
   const size_t base = outs.size();
   outs.resize(base + (size_t)d.m);
   parallel_for((size_t)d.m, (size_t)1 << 16, [&](size_t lo, size_t hi) {
@@ -1403,7 +1458,7 @@ void materialize(sm_app* a, const DevOut& d, std::vector<HostOut>& outs) {
       h.r.phase = 1;
       h.r.query = cq.hdr.query_order;
       h.r.seq = (int32_t)k;
-      h.vals = d.hv + k * ns;
+      h.vals = hv + k * ns;
       h.nvals = ns;
       h.refs = rf;
       h.nrefs = nr;
@@ -1446,7 +1501,8 @@ void deliver_direct(sm_app* a, const DevOut& d) {
       size_t c = c0 + cnt[t];
       const size_t kb = m * t / T, ke = m * (t + 1) / T;
       for (size_t k = kb; k < ke; ++k) {
-        to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
+        if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
+        else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
         pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
         if (k == 0 || trig(k) != trig(k - 1)) {
           PreparedChunk& ch = pd.chunks[c++];

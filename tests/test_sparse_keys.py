@@ -128,3 +128,18 @@ def test_compared_key_attribute_is_not_remapped():
     exp = oracle_subsample(text, key.cpu().numpy(), price.cpu().numpy(), ts.cpu().numpy(), np.arange(N))
     g = got.cpu().numpy()
     np.testing.assert_array_equal(np.stack([g & 0xFFFFFFFF, g >> 32], 1), exp)
+
+
+@pytest.mark.timeout(600)
+def test_int_keys_wider_than_the_bucket_window_get_ids():
+    """INT keys spread over a 2^25-wide span (2^20 keys, every 31st value): within the closed form's 2^30 key window
+    but wider than the bucket-stack's 2^20, so the first batch's prep pass reports the span and the keys become dense
+    ids (bucket stack, path 3) instead of the sort / walk pipeline; equal to the brute force."""
+    import torch
+    N, K = 8_000_000, 1 << 20
+    sym, _, price, ts = sparse_stream(N, K, 100)
+    key = (sym.to(torch.int64) * 31).to(torch.int32)
+    got, paths = run(bench.APP, key, price, ts)
+    assert paths == [3], paths
+    ref = closed_form_torch(key.to(torch.int64), price, ts, 1000)
+    assert torch.equal(ref, got)
