@@ -140,7 +140,7 @@ size_t sm_app_dump_outputs(sm_app* app, char* buf, size_t len);
  * "batch_events" (auto-flush threshold), "fast_general" (1 = device batches always take the general
  * closed-form kernels), "fast_timing" (1 = record HIP events around the device-batch phases), "reset" (drop all
  * matching state, keep the device allocations), "lane_balance" (N > 0: order the NFA lanes of a partitioned batch
- * with >= N keys by descending event count; 0 = off, the default; outputs are unchanged either way),
+ * with >= N keys by descending event count, default 2^16; 0 = off; outputs are unchanged either way),
  * "fast_stack" (closed-form pipeline: 0 automatic, 1 bucket stack whenever it applies, 2 sort / walk),
  * "key_remap" (closed-form partition keys as dense device ids: 1 always, 0 never, -1 automatic = when the first
  * batch's key span exceeds 2^20 or a later batch's keys leave the span the closed form can hold),

@@ -361,10 +361,11 @@ struct sm_app {
   int32_t heap_half = 1024;
   int64_t pool_init = (int64_t)1 << 25;  // option "pool_words": first size of a query's overflow pool (words)
   // NFA lanes in descending event-count order for batches with at least this many keys (0 = off;
-  // SM_NFA_BALANCE=<min keys> / option "lane_balance"). A wave runs as long as its busiest lane: config 5 NFA kernel
-  // 19.4 -> 18.5 ms, but a wave's lanes then stage and write back 64 scattered keys' state words and timer queues,
-  // 41.9 -> 57.8 GB of HBM traffic per launch; off by default.
-  int64_t lane_balance = 0;
+  // SM_NFA_BALANCE=<min keys> / option "lane_balance"). A wave runs as long as its busiest lane; a wave's lanes then
+  // stage and write back 64 scattered keys' state words and timer queues (more HBM traffic per launch), which the
+  // shorter waves outweigh: round 4, config 5 literal 17.85 -> 17.7 ms (step unchanged with the sort), emitting
+  // variant 147.1 -> 140.6 ms.
+  int64_t lane_balance = (int64_t)1 << 16;
   int64_t out_records = 0;  // option "output_records" (0 = automatic)
   bool keep_outputs = false;  // option "keep_outputs": device-events batches keep their ordered output records
   int nfa_jit = -1;         // option "nfa_jit": 1 = query-specialised NFA kernels (nfa_jit.cpp), 0 = the
