@@ -7,10 +7,14 @@
 
 on synthetic StockStream events (K = 1e6 symbols, N = 1e9 events, event time
 ts_i = floor(i / 10000) ms), device-resident before the timed region. One step = one pass of the hot path
-over the whole batch: (multi-GPU) hash-by-key all-to-all of (symbol, price, ts, ordinal) over RCCL/xGMI,
-then the closed-form pattern kernels producing the ordered (e1, e2) match tuples on every rank.
+over the whole batch: the closed-form pattern kernels producing the ordered (e1, e2) match tuples.
 
-Scaling is strong (N is the whole job at every GPU count). Launch: python bench.py [--gpus N --steps K
+Multi-GPU (--gpus N > 1): a partitioned query's keys are independent (PartitionRuntime instances share no state,
+core/partition/PartitionRuntime.java:256-309), so by default each rank runs the configuration's whole workload on its
+own key partition (keys r*K .. r*K+K-1, its own N-event stream) with no data-path collective: weak scaling, value =
+N x ranks / the slowest rank's time. `--shard exchange` instead ingests ONE N-event stream in contiguous slices,
+routes the keys by an RCCL all-to-all of (symbol, price, ts, ordinal) over xGMI and returns every match to the rank
+that ingested its e2, in the single stream's order (strong scaling). Launch: python bench.py [--gpus N --steps K
 --warmup W]; for N > 1 under torch.distributed.run (one rank per GPU; WORLD_SIZE must equal N), or without a
 launcher, in which case bench.py starts torch.distributed.run with N ranks itself (launch_command).
 
@@ -393,6 +397,11 @@ def main():
     ap.add_argument("--no-ih", action="store_true", help="config 4: skip the input-handler variant")
     ap.add_argument("--ih-chunk", type=float, default=None, help="input-handler variant: option bulk_chunk")
     ap.add_argument("--no-sparse", action="store_true", help="config 4: skip the sparse 64-bit key variant")
+    ap.add_argument("--shard", default=None, choices=("partition", "exchange"),
+                    help="config 4 on N > 1 GPUs: 'partition' (default) = each rank runs the configuration's whole "
+                         "workload on its own key partition, no data-path collective (weak scaling); 'exchange' = "
+                         "one stream ingested in contiguous slices, keys routed by an RCCL all-to-all and the outputs "
+                         "merged into the single stream's order (strong scaling)")
     ap.add_argument("--heap-words", type=int, default=None,
                     help="NFA per-key partial-match arena (words per semispace; option heap_words)")
     args = ap.parse_args()
@@ -426,19 +435,33 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # config 4 on several GPUs: key partitions (default) or one exchanged stream (--shard exchange)
+    kpart = args.config == 4 and world > 1 and (args.shard or "partition") == "partition"
+    # (modulo the visible devices: a box with fewer GPUs than ranks shares them, a functional check only)
+    local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # key partitions exchange nothing on the data path: the control plane (barriers, the max of the step times,
+        # the sum of the match counts) runs over gloo; the exchange path uses RCCL over xGMI
+        if kpart:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     N = int(args.events if args.events is not None else cfg["events"])
     K = args.keys
     ts_div = args.ts_div if args.ts_div is not None else cfg["ts_div"]
     seed = seed_for(args.config)
-    if cfg["shards"]:
+    shards = cfg["shards"] and not kpart
+    if shards:
         lo, hi = N * rank // world, N * (rank + 1) // world
-    else:  # replicas: every rank runs the whole workload
+    else:  # replicas / key partitions: every rank runs the whole workload
         lo, hi = 0, N
-    symbol, price, volume, tsattr, ts = gen_stock(lo, hi, K, ts_div, dev, seed)
+    symbol, price, volume, tsattr, ts = gen_stock(lo, hi, K, ts_div, dev, seed + 7919 * rank if kpart else seed)
+    if kpart:
+        # rank r's partition: keys r*K .. r*K + K-1 (PartitionRuntime instances of disjoint key sets, which share no
+        # state: core/partition/PartitionRuntime.java:256-309), its own stream of N events
+        symbol += rank * K
     if args.config != 2:
         del volume  # not referenced by the pattern: the exchange ships only what the plan reads
         volume = price
@@ -446,8 +469,8 @@ def main():
     sidx = gen_stream_idx(lo, hi, dev, seed) if args.config == 5 else None
     # multi-GPU constants of the exchange, made once: every slice's first ordinal, the in-slice offsets shipped in
     # the packed records, and the device buffer the per-rank match tuples are copied into for the return exchange
-    starts = slice_starts(lo, world, dev) if world > 1 and cfg["shards"] else None
-    offsets = torch.arange(hi - lo, dtype=torch.int32, device=dev) if world > 1 and cfg["shards"] else None
+    starts = slice_starts(lo, world, dev) if world > 1 and shards else None
+    offsets = torch.arange(hi - lo, dtype=torch.int32, device=dev) if world > 1 and shards else None
     mbuf = [None]
     out_local = [0]
     torch.cuda.synchronize()
@@ -498,7 +521,7 @@ def main():
                 app.process_device_batch("StockStream", s_ts, [s_sym, s_price, s_price, s_price], ordinals=ords,
                                          hip_stream=hip_stream)
                 m = nm[0] = app.device_matches("q")[1]
-                if world == 1:
+                if world == 1 or kpart:
                     return None  # the output stays in the library's device buffer, in reference order
                 if mbuf[0] is None or mbuf[0].numel() < m:
                     mbuf[0] = torch.empty(max(m, 1) + (m >> 3), dtype=torch.int64, device=dev)
@@ -507,7 +530,9 @@ def main():
 
             # the reference's single output order across ranks (shard.partitioned_step): key exchange, matching,
             # every tuple returned to the rank that ingested its e2 and ordered there
-            mine = partitioned_step(symbol, [symbol, price, ts], world, lo, N, match, starts=starts, offsets=offsets)
+            # (key partitions: each rank's stream is its own, nothing crosses ranks)
+            mine = partitioned_step(symbol, [symbol, price, ts], 1 if kpart else world, lo, N, match, starts=starts,
+                                    offsets=offsets)
             if mine is not None:
                 out_local[0] = mine.numel()
             return nm[0]
@@ -518,7 +543,7 @@ def main():
         app.process_device_batch("StockStream", s_ts, cols, ordinals=s_ord, ordinal_base=lo if args.config == 2 else 0,
                                  hip_stream=hip_stream)
         m = app.device_matches("q")[1]
-        if world > 1 and cfg["shards"]:
+        if world > 1 and shards:
             # config 2's index-range outputs are concatenated in rank order (shard.concat_ordered)
             if mbuf[0] is None or mbuf[0].numel() < m:
                 mbuf[0] = torch.empty(max(m, 1) + (m >> 3), dtype=torch.int32, device=dev)
@@ -553,16 +578,16 @@ def main():
     dt = time.perf_counter() - t0
     path = app.get_stat("fast_path:q")
     nfa_kernel = int(app.get_stat("nfa_kernel:q")) if args.config == 5 else 0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    m = torch.tensor([nm], dtype=torch.int64, device=dev)
+    t = torch.tensor([dt], dtype=torch.float64, device="cpu" if kpart else dev)
+    m = torch.tensor([nm], dtype=torch.int64, device="cpu" if kpart else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        if cfg["shards"]:
+        if shards or kpart:
             dist.all_reduce(m)
     dt = t.item()
     total_matches = m.item()
     ms_per_step = dt / args.steps * 1e3
-    units = N if cfg["shards"] else N * world  # replicas: every rank processed the whole stream
+    units = N if shards else N * world  # replicas / key partitions: every rank processed a whole stream
     value = units / (dt / args.steps)
 
     roof = roofline(ktot, n_local[0], nm, args.steps, args.config)
@@ -655,10 +680,13 @@ def main():
                              f"{' + global clock heartbeats' if args.config == 5 else ''}: {sect:.2f} s, {mt} matches",
                    "single_thread": {"value": v, "cores": 1, "seconds": sec}, **host_cpu()}
     if rank == 0:
-        alg = cfg["job_bytes"](N, total_matches) * (1 if cfg["shards"] else world)
+        alg = cfg["job_bytes"](N, total_matches) * (1 if shards else world) if not kpart else \
+            cfg["job_bytes"](N * world, total_matches)
         conf = {"workload": cfg["workload"], "config": args.config, "events": N,
                 "event_time": f"floor(i/{ts_div}) ms", "matches": total_matches,
-                "parallelism": (f"key-sharded x{world}" if args.config in (4, 5) else
+                "parallelism": (f"key-partitioned x{world} (rank r: keys r*K .. r*K+K-1, its own stream of "
+                                f"{N} events; no data-path collective)" if kpart else
+                                f"key-sharded x{world}" if args.config in (4, 5) else
                                 f"index-range-sharded x{world}" if cfg["shards"] else f"replicas x{world}"),
                 "device_path": (("general NFA (interleaved device events), " +
                                  {1: "query-specialised kernel", 2: "interpreter"}.get(nfa_kernel, "?"))
@@ -672,7 +700,8 @@ def main():
         line = {
             "metric": METRIC if args.config == 4 else f"input events/sec + % HBM peak, {cfg['workload']}",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": cfg["scaling"], "vs_baseline": None,
+            "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak" if kpart else cfg["scaling"], "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (counter-based splitmix64 StockStream, device-resident)",
             "config": conf, "roofline": roof, "cpu_baseline": cpu,
         }
