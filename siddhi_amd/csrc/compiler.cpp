@@ -342,6 +342,9 @@ struct Lowering {
         pres[pre].stateId = stateIndex;
         pres[pre].progOff = off;
         pres[pre].progLen = len;
+        pres[pre].trialCur = 1;
+        for (int i = off; i < off + len; ++i)
+          if (code[i].op == OP_VAR && code[i].a == stateIndex && code[i].b != kCurrent) pres[pre].trialCur = 0;
         if (post < 0) post = new_post(el->kind == StateKind::ABSENT ? PK_ABSENT_STREAM : PK_STREAM);
         posts[post].stateId = stateIndex;
         posts[post].thisPre = pre;

@@ -95,6 +95,15 @@ struct StateLoader {  // OP_VAR loads for a run record
   int rec;
   __device__ StackVal var(const Instr& in) const;
 };
+// A state's filter tried before the incoming event joins the partial (DPre.trialCur): loads of the state's own slot
+// (always at CURRENT, which the incoming event would become) read the event's LaneEv record; other slots as above.
+struct TrialLoader {
+  const Lane* L;
+  int rec;
+  int sid;
+  const int64_t* evr;
+  __device__ StackVal var(const Instr& in) const;
+};
 
 // The words of one lane inside a lane-interleaved allocation (structure of arrays across lanes): word w of lane k
 // lives at base[w * lanes + k]. The 64 lanes of a wave that touch the same per-key state word (list heads,
@@ -394,6 +403,25 @@ struct Lane {
     return truthy(eval_prog(PCODE + P.progOff, P.progLen, PCONSTS, ld));
 #endif
   }
+  // filter_pass for a trialCur state with the incoming event in place of its own slot's CURRENT: nothing is added to
+  // the partial, so a partial that fails costs only the loads of the other slots' values
+  SM_JIT_INL __device__ bool trial_pass(int p, int32_t rec, const int64_t* evr) const {
+#ifdef SM_NFA_JIT_INLINE_ALL
+    bool pass = true;
+#pragma unroll
+    for (int q = 0; q < PQ->npre; ++q)
+      if (q == p && PPRE[q].progLen != 0) {
+        TrialLoader ld{this, rec, PPRE[q].stateId, evr};
+        pass = truthy(eval_prog(PCODE + PPRE[q].progOff, PPRE[q].progLen, PCONSTS, ld));
+      }
+    return pass;
+#else
+    const DPre& P = PPRE[p];
+    if (P.progLen == 0) return true;
+    TrialLoader ld{this, rec, P.stateId, evr};
+    return truthy(eval_prog(PCODE + P.progOff, P.progLen, PCONSTS, ld));
+#endif
+  }
   __device__ bool is_absent(int p) const { return PPRE[p].kind == PK_ABSENT_STREAM || PPRE[p].kind == PK_ABSENT_LOGICAL; }
 
   // StreamPreStateProcessor.isExpired :102-121
@@ -682,11 +710,17 @@ struct Lane {
             continue;
           }
           if (trial) {
-            if (shared < 0) shared = copy_event(evr);
-            set_slot(s, sid, shared);
+            bool pass;
+            if (P.trialCur) {
+              pass = trial_pass(p, s, evr);
+            } else {
+              if (shared < 0) shared = copy_event(evr);
+              set_slot(s, sid, shared);
+              pass = filter_pass(p, s);
+              if (!pass) set_slot(s, sid, -1);
+            }
             setfl(p, F_STATE_CHANGED, false);
-            if (!filter_pass(p, s)) {  // what the loop below does for a partial the filter rejects
-              set_slot(s, sid, -1);
+            if (!pass) {  // what the loop below does for a partial the filter rejects
               if (!P.sequence) {
                 prev = ln;
                 ln = ln_next(ln);
@@ -697,6 +731,8 @@ struct Lane {
               }
               continue;
             }
+            if (shared < 0) shared = copy_event(evr);
+            set_slot(s, sid, shared);
             shared = -1;
             post_process(P.post, s);  // pre_process after its filter
           } else {
@@ -736,12 +772,18 @@ struct Lane {
             continue;
           }
           if (trial) {
-            if (shared < 0) shared = copy_event(evr);
-            add_event(s, sid, shared);
+            bool pass;
+            if (P.trialCur) {
+              pass = trial_pass(p, s, evr);
+            } else {
+              if (shared < 0) shared = copy_event(evr);
+              add_event(s, sid, shared);
+              pass = filter_pass(p, s);
+              if (!pass) remove_last_event(s, sid);
+            }
             setfl(p, F_SUCCESS, false);
             setfl(p, F_STATE_CHANGED, false);
-            if (!filter_pass(p, s)) {  // what the loop below does for a partial the filter rejects
-              remove_last_event(s, sid);
+            if (!pass) {  // what the loop below does for a partial the filter rejects
               if (!P.sequence) {
                 prev = ln;
                 ln = ln_next(ln);
@@ -749,6 +791,10 @@ struct Lane {
                 ln = lerase(p, 0, prev, ln);
               }
               continue;
+            }
+            if (P.trialCur) {
+              if (shared < 0) shared = copy_event(evr);
+              add_event(s, sid, shared);
             }
             shared = -1;  // the partial keeps the copy
             post_process(P.post, s);  // pre_process after its filter
@@ -1268,6 +1314,20 @@ __device__ StackVal StateLoader::var(const Instr& in) const {
   if (n < 0) return v;
   if ((L->heap[n + 3] >> in.c) & 1) return v;
   int64_t w = L->heap[n + 4 + in.c];
+  v.null = 0;
+  if (in.t0 == T_FLOAT || in.t0 == T_DOUBLE) v.d = __longlong_as_double(w);
+  else v.i = w;
+  return v;
+}
+
+__device__ StackVal TrialLoader::var(const Instr& in) const {
+  if (in.a != sid) return StateLoader{L, rec}.var(in);
+  StackVal v;
+  v.i = 0;
+  v.d = 0;
+  v.null = 1;
+  if ((le_node(*L->b, evr, 3) >> in.c) & 1) return v;
+  const int64_t w = le_node(*L->b, evr, 4 + in.c);
   v.null = 0;
   if (in.t0 == T_FLOAT || in.t0 == T_DOUBLE) v.d = __longlong_as_double(w);
   else v.i = w;

@@ -76,6 +76,9 @@ struct DPre {
   int32_t minCount, maxCount, ltype;
   int32_t sched;             // scheduler index or -1
   int32_t ksOff;             // first of its per-key state words (kPreWords, or kPreWordsAbsent for an absent pre)
+  int32_t trialCur;          // 1: the filter reads its own state's chain only at CURRENT (the incoming event), so a
+                             // partial can be tried against the incoming event without adding it to the chain
+  int32_t pad0;
   int64_t waitingTime;       // absent: 'for' time, -1 when absent (logical 'and not X' without for)
 };
 
