@@ -713,6 +713,9 @@ struct Lane {
             bool pass;
             if (P.trialCur) {
               pass = trial_pass(p, s, evr);
+              // the reference sets the slot to the event and back to null on a rejection: an every-copy that
+              // arrived with the slot filled leaves it null
+              if (!pass) set_slot(s, sid, -1);
             } else {
               if (shared < 0) shared = copy_event(evr);
               set_slot(s, sid, shared);
