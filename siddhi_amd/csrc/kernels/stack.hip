@@ -52,6 +52,8 @@ constexpr int kLog = 4096;     // match log of a slice: kLog / H entries per key
 constexpr int kOvf = 1024;     // ... and a shared overflow (more: the batch takes the sort / walk kernels)
 // matches of a tile staged in LDS before one coalesced write (what the tile counts leave of the LDS; none for tiles of
 // 2^15 ordinals, whose direct writes land in a ~190 KB window that the L2 combines)
+// (tiles of 2^14 ordinals counted in packed u16 pairs, to keep the image in LDS, were exact and ran 22.9 ms against
+// 6.5: adjacent ordinals' atomics then hit one LDS word)
 constexpr int kOCap = kOT * 4 + 12288 * 8 <= 160 * 1024 ? 12288 : 0;
 #ifndef SM_ORDER_GT
 #define SM_ORDER_GT (SM_ORDER_TB >= 15 ? 4 : 16)  // A/B build flag
@@ -531,6 +533,7 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
     for (int e = tid; e < kOT; e += kOB) cnt[e] = 0;
     ms = me;
     lds_barrier();
+    auto count = [&](uint32_t j) { atomicAdd(&cnt[j - j0], 1u); };
     // pass A: matches per ordinal. The first 16 matches of each of the wave's 64 buckets are loaded at once (one
     // load per round, all in flight) and kept for pass B; longer segments (rare) are walked chunk by chunk.
     uint64_t v0[16];
@@ -547,25 +550,24 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
     for (int r = 0; r < 16; ++r) v0[r] = (uint32_t)l16 < lenr[r] ? a.stage[s0r[r] + l16] : 0ull;
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      if ((uint32_t)l16 < lenr[r]) atomicAdd(&cnt[(uint32_t)(v0[r] >> 32) - j0], 1u);
+      if ((uint32_t)l16 < lenr[r]) count((uint32_t)(v0[r] >> 32));
     if (__any(more))
       for (int r = 0; r < 16; ++r)
         for (uint32_t c = 16; __any(c < lenr[r]); c += 16)
-          if (c + l16 < lenr[r]) atomicAdd(&cnt[(uint32_t)(a.stage[s0r[r] + c + l16] >> 32) - j0], 1u);
+          if (c + l16 < lenr[r]) count((uint32_t)(a.stage[s0r[r] + c + l16] >> 32));
     lds_barrier();
-    {
+    {  // exclusive scan of the counts, kPer ordinals per thread (read again from LDS rather than held in registers:
+       // holding them spilled 4 VGPRs; 6.75 -> 6.5 ms)
       constexpr int kPer = kOT / kOB;
-      uint32_t v[kPer], sum = 0;
+      uint32_t sum = 0;
 #pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        v[k] = cnt[tid * kPer + k];
-        sum += v[k];
-      }
+      for (int k = 0; k < kPer; ++k) sum += cnt[tid * kPer + k];
       uint32_t r = block_excl(sum, lw, &tot);
 #pragma unroll
       for (int k = 0; k < kPer; ++k) {
+        const uint32_t c = cnt[tid * kPer + k];
         cnt[tid * kPer + k] = r;
-        r += v[k];
+        r += c;
       }
     }
     lds_barrier();
