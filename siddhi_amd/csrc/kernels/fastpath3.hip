@@ -36,6 +36,10 @@
 #include "fastpath_dev.h"
 #include "pass0_dev.h"
 
+#ifndef SM_ORIG_NT_LOAD
+#define SM_ORIG_NT_LOAD 1  // A/B build flag: nontemporal column loads in key pass 0 (OrigSrc; 13.56 -> 13.32 ms)
+#endif
+
 namespace sm {
 
 namespace {
@@ -405,10 +409,18 @@ struct OrigSrc {
   };
   __device__ Raw load(int64_t p) const {
     Raw r;
+#if SM_ORIG_NT_LOAD
+    // read-once columns: nontemporal loads keep the L2 for the pass's scattered record stores (as RecSrc)
+    r.k = __builtin_nontemporal_load(kcol + p);
+    r.v = __builtin_nontemporal_load(vcol + p);
+    r.t = __builtin_nontemporal_load(ts + p);
+    r.o = ord ? __builtin_nontemporal_load(ord + p) - obase : p;
+#else
     r.k = kcol[p];
     r.v = vcol[p];
     r.t = ts[p];
     r.o = ord ? ord[p] - obase : p;
+#endif
     r.m = c1_inline ? 0ull : c1mask[p >> 6];
     return r;
   }
