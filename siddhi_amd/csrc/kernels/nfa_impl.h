@@ -1360,19 +1360,28 @@ __device__ int64_t gallop(const int64_t* __restrict__ v, int64_t from, int64_t n
   return hi;
 }
 
+#ifndef SM_LE_NT
+#define SM_LE_NT 1  // A/B build flag: nontemporal column loads in the lane-events pass (config 5 step 33.5 -> 33.0 ms)
+#endif
 // Record k of the query's batch, in key order, as its LaneEv record (nfa.h): a lane then reads one contiguous
 // record per event instead of chasing key_pos -> stream / row / ts / clock / ordinal / columns.
 __device__ __forceinline__ int64_t lane_attr(const NfaStream& st, int a, int64_t row, int64_t& nulls) {
   int64_t v = 0;
   bool isnull = st.nulls[a] && st.nulls[a][row];
+#if SM_LE_NT && defined(__HIP_DEVICE_COMPILE__)
+#define SM_LE_LD(T, p) __builtin_nontemporal_load((const T*)(p))
+#else
+#define SM_LE_LD(T, p) (*(const T*)(p))
+#endif
   switch (st.types[a]) {
-    case T_INT: v = ((const int32_t*)st.cols[a])[row]; break;
-    case T_LONG: v = ((const int64_t*)st.cols[a])[row]; break;
-    case T_FLOAT: { double d = (double)((const float*)st.cols[a])[row]; v = __double_as_longlong(d); break; }
-    case T_DOUBLE: v = __double_as_longlong(((const double*)st.cols[a])[row]); break;
-    case T_STRING: v = ((const int32_t*)st.cols[a])[row]; isnull = isnull || v < 0; break;
+    case T_INT: v = SM_LE_LD(int32_t, (const int32_t*)st.cols[a] + row); break;
+    case T_LONG: v = SM_LE_LD(int64_t, (const int64_t*)st.cols[a] + row); break;
+    case T_FLOAT: { double d = (double)SM_LE_LD(float, (const float*)st.cols[a] + row); v = __double_as_longlong(d); break; }
+    case T_DOUBLE: v = __double_as_longlong(SM_LE_LD(double, (const double*)st.cols[a] + row)); break;
+    case T_STRING: v = SM_LE_LD(int32_t, (const int32_t*)st.cols[a] + row); isnull = isnull || v < 0; break;
     default: v = ((const uint8_t*)st.cols[a])[row]; break;
   }
+#undef SM_LE_LD
   if (isnull) nulls |= (1ll << a);
   return v;
 }
