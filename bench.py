@@ -9,12 +9,15 @@ on synthetic StockStream events (K = 1e6 symbols, N =
 ts_i = floor(i / 10000) ms), device-resident before the timed region. One step = one pass of the hot path
 over the whole batch: the closed-form pattern kernels producing the ordered (e1, e2) match tuples.
 
-Multi-GPU (--gpus N > 1): a partitioned query's keys are independent (PartitionRuntime instances share no state,
-core/partition/PartitionRuntime.java:256-309), so by default each rank runs the configuration's whole workload on its
-own key partition (keys r*K .. r*K+K-1, its own N-event stream) with no data-path collective: weak scaling, value =
-N x ranks / the slowest rank's time. `--shard exchange` instead ingests ONE N-event stream in contiguous slices,
-routes the keys by an RCCL all-to-all of (symbol, price, ts, ordinal) over xGMI and returns every match to the rank
-that ingested its e2, in the single stream's order (strong scaling). Launch: python bench.py [--gpus N --steps K
+Multi-GPU (--gpus N > 1): the reference ingests ONE stream and routes every event to its key's partition instance
+(PartitionStreamReceiver.receive core/partition/PartitionStreamReceiver.java:156-168, PartitionRuntime.cloneIfNotExist
+core/partition/PartitionRuntime.java:256-309), with one global output order. bench.py measures exactly that
+configuration: every rank ingests a contiguous slice of the one N-event stream, the keys are routed to their owner
+rank by a hash-by-key RCCL all-to-all of packed (symbol, price, ts, offset) records over xGMI, each rank matches its
+keys, and every match tuple returns to the rank that ingested its e2, ordered there (shard.partitioned_step): strong
+scaling, value = N / the slowest rank's step time, config.rccl_world = the size of the RCCL (nccl) group.
+`--key-partitions` adds an opt-in side line (`key_partitions`, never `value`): each rank runs its own N-event stream on
+its own key range with no data-path collective (weak scaling). Launch: python bench.py [--gpus N --steps K
 --warmup W]; for N > 1 under torch.distributed.run (one rank per GPU; WORLD_SIZE must equal N), or without a
 launcher, in which case bench.py starts torch.distributed.run with N ranks itself (launch_command).
 
@@ -374,7 +377,53 @@ def launch_command(gpus, argv, env, port=None):
             "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
-def main():
+def run_plan(config, world, env=None):
+    """How a run of `config` on `world` ranks is laid out (no GPU needed; tests/test_bench_launch.py). A configuration
+    that shards (2: index ranges; 4, 5: keys) splits ONE stream of N events over the ranks, and value counts N; config
+    3 (non-partitioned) runs `world` replicas and counts N x world. Several ranks always form an RCCL (nccl) group:
+    configs 4 and 5 exchange keys over it (hash-by-key all-to-all), config 2 gathers its rows over it.
+    SM_BENCH_BACKEND=gloo is a functional rehearsal only (several ranks sharing one GPU, which RCCL refuses; the
+    collectives then stage through host memory) and reports rccl_world null."""
+    cfg = CONFIGS[config]
+    env = os.environ if env is None else env
+    return {"shards": bool(cfg["shards"]), "units_factor": 1 if cfg["shards"] else world,
+            "backend": env.get("SM_BENCH_BACKEND", "nccl") if world > 1 else None,
+            "exchange": config in (4, 5) and world > 1,
+            "scaling": cfg["scaling"]}
+
+
+def key_partitions_line(app, N, K, ts_div, seed, rank, world, dev, hip_stream, steps, warmup):
+    """Opt-in side line (`--key-partitions`, never `value`): rank r runs its own N-event stream on keys r*K .. r*K+K-1
+    (disjoint PartitionRuntime instances share no state, core/partition/PartitionRuntime.java:256-309) with no
+    data-path collective: weak scaling, N x world / the slowest rank's step time."""
+    import torch
+    import torch.distributed as dist
+    symbol, price, _, _, ts = gen_stock(0, N, K, ts_div, dev, seed + 7919 * rank)
+    symbol += rank * K
+
+    def step():
+        app.set_option("reset", 0)
+        app.process_device_batch("StockStream", ts, [symbol, price, price, price], hip_stream=hip_stream)
+        return app.device_matches("q")[1]
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item() / steps
+    return {"value": N * world / dt, "unit": "events/s", "ms_per_step": dt * 1e3, "scaling": "weak",
+            "events_per_rank": N, "keys_per_rank": K,
+            "note": "side line: each rank its own stream on its own key range, no data-path collective"}
+
+
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -397,13 +446,17 @@ def main():
     ap.add_argument("--no-ih", action="store_true", help="config 4: skip the input-handler variant")
     ap.add_argument("--ih-chunk", type=float, default=None, help="input-handler variant: option bulk_chunk")
     ap.add_argument("--no-sparse", action="store_true", help="config 4: skip the sparse 64-bit key variant")
-    ap.add_argument("--shard", default=None, choices=("partition", "exchange"),
-                    help="config 4 on N > 1 GPUs: 'partition' (default) = each rank runs the configuration's whole "
-                         "workload on its own key partition, no data-path collective (weak scaling); 'exchange' = "
-                         "one stream ingested in contiguous slices, keys routed by an RCCL all-to-all and the outputs "
-                         "merged into the single stream's order (strong scaling)")
+    ap.add_argument("--key-partitions", action="store_true",
+                    help="config 4 on N > 1 GPUs: also time the opt-in side line `key_partitions` (each rank its own "
+                         "N-event stream on its own key range, no data-path collective, weak scaling); the headline "
+                         "value is always the one exchanged stream")
     ap.add_argument("--heap-words", type=int, default=None,
                     help="NFA per-key partial-match arena (words per semispace; option heap_words)")
+    return ap
+
+
+def main():
+    ap = build_parser()
     args = ap.parse_args()
     # before anything touches the GPU: N > 1 without a launcher starts one (a child process, never an exec)
     cmd = launch_command(args.gpus, sys.argv[1:], os.environ)
@@ -435,33 +488,29 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # config 4 on several GPUs: key partitions (default) or one exchanged stream (--shard exchange)
-    kpart = args.config == 4 and world > 1 and (args.shard or "partition") == "partition"
+    plan = run_plan(args.config, world)
     # (modulo the visible devices: a box with fewer GPUs than ranks shares them, a functional check only)
     local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    rccl_world = None
     if world > 1:
-        # key partitions exchange nothing on the data path: the control plane (barriers, the max of the step times,
-        # the sum of the match counts) runs over gloo; the exchange path uses RCCL over xGMI
-        if kpart:
-            dist.init_process_group("gloo")
-        else:
+        # one process per GPU; the data path (key exchange, match return, output merge) runs over RCCL / xGMI
+        if plan["backend"] == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+            rccl_world = dist.get_world_size()
+        else:
+            dist.init_process_group(plan["backend"])
     N = int(args.events if args.events is not None else cfg["events"])
     K = args.keys
     ts_div = args.ts_div if args.ts_div is not None else cfg["ts_div"]
     seed = seed_for(args.config)
-    shards = cfg["shards"] and not kpart
+    shards = plan["shards"]
     if shards:
         lo, hi = N * rank // world, N * (rank + 1) // world
-    else:  # replicas / key partitions: every rank runs the whole workload
+    else:  # replicas: every rank runs the whole workload
         lo, hi = 0, N
-    symbol, price, volume, tsattr, ts = gen_stock(lo, hi, K, ts_div, dev, seed + 7919 * rank if kpart else seed)
-    if kpart:
-        # rank r's partition: keys r*K .. r*K + K-1 (PartitionRuntime instances of disjoint key sets, which share no
-        # state: core/partition/PartitionRuntime.java:256-309), its own stream of N events
-        symbol += rank * K
+    symbol, price, volume, tsattr, ts = gen_stock(lo, hi, K, ts_div, dev, seed)
     if args.config != 2:
         del volume  # not referenced by the pattern: the exchange ships only what the plan reads
         volume = price
@@ -521,7 +570,7 @@ def main():
                 app.process_device_batch("StockStream", s_ts, [s_sym, s_price, s_price, s_price], ordinals=ords,
                                          hip_stream=hip_stream)
                 m = nm[0] = app.device_matches("q")[1]
-                if world == 1 or kpart:
+                if world == 1:
                     return None  # the output stays in the library's device buffer, in reference order
                 if mbuf[0] is None or mbuf[0].numel() < m:
                     mbuf[0] = torch.empty(max(m, 1) + (m >> 3), dtype=torch.int64, device=dev)
@@ -530,9 +579,7 @@ def main():
 
             # the reference's single output order across ranks (shard.partitioned_step): key exchange, matching,
             # every tuple returned to the rank that ingested its e2 and ordered there
-            # (key partitions: each rank's stream is its own, nothing crosses ranks)
-            mine = partitioned_step(symbol, [symbol, price, ts], 1 if kpart else world, lo, N, match, starts=starts,
-                                    offsets=offsets)
+            mine = partitioned_step(symbol, [symbol, price, ts], world, lo, N, match, starts=starts, offsets=offsets)
             if mine is not None:
                 out_local[0] = mine.numel()
             return nm[0]
@@ -578,19 +625,24 @@ def main():
     dt = time.perf_counter() - t0
     path = app.get_stat("fast_path:q")
     nfa_kernel = int(app.get_stat("nfa_kernel:q")) if args.config == 5 else 0
-    t = torch.tensor([dt], dtype=torch.float64, device="cpu" if kpart else dev)
-    m = torch.tensor([nm], dtype=torch.int64, device="cpu" if kpart else dev)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    m = torch.tensor([nm], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        if shards or kpart:
+        if shards:
             dist.all_reduce(m)
     dt = t.item()
     total_matches = m.item()
     ms_per_step = dt / args.steps * 1e3
-    units = N if shards else N * world  # replicas / key partitions: every rank processed a whole stream
+    units = N * plan["units_factor"]  # sharded: the one stream; replicas: every rank processed a whole stream
     value = units / (dt / args.steps)
+    kparts = None
+    if args.key_partitions and args.config == 4 and world > 1:
+        kparts = key_partitions_line(app, N, K, ts_div, seed, rank, world, dev, hip_stream, args.steps, args.warmup)
 
-    roof = roofline(ktot, n_local[0], nm, args.steps, args.config)
+    from siddhi_amd import _lib
+    build_id = _lib.lib().sm_build_id().decode()
+    roof = roofline(ktot, n_local[0], nm, args.steps, args.config, build_id, args.variant)
     e2e = None
     if args.config == 4 and world == 1 and not args.no_e2e:
         # SURVEY.md §8(d) end-to-end variant: the same step with the three columns the plan reads (symbol i32,
@@ -680,13 +732,12 @@ def main():
                              f"{' + global clock heartbeats' if args.config == 5 else ''}: {sect:.2f} s, {mt} matches",
                    "single_thread": {"value": v, "cores": 1, "seconds": sec}, **host_cpu()}
     if rank == 0:
-        alg = cfg["job_bytes"](N, total_matches) * (1 if shards else world) if not kpart else \
-            cfg["job_bytes"](N * world, total_matches)
+        alg = cfg["job_bytes"](N, total_matches) * plan["units_factor"]
         conf = {"workload": cfg["workload"], "config": args.config, "events": N,
                 "event_time": f"floor(i/{ts_div}) ms", "matches": total_matches,
-                "parallelism": (f"key-partitioned x{world} (rank r: keys r*K .. r*K+K-1, its own stream of "
-                                f"{N} events; no data-path collective)" if kpart else
-                                f"key-sharded x{world}" if args.config in (4, 5) else
+                "parallelism": (f"key-sharded x{world} (one stream, hash-by-key RCCL all-to-all)"
+                                if args.config in (4, 5) and world > 1 else
+                                "single GPU" if world == 1 else
                                 f"index-range-sharded x{world}" if cfg["shards"] else f"replicas x{world}"),
                 "device_path": (("general NFA (interleaved device events), " +
                                  {1: "query-specialised kernel", 2: "interpreter"}.get(nfa_kernel, "?"))
@@ -697,11 +748,14 @@ def main():
                 "step_hbm_fraction": alg / (ms_per_step * 1e-3) / HBM_PEAK}
         if args.config in (4, 5):
             conf["keys"] = K
+        conf["rccl_world"] = rccl_world
+        conf["build_id"] = build_id
+        conf["variant"] = args.variant or "literal"
         line = {
             "metric": METRIC if args.config == 4 else f"input events/sec + % HBM peak, {cfg['workload']}",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak" if kpart else cfg["scaling"], "vs_baseline": None,
+            "scaling": plan["scaling"], "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (counter-based splitmix64 StockStream, device-resident)",
             "config": conf, "roofline": roof, "cpu_baseline": cpu,
         }
@@ -711,6 +765,8 @@ def main():
             line["via_input_handler"] = ih
         if sparse:
             line["sparse_keys"] = sparse
+        if kparts:
+            line["key_partitions"] = kparts
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -758,7 +814,7 @@ def alg_bytes(label, n, m, config):
             }[label]
 
 
-def roofline(ktot, n, m, steps, config):
+def roofline(ktot, n, m, steps, config, build_id=None, variant=None):
     """Dominant kernel (largest total time over the timed steps). `achieved` follows SURVEY.md §8(d): the job's
     algorithmic bytes per event / per match (config 4: 20 B per event + 8 B per match) x the events and matches
     one launch of it processes (the dominant kernel handles the whole batch), / its average launch duration
@@ -774,10 +830,11 @@ def roofline(ktot, n, m, steps, config):
     own = alg_bytes(dom, n, m, config)
     brk = {k: {"avg_ms": v[0] / v[1], "calls_per_step": v[1] / steps,
                "gbps": alg_bytes(k, n, m, config) / (v[0] / v[1] * 1e-3) / 1e9} for k, v in ktot.items()}
-    traffic, src = pmc_traffic(config, n, dom)
-    step_traffic = pmc_step_traffic(config, n, brk)
+    doc, why = pmc_doc(config, n, build_id, variant)
+    traffic, src = pmc_traffic(doc, dom, config, variant)
+    step_traffic = pmc_step_traffic(doc, brk)
     return {"bound": "hbm", "achieved": ach / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": ach / HBM_PEAK,
-            "traffic": traffic, "traffic_unit": "HBM bytes per launch", "traffic_source": src,
+            "traffic": traffic, "traffic_unit": "HBM bytes per launch", "traffic_source": src or why,
             "kernel": dom, "avg_launch_ms": avg_ms, "alg_bytes_per_launch": job,
             "alg_bytes_basis": "SURVEY.md §8(d) job bytes of the batch the launch processes",
             "kernel_own_alg_bytes": own, "kernel_own_frac": own / (avg_ms * 1e-3) / HBM_PEAK,
@@ -786,17 +843,36 @@ def roofline(ktot, n, m, steps, config):
             "breakdown": brk}
 
 
-def pmc_step_traffic(config, n, brk):
-    """HBM bytes of one step: the committed PMC bytes per launch of every kernel label x its launches per step
-    (None unless the summary covers every kernel of the step at this event count)."""
-    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+def pmc_path(config, variant=None):
+    """profiles/pmc_config<C>.json (literal query) or profiles/pmc_config<C>_<variant>.json."""
+    return os.path.join(ROOT, "profiles", f"pmc_config{config}" + (f"_{variant}" if variant else "") + ".json")
+
+
+def pmc_doc(config, n, build_id, variant=None):
+    """The committed PMC summary of this configuration (tools/summarize_profile.py, from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this bench) if it describes THIS run: the same event count, the same query
+    variant and the same library build (sm_build_id, a hash of the kernel sources and build flags). Otherwise
+    (None, why): a profile of another build or variant never reaches the bench line."""
+    path = pmc_path(config, variant)
     try:
         doc = json.load(open(path))
     except (OSError, ValueError):
+        return None, f"no {os.path.relpath(path, ROOT)}"
+    if doc.get("events") != n:
+        return None, f"stale: {os.path.basename(path)} profiled {doc.get('events')} events, this run {n}"
+    if doc.get("variant", "literal") != (variant or "literal"):
+        return None, f"stale: {os.path.basename(path)} profiled variant {doc.get('variant')}"
+    if build_id is None or doc.get("build_id") != build_id:
+        return None, f"stale: {os.path.basename(path)} profiled build {doc.get('build_id')}, this build {build_id}"
+    return doc, None
+
+
+def pmc_step_traffic(doc, brk):
+    """HBM bytes of one step: the committed PMC bytes per launch of every kernel label x its launches per step
+    (None unless the summary matches this run and covers every kernel of the step)."""
+    if doc is None:
         return None
     labels = doc.get("labels", {})
-    if doc.get("events") != n:
-        return None
     tot = 0.0
     for lab, b in brk.items():
         ent = labels.get(lab)
@@ -808,19 +884,15 @@ def pmc_step_traffic(config, n, brk):
     return tot
 
 
-def pmc_traffic(config, n, label):
-    """HBM bytes per launch of `label` from the committed PMC summary of this configuration
-    (profiles/pmc_config<C>.json, written by tools/summarize_profile.py from separate rocprofv3 --pmc FETCH_SIZE /
-    WRITE_SIZE passes of this bench at the same event count), else None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
-    try:
-        doc = json.load(open(path))
-    except (OSError, ValueError):
+def pmc_traffic(doc, label, config, variant=None):
+    """HBM bytes per launch of `label` from the matching PMC summary (pmc_doc), else (None, None)."""
+    if doc is None:
         return None, None
     ent = doc.get("labels", {}).get(label)
-    if doc.get("events") != n or not ent or not ent.get("hbm_bytes"):
+    if not ent or not ent.get("hbm_bytes"):
         return None, None
-    return ent["hbm_bytes"], f"profiles/pmc_config{config}.json ({doc.get('tag')}: {doc.get('method')})"
+    return ent["hbm_bytes"], (f"{os.path.relpath(pmc_path(config, variant), ROOT)} ({doc.get('tag')}, build "
+                              f"{doc.get('build_id')}: {doc.get('method')})")
 
 
 if __name__ == "__main__":

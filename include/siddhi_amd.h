@@ -86,6 +86,9 @@ typedef void (*sm_query_callback)(void* user, int64_t timestamp, const sm_event*
 
 const char* sm_last_error(void);
 const char* sm_version(void);
+/* Identity of this build: 16 hex digits of sha256 over the library's sources, headers and build flags. Not a
+ * reference API; profiles/pmc_config<C>.json records it so bench.py reports PMC traffic only for the build measured. */
+const char* sm_build_id(void);
 
 int sm_manager_create(sm_manager** out);
 void sm_manager_destroy(sm_manager* m);

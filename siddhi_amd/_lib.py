@@ -15,7 +15,7 @@ TYPE_NAMES = {v: k for k, v in TYPE_CODES.items()}
 
 # Every symbol include/siddhi_amd.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
-    "sm_last_error", "sm_version", "sm_manager_create", "sm_manager_destroy", "sm_app_create", "sm_app_destroy",
+    "sm_last_error", "sm_version", "sm_build_id", "sm_manager_create", "sm_manager_destroy", "sm_app_create", "sm_app_destroy",
     "sm_app_start", "sm_app_flush", "sm_app_shutdown", "sm_app_input_handler", "sm_input_send",
     "sm_input_send_columns", "sm_app_stream_schema", "sm_app_advance_time", "sm_app_advance_wallclock",
     "sm_app_add_stream_callback", "sm_app_add_query_callback", "sm_app_set_collect", "sm_app_dump_outputs",
@@ -51,6 +51,7 @@ def lib():
         vp, cp, i64, sz = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_size_t
         L.sm_last_error.restype = cp
         L.sm_version.restype = cp
+        L.sm_build_id.restype = cp
         L.sm_manager_create.argtypes = [ctypes.POINTER(vp)]
         L.sm_manager_destroy.argtypes = [vp]
         L.sm_app_create.argtypes = [vp, cp, ctypes.POINTER(vp)]

@@ -26,6 +26,32 @@ _INT_DTYPES = (torch.int32, torch.int64)
 _BY_WIDTH = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
 
 
+def _staged(t: torch.Tensor, group) -> bool:
+    """A collective on device tensors over a gloo group (the functional rehearsal of the multi-GPU path with several
+    ranks sharing one GPU, where RCCL refuses duplicate devices) goes through host copies; over RCCL the tensors stay
+    in HBM and the collective runs over xGMI."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _all_to_all_single(out, inp, out_splits=None, in_splits=None, group=None):
+    if _staged(inp, group):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(h)
+        return
+    dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
+def _all_gather(outs, t, group=None):
+    if _staged(t, group):
+        hs = [torch.empty(o.shape, dtype=o.dtype) for o in outs]
+        dist.all_gather(hs, t.cpu(), group=group)
+        for o, h in zip(outs, hs):
+            o.copy_(h)
+        return
+    dist.all_gather(outs, t, group=group)
+
+
 def _i64(v):
     return v - (1 << 64) if v >= 1 << 63 else v
 
@@ -136,7 +162,7 @@ def unpack(rec: torch.Tensor, lay, dtypes):
 def _all_to_all_counts(send_counts, device, group):
     sc = torch.tensor(send_counts, dtype=torch.int64, device=device)
     rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
+    _all_to_all_single(rc, sc, group=group)
     return rc.tolist()
 
 
@@ -181,7 +207,7 @@ def exchange_by_key(keys: torch.Tensor, columns, world: int, group=None, packed=
     rec, sc, lay = pack_by_owner(keys, columns, world)
     rc = _all_to_all_counts(sc, keys.device, group)
     buf = torch.empty((sum(rc), rec.shape[1]), dtype=torch.int64, device=keys.device)
-    dist.all_to_all_single(buf, rec, rc, sc, group=group)
+    _all_to_all_single(buf, rec, rc, sc, group=group)
     if packed:  # the caller unpacks (exchange_with_ordinals: one pass with the ordinals)
         return (buf, lay), rc
     return unpack(buf, lay, [c.dtype for c in columns]), rc
@@ -191,7 +217,7 @@ def slice_starts(lo: int, world: int, device, group=None):
     """First global ordinal of every rank's ingest slice (all-gathered; a list of world ints)."""
     los = torch.tensor([lo], dtype=torch.int64, device=device)
     all_lo = [torch.empty_like(los) for _ in range(world)]
-    dist.all_gather(all_lo, los, group=group)
+    _all_gather(all_lo, los, group=group)
     return [int(x.item()) for x in all_lo]
 
 
@@ -266,7 +292,7 @@ def return_matches(pairs: torch.Tensor, starts, hi_last: int, world: int, group=
     sc = [cuts[r + 1] - cuts[r] for r in range(world)]
     rc = _all_to_all_counts(sc, pairs.device, group)
     buf = torch.empty(sum(rc), dtype=torch.int64, device=pairs.device)
-    dist.all_to_all_single(buf, pairs, rc, sc, group=group)
+    _all_to_all_single(buf, pairs, rc, sc, group=group)
     return order_matches(buf, lo, hi)
 
 
@@ -294,13 +320,13 @@ def concat_ordered(rows: torch.Tensor, world: int, group=None) -> torch.Tensor:
         return rows
     cnt = torch.tensor([rows.numel()], dtype=torch.int64, device=rows.device)
     cnts = [torch.empty_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt, group=group)
+    _all_gather(cnts, cnt, group=group)
     cs = [int(c.item()) for c in cnts]
     mx = max(cs)
     pad = torch.zeros(mx, dtype=rows.dtype, device=rows.device)
     pad[:rows.numel()] = rows
     parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
+    _all_gather(parts, pad, group=group)
     return torch.cat([p[:c] for p, c in zip(parts, cs)])
 
 
@@ -319,12 +345,12 @@ def clock_ticks(ts: torch.Tensor, lo: int, world: int, group=None) -> torch.Tens
         return mine
     cnt = torch.tensor([mine.shape[0]], dtype=torch.int64, device=ts.device)
     cnts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt, group=group)
+    _all_gather(cnts, cnt, group=group)
     cs = [int(c.item()) for c in cnts]
     pad = torch.zeros((max(cs), 2), dtype=torch.int64, device=ts.device)
     pad[:mine.shape[0]] = mine
     parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
+    _all_gather(parts, pad, group=group)
     return torch.cat([p[:c] for p, c in zip(parts, cs)])
 
 
@@ -401,7 +427,7 @@ def route_outputs(recs: torch.Tensor, starts, n_total: int, world: int, group=No
     sc = [(cuts[r + 1] - cuts[r]) * W for r in range(world)]
     rc = _all_to_all_counts(sc, recs.device, group)
     buf = torch.empty(sum(rc), dtype=torch.int64, device=recs.device)
-    dist.all_to_all_single(buf, recs.contiguous().view(-1), rc, sc, group=group)
+    _all_to_all_single(buf, recs.contiguous().view(-1), rc, sc, group=group)
     return buf.view(-1, W)
 
 

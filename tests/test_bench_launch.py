@@ -117,3 +117,45 @@ def test_partitioned_step_world2_equals_world1(tmp_path):
     assert single.numel() > 0.3 * N
     got = np.concatenate([np.asarray(p, dtype=np.int64) for p in parts])
     np.testing.assert_array_equal(got, single.numpy())
+
+
+def test_default_multi_gpu_plan_is_the_exchanged_stream():
+    """`bench.py --gpus N` (config 4, no flags) measures BASELINE's configuration, one stream of N
+    events routed by key over RCCL: value counts N (strong scaling), not N x world."""
+    args = bench.build_parser().parse_args(["--gpus", "2"])
+    assert args.config == 4 and not args.key_partitions
+    plan = bench.run_plan(args.config, 2, env={})
+    assert plan == {"shards": True, "units_factor": 1, "backend": "nccl", "exchange": True, "scaling": "strong"}
+    for c in (2, 5):
+        p = bench.run_plan(c, 8, env={})
+        assert p["units_factor"] == 1 and p["backend"] == "nccl"
+    assert bench.run_plan(5, 8, env={})["exchange"]
+    # config 3 does not shard: replicas, counted per rank
+    p3 = bench.run_plan(3, 4, env={})
+    assert p3["units_factor"] == 4 and p3["scaling"] == "weak" and not p3["exchange"]
+    assert bench.run_plan(4, 1, env={})["backend"] is None
+    assert bench.run_plan(4, 2, env={"SM_BENCH_BACKEND": "gloo"})["backend"] == "gloo"
+
+
+def test_stale_pmc_profile_yields_null_traffic(tmp_path, monkeypatch):
+    """the roofline's PMC traffic is reported only when the committed summary names the same
+    event count, query variant and library build (sm_build_id) as the running bench."""
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    (tmp_path / "profiles").mkdir()
+    n, m = 1000, 400
+    ktot = {"stack": [10.0, 5], "order": [2.0, 5]}
+    doc = {"config": 4, "events": n, "matches": m, "tag": "t", "build_id": "abcd", "variant": "literal",
+           "method": "x", "labels": {"stack": {"hbm_bytes": 5e4}, "order": {"hbm_bytes": 1e4}}}
+    (tmp_path / "profiles" / "pmc_config4.json").write_text(json.dumps(doc))
+    r = bench.roofline(ktot, n, m, 5, 4, build_id="abcd")
+    assert r["traffic"] == 5e4 and r["traffic_step"] == 6e4 and "build abcd" in r["traffic_source"]
+    r = bench.roofline(ktot, n, m, 5, 4, build_id="ffff")
+    assert r["traffic"] is None and r["traffic_step"] is None and "stale" in r["traffic_source"]
+    r = bench.roofline(ktot, n + 1, m, 5, 4, build_id="abcd")
+    assert r["traffic"] is None
+    # a variant reads its own file; the literal query's profile never stands in for it
+    r = bench.roofline(ktot, n, m, 5, 4, build_id="abcd", variant="pattern_count_not5s")
+    assert r["traffic"] is None and "no profiles/pmc_config4_pattern_count_not5s.json" in r["traffic_source"]
+    doc["variant"] = "pattern_count_not5s"
+    (tmp_path / "profiles" / "pmc_config4_pattern_count_not5s.json").write_text(json.dumps(doc))
+    assert bench.roofline(ktot, n, m, 5, 4, build_id="abcd", variant="pattern_count_not5s")["traffic"] == 5e4

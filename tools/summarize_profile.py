@@ -118,16 +118,34 @@ def main():
                      f"{rd / 1e9 if rd is not None else float('nan'):.2f} | "
                      f"{wr / 1e9 if wr is not None else float('nan'):.2f} | "
                      f"{alg / (avg * 1e-3) if avg else 0:.0f} |")
-    lines += ["", "bench line:", "", "```", json.dumps(bench), "```"]
+    # the embedded bench line carries THIS profile's PMC bytes (the bench ran before the PMC passes existed, so its
+    # own traffic fields came from the previous summary or were null): one source for the table and the line
+    roof = bench["roofline"]
+    dom = roof.get("kernel")
+    if dom in traffic:
+        roof["traffic"] = traffic[dom]["read_bytes"] + traffic[dom]["write_bytes"]
+        roof["traffic_source"] = f"this profile's PMC passes ({tag})"
+        tot = 0.0
+        for lab, b in brk.items():
+            if lab in traffic:
+                tot += (traffic[lab]["read_bytes"] + traffic[lab]["write_bytes"]) * b["calls_per_step"]
+        roof["traffic_step"] = tot
+        roof["traffic_step_ratio"] = tot / roof["alg_bytes_per_launch"]
+    lines += ["", f"library build `{bench['config'].get('build_id')}`, variant `{bench['config'].get('variant')}`",
+              "", "bench line (roofline traffic fields from the PMC passes above):", "", "```", json.dumps(bench),
+              "```"]
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     open(os.path.join(ROOT, "profiles", f"{tag}.md"), "w").write("\n".join(lines) + "\n")
-    doc = {"config": config, "events": n, "matches": m, "tag": tag,
+    variant = bench["config"].get("variant", "literal")
+    doc = {"config": config, "events": n, "matches": m, "tag": tag, "build_id": bench["config"].get("build_id"),
+           "variant": variant,
            "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction) and --pmc WRITE_SIZE, separate "
                      "passes, 1 step; bytes per launch",
            "labels": {k: {"read_bytes": v["read_bytes"], "write_bytes": v["write_bytes"],
                           "hbm_bytes": v["read_bytes"] + v["write_bytes"], "kernels": v["kernels"]}
                       for k, v in traffic.items()}}
-    json.dump(doc, open(os.path.join(ROOT, "profiles", f"pmc_config{config}.json"), "w"), indent=1)
+    name = f"pmc_config{config}" + ("" if variant == "literal" else f"_{variant}") + ".json"
+    json.dump(doc, open(os.path.join(ROOT, "profiles", name), "w"), indent=1)
     print("\n".join(lines[:40]))
 
 
