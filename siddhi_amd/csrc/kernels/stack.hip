@@ -59,6 +59,9 @@ constexpr int kOCap = kOT * 4 + 12288 * 8 <= 160 * 1024 ? 12288 : 0;
 #define SM_ORDER_GT (SM_ORDER_TB >= 15 ? 4 : 16)  // A/B build flag
 #endif
 constexpr int kGT = SM_ORDER_GT;  // consecutive tiles per order workgroup
+#ifndef SM_ORDER_XCD
+#define SM_ORDER_XCD 0  // A/B build flag: 1 = XCD-contiguous tile groups (blocks b and b + 8 share an XCD and its L2)
+#endif
 
 static_assert(kBins == kKeys && kKeys == kKPT * kSB && kBins == kOB && (kKPT == 1 || kKPT == 2),
               "one or two in-bucket keys per thread, one bucket per order thread");
@@ -517,8 +520,16 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const uint64_t gmask = 0xffffull << (g * 16);
-  // groups of kGT tiles, one per workgroup
-  for (int64_t tb = (int64_t)blockIdx.x * kGT; tb < a.ntiles; tb += (int64_t)gridDim.x * kGT) {
+  // groups of kGT tiles, one per workgroup. XCD-contiguous: the dispatcher deals blocks round-robin over the 8 XCDs
+  // (MI355X_MICROARCH.md, dispatch), so block b is remapped to group xcd_rank(b): the ~32 workgroups an XCD runs at
+  // once take consecutive groups, and the segment lines two neighbouring tiles share are fetched into that XCD's L2
+  // once, by whichever of them reads first (a bucket's segments of consecutive tiles are adjacent in its run)
+  int64_t blk = blockIdx.x;
+  if (SM_ORDER_XCD) {
+    const int64_t G = gridDim.x, q = G >> 3, r = G & 7, x = blk & 7, i = blk >> 3;
+    blk = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+  }
+  for (int64_t tb = blk * kGT; tb < a.ntiles; tb += (int64_t)gridDim.x * kGT) {
   const int64_t te = tb + kGT < a.ntiles ? tb + kGT : a.ntiles;
   uint32_t ms = a.mt[tb * kBins + tid];
   uint32_t tot;

@@ -1,11 +1,14 @@
-"""Sum rocprofv3 PMC CSVs (gpurun_out/pmc_*/run_counter_collection.csv) per kernel family."""
+"""Sum rocprofv3 PMC CSVs (gpurun_out/pmc_*/run_counter_collection.csv, or the directory given) per kernel family."""
 import collections
 import csv
 import glob
 import re
+import sys
 
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
-for f in sorted(glob.glob("gpurun_out/pmc_*/run_counter_collection.csv")):
+pat = (sys.argv[1].rstrip("/") + "/**/*counter_collection.csv") if len(sys.argv) > 1 else \
+    "gpurun_out/pmc_*/run_counter_collection.csv"
+for f in sorted(glob.glob(pat, recursive=True)):
     for r in csv.DictReader(open(f)):
         m = re.search(r"(walk_kernel<\w+>|onesweep_kernel<\d|prep_kernel|key_hist|u32_hist|hist_scan|filter_\w+_kernel|pass0_kernel|downsweep_wc_kernel<\d|stack4_kernel|order_kernel)",
                       r["Kernel_Name"])
