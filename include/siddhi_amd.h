@@ -281,7 +281,12 @@ int sm_app_device_project(sm_app* app, const char* query_name, sm_dval* d_values
  * kernels, 2 = sort / walk kernels, 1 = general closed form (option fast_general), 5 = general NFA kernel (hand-over);
  * filter queries 3 = filter interpreter, 4 = typed conjunction. "output_events:<query>" = its output count.
  * "kernel_ms:<label>" / "kernel_calls:<label>" and "fast_ms:group" / "fast_ms:walk" / "fast_ms:order" (per-kernel
- * and phase times in ms; need the "fast_timing" option). */
+ * and phase times in ms; need the "fast_timing" option). "nfa_state:<query>" = 1 once a closed-form pattern's matching
+ * state is held by the general NFA kernel for good: host events it could not take on the closed form (a null value,
+ * a chained or broadcast app) or a device batch outside its premise (event time decreasing) handed its carried
+ * partials over, and every later batch of that query runs on the NFA kernel (same results, the NFA's speed).
+ * NFA overflow pool of a pattern query: "pool_words:<query>", "pool_used:<query>", "pool_compactions:<query>",
+ * "pool_refused:<query>" (batches in which a key's promotion did not fit; the pool is grown for it after the batch). */
 int sm_app_get_stat(sm_app* app, const char* key, double* out);
 
 #ifdef __cplusplus

@@ -70,8 +70,9 @@ struct NfaBatch {
   uint32_t out_cap;
   uint32_t out_stride;
   // device-wide overflow pool of per-key arenas: a key whose live partial matches outgrow its own arena moves its
-  // heap into a larger region bump-allocated here (Lane::promote). pool_top counts the words handed out (it may
-  // pass pool_cap: that request failed and the key stayed in its arena; the host grows the pool after the batch).
+  // heap into a larger region bump-allocated here (Lane::promote). pool_top counts the words handed out; a request
+  // that does not fit claims nothing, and pool_top[1] keeps the largest such request, so that the host sizes the pool
+  // for it after the batch (without the demand a hot key's failed promotion never grew the pool).
   int64_t* pool;
   unsigned long long* pool_top;
   int64_t pool_cap;

@@ -1170,12 +1170,15 @@ struct Lane {
     if (nh < 8 * live) nh = 8 * live;
     return (nh + 63) & ~(int64_t)63;
   }
-  // `words` of the overflow pool, or -1 when it is full (a failed request claims nothing: the host sizes the pool
-  // from pool_top after the batch)
+  // `words` of the overflow pool, or -1 when it is full (a failed request claims nothing; it leaves its size in
+  // pool_top[1], from which the host sizes the pool after the batch)
   __device__ int64_t pool_claim(int64_t words) {
     unsigned long long cur = *(volatile unsigned long long*)b->pool_top;
     for (;;) {
-      if ((int64_t)cur + words > b->pool_cap) return -1;
+      if ((int64_t)cur + words > b->pool_cap) {
+        atomicMax(b->pool_top + 1, (unsigned long long)words);
+        return -1;
+      }
       const unsigned long long prev = atomicCAS(b->pool_top, cur, cur + (unsigned long long)words);
       if (prev == cur) return (int64_t)cur;
       cur = prev;

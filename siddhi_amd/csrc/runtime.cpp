@@ -272,6 +272,7 @@ struct QueryRt {
   DBuf pool, pool_top_dev;
   int64_t pool_words = 0;
   uint64_t pool_used = 0;
+  int64_t pool_refused = 0;  // batches in which a promotion did not fit the pool (stat pool_refused:<query>)
   int64_t pool_compactions = 0;
   ~QueryRt() {
     carry.release();
@@ -996,9 +997,9 @@ void ensure_state(sm_app* a, QueryRt& q, int64_t nkeys) {
 // The query's overflow pool holds at least `words` words, the first `keep` of them preserved (a promoted key's heap
 // is addressed by its pool offset, so growing copies the used prefix into the larger buffer).
 void ensure_pool(sm_app* a, QueryRt& q, int64_t words, int64_t keep) {
-  if (!q.pool_top_dev.p) {
-    q.pool_top_dev.ensure(8);
-    SM_HIP(hipMemsetAsync(q.pool_top_dev.p, 0, 8, a->stream));
+  if (!q.pool_top_dev.p) {  // {words handed out, largest failed request of the batch}
+    q.pool_top_dev.ensure(16);
+    SM_HIP(hipMemsetAsync(q.pool_top_dev.p, 0, 16, a->stream));
   }
   if (words <= q.pool_words) return;
   void* np = nullptr;
@@ -1139,6 +1140,7 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.pool = (int64_t*)q.pool.p;
   b.pool_top = (unsigned long long*)q.pool_top_dev.p;
   b.pool_cap = q.pool_words;
+  SM_HIP(hipMemsetAsync((uint64_t*)q.pool_top_dev.p + 1, 0, 8, hs));
   SM_HIP(hipMemsetAsync(a->d_count.p, 0, 4, hs));
   SM_HIP(hipMemsetAsync(a->d_err.p, 0, 4, hs));
   launch_lane_events(b, N, nq, h.node_words, (int32_t*)a->sc.take((size_t)std::max<int64_t>(N, 1) * 4),
@@ -1174,13 +1176,17 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   int32_t he = 0;
   SM_HIP(hipMemcpyAsync(&hc, a->d_count.p, 4, hipMemcpyDeviceToHost, hs));
   SM_HIP(hipMemcpyAsync(&he, a->d_err.p, 4, hipMemcpyDeviceToHost, hs));
-  SM_HIP(hipMemcpyAsync(&q.pool_used, q.pool_top_dev.p, 8, hipMemcpyDeviceToHost, hs));
+  uint64_t ptop[2] = {0, 0};
+  SM_HIP(hipMemcpyAsync(ptop, q.pool_top_dev.p, 16, hipMemcpyDeviceToHost, hs));
   SM_HIP(hipStreamSynchronize(hs));
-  // keep the pool at most half full for the next batch's promotions: reclaim dead regions first (compact_pool), grow
-  // only if the live partial matches need it
-  if ((int64_t)q.pool_used * 2 > q.pool_words) compact_pool(a, q, nkeys, hs);
-  if ((int64_t)q.pool_used * 2 > q.pool_words)
-    ensure_pool(a, q, std::max<int64_t>(2 * q.pool_words, 2 * (int64_t)q.pool_used), (int64_t)q.pool_used);
+  q.pool_used = ptop[0];
+  const int64_t want = (int64_t)ptop[1];  // largest promotion the pool could not take this batch (0: none failed)
+  if (want > 0) ++q.pool_refused;
+  // keep the pool at most half full for the next batch's promotions, with room for the largest refused one: reclaim
+  // dead regions first (compact_pool), grow only if the live partial matches and that request need it
+  if (((int64_t)q.pool_used + want) * 2 > q.pool_words) compact_pool(a, q, nkeys, hs);
+  if (((int64_t)q.pool_used + want) * 2 > q.pool_words)
+    ensure_pool(a, q, std::max<int64_t>(2 * q.pool_words, 2 * ((int64_t)q.pool_used + want)), (int64_t)q.pool_used);
   if (he) {
     std::string why;
     if (he & NFA_ERR_ARENA)
@@ -3377,6 +3383,14 @@ int sm_app_get_stat(sm_app* a, const char* key, double* out) {
         }
       throw sql::ValidationError("No query with name " + k.substr(14));
     }
+    if (k.rfind("nfa_state:", 0) == 0) {  // 1 = the query's matching state is held by the NFA kernel from now on
+      for (auto& q : a->queries)
+        if (q->cq.name == k.substr(10)) {
+          *out = (q->nfa_mode || q->nfa_used) ? 1.0 : 0.0;
+          return;
+        }
+      throw sql::ValidationError("No query with name " + k.substr(10));
+    }
     if (k.rfind("nfa_kernel:", 0) == 0) {  // 1 = query-specialised kernel, 2 = interpreter, 0 = not run
       for (auto& q : a->queries)
         if (q->cq.name == k.substr(11)) {
@@ -3385,13 +3399,14 @@ int sm_app_get_stat(sm_app* a, const char* key, double* out) {
         }
       throw sql::ValidationError("No query with name " + k.substr(11));
     }
-    for (const char* pk : {"pool_words:", "pool_used:", "pool_compactions:"}) {  // overflow pool of a pattern query
+    for (const char* pk : {"pool_words:", "pool_used:", "pool_compactions:", "pool_refused:"}) {  // overflow pool
       const std::string pre = pk;
       if (k.rfind(pre, 0) == 0) {
         for (auto& q : a->queries)
           if (q->cq.name == k.substr(pre.size())) {
             *out = pre == "pool_words:" ? (double)q->pool_words
                  : pre == "pool_used:"  ? (double)q->pool_used
+                 : pre == "pool_refused:" ? (double)q->pool_refused
                                         : (double)q->pool_compactions;
             return;
           }

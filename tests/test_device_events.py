@@ -259,3 +259,59 @@ def test_rotating_hot_keys_keep_the_pool_bounded():
     assert got == exp
     assert compactions > 0
     assert max(words[batches // 2:]) <= 2 * max(words[:4]), "the pool keeps growing with every hot key"
+
+
+@pytest.mark.gpu
+def test_growing_key_after_compaction_gets_room():
+    """one key keeps collecting open partials across small batches while rotating hot keys make
+    the pool compact at batch boundaries. A compaction sizes the pool from the live words; when the growing key's next
+    promotion then does not fit, the refused request is recorded on the device (pool_top[1]) and the host grows the
+    pool for it after the batch, so the key is promoted in a later batch instead of filling its region until the
+    query fails. Outputs equal the oracle's."""
+    rng = np.random.default_rng(11)
+    text = synth.app5("every e1=A -> e2=B[price > e1.price]", playback=False,
+                      select="select e1.timestamp as a, e2.timestamp as b insert into Out;")
+    batches, per, grow = 16, 2500, 900
+    sid_l, sym_l, price_l = [], [], []
+    for b in range(batches):
+        hot = np.full(per, 200_000 + b, np.int32)
+        keep = np.full(grow, 7, np.int32)  # the growing key: A's that no B of this stream exceeds until the end
+        other = rng.integers(1000, 3000, per).astype(np.int32)
+        sym = np.concatenate([hot, keep, other])
+        sid = np.concatenate([np.zeros(per + grow, np.int32), rng.integers(0, 2, per).astype(np.int32)])
+        price = np.concatenate([rng.random(per) * 50, 60 + rng.random(grow) * 30, rng.random(per) * 100])
+        perm = rng.permutation(len(sym))
+        sym_l += [sym[perm], np.array([200_000 + b], np.int32)]
+        sid_l += [sid[perm], np.array([1], np.int32)]
+        price_l += [price[perm], np.array([99.0])]
+    sym_l.append(np.array([7], np.int32))
+    sid_l.append(np.array([1], np.int32))
+    price_l.append(np.array([99.9]))
+    sizes = [len(x) for x in sym_l]
+    bounds = list(np.cumsum([0] + [sizes[2 * b] + sizes[2 * b + 1] for b in range(batches)]))
+    bounds[-1] += 1  # the final B joins the last batch
+    sym, sid, price = np.concatenate(sym_l), np.concatenate(sid_l), np.concatenate(price_l)
+    n = len(sym)
+    assert bounds[-1] == n
+    cols = [sym, price, np.zeros(n, np.int64), np.arange(n, dtype=np.int64)]
+    ts = np.arange(n, dtype=np.int64)
+    exp = oracle_out(text, sid, cols, ts)
+    import torch
+    from siddhi_amd.testing import ProductApp
+    dev = torch.device("cuda", 0)
+    a = ProductApp(text, heap_words=1024)
+    a.start()
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        tsid = torch.from_numpy(np.ascontiguousarray(sid[lo:hi])).to(dev)
+        tts = torch.from_numpy(np.ascontiguousarray(ts[lo:hi])).to(dev)
+        tcols = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
+        torch.cuda.synchronize()
+        a.process_device_events(tsid, tts, tcols, ordinal_base=int(lo))
+    stats = {k: int(a.get_stat(f"{k}:q")) for k in ("pool_words", "pool_used", "pool_compactions", "pool_refused")}
+    a.flush()
+    got = a.outputs()
+    a.close()
+    print("pool", stats)
+    assert sum(1 for r in exp["streams"]["Out"] if r[1][1] == n - 1) == batches * grow
+    assert got == exp
+    assert stats["pool_compactions"] > 0
