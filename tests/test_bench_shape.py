@@ -208,3 +208,86 @@ def test_brute_force_statement_matches_oracle_small():
                                 torch.from_numpy(ts), 1000).numpy()
         np.testing.assert_array_equal(np.stack([ref & 0xFFFFFFFF, ref >> 32], 1), exp)
 
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_config5_emitting_variant_at_bench_size():
+    """bench.py --config 5 --variant pattern_count_not5s at its benchmarked size (N = 1e8 events,
+    K = 1e6 keys, ts_i = floor(i / 100) ms, the bench's device-generated stream, heap_words 4096, query-specialised
+    NFA kernel, one batch). The output records of the keys `symbol % 1009 == 5` (timestamp, select values, nulls, in
+    delivery order) equal the oracle run on that key subsample with every other event's clock advance as a heartbeat
+    (the playback clock is global: core/stream/StreamJunction.java:232-237)."""
+    import torch
+    from siddhi_amd.testing import ProductApp
+    import synth
+    from test_device_events import oracle_out
+    N, K, div = 100_000_000, 1_000_000, 100
+    seed = bench.seed_for(5)
+    dev = _dev()
+    sym, price, vol, idx, ts = bench.gen_stock(0, N, K, div, dev, seed)
+    sid = bench.gen_stream_idx(0, N, dev, seed)
+    text = synth.app5(bench.VARIANTS5["pattern_count_not5s"])
+    # the oracle on the key subsample + heartbeats
+    first = torch.ones(N, dtype=torch.bool, device=dev)
+    first[1:] = ts[1:] > ts[:-1]
+    mine = (sym.to(torch.int64) % 1009) == 5
+    keep = mine | first
+    s_sid = torch.where(mine, sid, torch.full_like(sid, -1))[keep].cpu().numpy().astype(np.int32)
+    s_cols = [c[keep].cpu().numpy() for c in (sym, price, vol, idx)]
+    exp = oracle_out(text, s_sid, s_cols, ts[keep].cpu().numpy())
+    want = exp["streams"].get("Out", [])
+    assert len(want) > 10_000
+    # the product over the whole stream, outputs kept on the device
+    app = ProductApp(text, heap_words=4096, keep_outputs=1)
+    app.set_collect(False)
+    app.start()
+    torch.cuda.synchronize()
+    app.process_device_events(sid, ts, [sym, price, vol, idx])
+    assert int(app.get_stat("nfa_kernel:q")) == 1
+    n_out = int(app.get_stat("output_events:q"))
+    recs = app.copy_device_outputs("q")
+    app.close()
+    assert recs.shape[0] == n_out > 10_000_000
+    nsel = 5
+    vals = recs[:, 7:7 + 2 * nsel:2]
+    nulls = (recs[:, 8:8 + 2 * nsel:2] & 0xFFFFFFFF) != 0
+    sel = (sym[vals[:, 0]].to(torch.int64) % 1009) == 5  # e1.timestamp = the e1 event's index
+    got_ts = recs[sel, 3].cpu().tolist()
+    got_v = vals[sel].cpu().tolist()
+    got_n = nulls[sel].cpu().tolist()
+    got = [[t, [None if nn else v for v, nn in zip(vs, ns)]] for t, vs, ns in zip(got_ts, got_v, got_n)]
+    assert got == [[r[0], r[1]] for r in want]
+    print(f"config 5 variant N={N}: {n_out} outputs; key subsample {len(want)} equal to the oracle")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_null_stream_batch_reads_what_torch_just_wrote():
+    """VERDICT r04 next #7 (the race fixed in round 4): sm_app_process_device_batch with hip_stream NULL must wait for
+    work torch has queued on its own stream. The columns are produced by torch right before the call and the test
+    does NOT synchronize; the result must equal the same batch run on settled inputs."""
+    import torch
+    from siddhi_amd.testing import ProductApp
+    N, div = 30_000_000, 1
+    dev = _dev()
+    app = ProductApp(bench.APP3)
+    app.set_collect(False)
+    ref = None
+    for settle in (True, False):
+        torch.cuda.synchronize()
+        sym, price, vol, tsa, ts = bench.gen_stock(0, N, 1_000_000, div, dev, bench.seed_for(3))
+        del vol, tsa
+        # a last long-running torch kernel writing the compared column, still queued when the library is called
+        price = (price * 3.0 + 1.0 - 1.0) / 3.0
+        price = torch.where(price > 1e300, price, price)
+        if settle:
+            torch.cuda.synchronize()
+        app.set_option("reset", 0)
+        app.process_device_batch("StockStream", ts, [sym, price, price, price])  # hip_stream NULL
+        got = product_pairs(app, N).clone()
+        if settle:
+            ref = got
+    app.close()
+    assert ref.numel() > 0.5 * N
+    assert got.numel() == ref.numel() and torch.equal(got, ref)
