@@ -254,6 +254,23 @@ def test_non_monotone_batch_hands_over_to_nfa(stack):
     np.testing.assert_array_equal(np.concatenate(got), exp)
 
 
+@pytest.mark.parametrize("wide", [False, True])
+def test_non_monotone_first_batch_hands_over(wide):
+    """Round 5: the keyed closed form's prep no longer reads the event times (key pass 0 checks them). A first batch
+    whose times decrease must still reach the NFA with the reference's outputs, also when its keys span more than the
+    bucket-stack window (wide: the key-span answer must not win over the time check, so no dense ids are assigned to
+    a batch the closed form never takes)."""
+    n, K, div = 40000, 300, 5
+    cols, ts = stock(n, K, div, key_dtype=np.int64)
+    if wide:
+        cols[0] = cols[0] * 5_000_011 - 7  # span of about 1.5e9 keys
+    ts = _shuffle_times(ts, 30000, 38000)
+    text = app_text(kt="long")
+    exp = oracle_pairs(text, cols, ts)
+    got = run_stream(text, cols, ts, [(0, 38000), (38000, n)], expect_path=5)
+    np.testing.assert_array_equal(got, exp)
+
+
 def test_batch_earlier_than_carried_state_hands_over():
     """A batch whose first event is older than the last carried one (time going back across batches)."""
     n, K, div = 20000, 100, 5
