@@ -146,6 +146,10 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
         if (TS) tt[k] = __builtin_nontemporal_load(ts + p);
         if (EXTRA && ord) oo[k] = ord[p];
         if (EXTRA && vlong) vv[k] = vlong[p];
+        if (!TS && lane == 0 && (p & 255) == 0 && p > 0) {  // lean: the pass-0 wave-block boundaries (OrigSrc::check)
+          tt[k] = ts[p];
+          tp[k] = ts[p - 1];
+        }
         if (lane == 0 && p > 0) {  // the element before each wave-item (other lanes take it from lane - 1)
           if (TS) tp[k] = ts[p - 1];
           if (EXTRA && ord) op[k] = ord[p - 1];
@@ -160,6 +164,8 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
         int64_t pt = __shfl_up(tt[k], 1, 64);
         if (lane == 0) pt = p > 0 ? tp[k] : tt[k];
         if (in && tt[k] < pt) bad = 1;
+      } else if (in && lane == 0 && (p & 255) == 0 && p > 0 && tt[k] < tp[k]) {
+        bad = 1;
       }
       if (EXTRA && ord) {
         int64_t po = __shfl_up(oo[k], 1, 64);
@@ -388,6 +394,7 @@ struct OrigSrc {
   bool c1_inline;
   Cond c1;
   Ctrl* chk;  // non-null: prep did not read the event times (TS = false); pass 0 checks they do not decrease
+  bool bad = false;
   __device__ void init() {
     if (c1_inline) c1 = make_cond(c1code, c1len, consts);
   }
@@ -429,14 +436,17 @@ struct OrigSrc {
     r.m = c1_inline ? 0ull : c1mask[p >> 6];
     return r;
   }
-  // pass0_kernel, chk set: event i of a wave-item against event i - 1 (lane - 1, or the column for lane 0); one
-  // flag per wave
-  __device__ void check(const Raw& r, int64_t p, bool valid) const {
+  // pass0_kernel, chk set: element p (wave-item k of a 256-event wave block) against element p - 1 from registers:
+  // lane - 1, or lane 63 of item k - 1 for lane 0. The first element of a wave block (p % 256 == 0) is checked by
+  // the lean prep instead (prep_kernel TS = false), so no load is added here. Reported once, at flush().
+  static_assert(kP0Items * 64 == 256 && kP0Tile % 256 == 0 && kTile % kP0Tile == 0,
+                "pass-0 wave blocks of 256 events on 256-aligned chunk tiles (the lean prep checks their boundaries)");
+  __device__ void check(const Raw& r, const Raw& rp, int k, bool valid) {
     if (!chk) return;
     int64_t pt = __shfl_up(r.t, 1, 64);
-    if ((threadIdx.x & 63) == 0) pt = p > 0 ? ts[p - 1] : r.t;
-    const bool bad = valid && r.t < pt;
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&chk->bad_ts, 1u);
+    const int64_t p63 = __shfl(rp.t, 63, 64);
+    if ((threadIdx.x & 63) == 0) pt = k > 0 ? p63 : r.t;
+    bad |= valid && r.t < pt;
   }
   __device__ void split(const Raw& r, int64_t p, uint64_t& a, uint64_t& b) const {
     const uint32_t c1 = c1_bit(r.v, r.m, p);
@@ -448,7 +458,9 @@ struct OrigSrc {
     return make_uint4((uint32_t)((int64_t)r.k - kmin) | (c1 << 31), (uint32_t)r.o, vcode<VT>(r.v, vmode, vmin),
                       (uint32_t)(r.t - ts0));
   }
-  __device__ void flush() {}
+  __device__ void flush() {
+    if (chk && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(&chk->bad_ts, 1u);
+  }
 };
 
 struct RecSrc {

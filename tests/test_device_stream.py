@@ -271,6 +271,21 @@ def test_non_monotone_first_batch_hands_over(wide):
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize("at", [8192, 8192 + 77, 255, 256, 4095, 37 * 256])
+def test_single_time_step_back_is_found(at):
+    """One event time lower than its predecessor's, at a pass-0 wave-block boundary (multiples of 256, checked by the
+    lean prep) or inside a block (checked by key pass 0): the batch goes to the NFA, outputs stay the reference's."""
+    n, K, div = 20000, 100, 4
+    cols, ts = stock(n, K, div)
+    ts = ts.copy()
+    ts[at] = ts[at - 1] - 1
+    assert ts[at] < ts[at - 1]
+    text = app_text()
+    exp = oracle_pairs(text, cols, ts)
+    got = run_stream(text, cols, ts, [(0, n)], expect_path=5)
+    np.testing.assert_array_equal(got, exp)
+
+
 def test_batch_earlier_than_carried_state_hands_over():
     """A batch whose first event is older than the last carried one (time going back across batches)."""
     n, K, div = 20000, 100, 5
