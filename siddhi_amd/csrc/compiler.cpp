@@ -532,6 +532,39 @@ CompiledQuery compile_query(const App& app, const Query& q, int order, int parti
     int root = lw.parse(q.state.get(), -1, -1);
     // StateInputStreamParser.parseInputStream :124-125
     lw.pres[lw.inners[root].first].thisLast = lw.inners[root].last;
+    // list-node operand caches (plan.h DPre.ncache): a trialCur stream / count state whose filter reads at most two
+    // distinct operands of other states, each an earlier PK_STREAM state (its single-event chain is set before the
+    // partial reaches this state and is changed afterwards only by that state's own processor, which has let the
+    // partial go). Loads are keyed by (state, index, attribute, op).
+    for (auto& P : lw.pres) {
+      P.ncache = 0;
+      P.cacheIns[0] = P.cacheIns[1] = -1;
+      if (!P.trialCur || P.progLen == 0 || (P.kind != PK_STREAM && P.kind != PK_COUNT)) continue;
+      bool ok = true;
+      int n = 0;
+      for (int i = P.progOff; i < P.progOff + P.progLen && ok; ++i) {
+        const Instr& in = lw.code[i];
+        if (in.op != OP_VAR && in.op != OP_TS) continue;
+        if (in.a == P.stateId) continue;  // own state: the incoming event (trialCur)
+        const DPre* src = nullptr;
+        for (auto& Q : lw.pres)
+          if (Q.stateId == in.a) src = &Q;
+        if (!src || src->kind != PK_STREAM || in.a >= P.stateId) {
+          ok = false;
+          break;
+        }
+        bool seen = false;
+        for (int k = 0; k < n; ++k) {
+          const Instr& c = lw.code[P.cacheIns[k]];
+          seen |= c.op == in.op && c.a == in.a && c.b == in.b && c.c == in.c;
+        }
+        if (seen) continue;
+        if (n == 2) ok = false;
+        else P.cacheIns[n++] = i;
+      }
+      if (ok && n > 0) P.ncache = n;
+      else P.cacheIns[0] = P.cacheIns[1] = -1;
+    }
     // receivers :95-114
     std::vector<std::string> ids;
     collect_stream_ids(q.state.get(), ids);

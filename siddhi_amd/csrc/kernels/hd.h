@@ -35,6 +35,11 @@ inline unsigned long long atomicCAS(unsigned long long* p, unsigned long long cm
   if (o == cmp) *p = v;
   return o;
 }
+inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) {
+  unsigned long long o = *p;
+  if (v > o) *p = v;
+  return o;
+}
 #else
 // Wave emulator (tests/native/stack_emu.cpp, test infrastructure): every GPU thread of a workgroup is a fiber of one
 // host thread; wave64 operations and __syncthreads are barriers of the fibers of a wave / the workgroup (the
@@ -106,6 +111,12 @@ inline int atomicOr(int* p, int v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ
 inline unsigned long long atomicCAS(unsigned long long* p, unsigned long long cmp, unsigned long long v) {
   __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
   return cmp;
+}
+inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) {
+  unsigned long long o = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+  while (v > o && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
+  }
+  return o;
 }
 inline unsigned __float_as_uint(float f) {
   unsigned u;

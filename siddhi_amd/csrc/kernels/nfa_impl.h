@@ -18,7 +18,9 @@
 namespace sm {
 namespace {
 
-constexpr int K_REC = 1, K_NODE = 2, K_LNODE = 3, K_FWD = 0xFF;
+constexpr int K_REC = 1, K_NODE = 2, K_LNODE = 3, K_LNODE4 = 4, K_FWD = 0xFF;
+// words of a heap object of kind k (K_LNODE4: a list node with its operand cache, DPre.ncache)
+#define SM_OBJ_WORDS(k) ((k) == K_REC ? PQ->rec_words : (k) == K_NODE ? PQ->node_words : (k) == K_LNODE4 ? 4 : 2)
 
 struct Lane;
 
@@ -101,6 +103,16 @@ struct TrialLoader {
   const Lane* L;
   int rec;
   int sid;
+  const int64_t* evr;
+  __device__ StackVal var(const Instr& in) const;
+};
+// A trial whose other-state operands come from the list node's cache (DPre.ncache, K_LNODE4): the partial's run record
+// and chain nodes are not read at all (one read of the node per rejected partial)
+struct CachedTrialLoader {
+  const Lane* L;
+  int32_t ln;
+  int sid;
+  int pre;
   const int64_t* evr;
   __device__ StackVal var(const Instr& in) const;
 };
@@ -299,9 +311,26 @@ struct Lane {
   __device__ int32_t ln_next(int32_t ln) const { return (int32_t)heap[ln + 1]; }
   __device__ void ln_set_next(int32_t ln, int32_t v) const { heap[ln + 1] = v; }
   __device__ bool lempty(int p, int w) const { return lhead(p, w) < 0; }
+  // the trial operands of pre q's filter for run record `rec`, read once when the partial joins q's list (DPre.ncache)
+  // into the K_LNODE4 node ln {hdr | nulls << 8, next, v0, v1}; returns the null bits for the header
+  __device__ int64_t cache_fill(int q, int32_t ln, int32_t rec) {
+    int64_t nb = 0;
+    StateLoader ld{this, rec};
+    for (int k = 0; k < PPRE[q].ncache; ++k) {
+      const StackVal v = ld.var(PCODE[PPRE[q].cacheIns[k]]);
+      heap[ln + 2 + k] = v.null ? 0 : v.i;
+      if (v.null) nb |= (int64_t)1 << (8 + k);
+    }
+    return nb;
+  }
+  // A node of a pre with a cache is K_LNODE4 from the start; its cache is filled when the node moves from the
+  // newAndEvery list to the pending list (lsplice, the only way a node reaches the list processAndReturn walks), so
+  // the fill has one call site instead of one per inlined append. Between the append and the splice nothing changes
+  // the cached states' chains (DPre.ncache).
   SM_INL_SMALL __device__ void lappend(int p, int w, int32_t rec) {
-    int32_t ln = alloc(2);
-    heap[ln] = K_LNODE | ((int64_t)(uint32_t)rec << 32);
+    const bool c4 = w < 2 && PPRE[p].ncache > 0;
+    int32_t ln = alloc(c4 ? 4 : 2);
+    heap[ln] = (c4 ? K_LNODE4 : K_LNODE) | ((int64_t)(uint32_t)rec << 32);
     heap[ln + 1] = -1;
     int32_t t = ltail(p, w);
     if (t < 0) lset(p, w, ln, ln);
@@ -319,6 +348,17 @@ struct Lane {
   __device__ void lsplice(int p, int dst, int src) {  // dst.addAll(src); src.clear()
     int32_t sh = lhead(p, src);
     if (sh < 0) return;
+    if (dst == 0) {  // newAndEvery -> pending: fill the operand caches of the arriving nodes (lappend)
+#ifdef SM_NFA_JIT_INLINE_ALL
+#pragma unroll
+      for (int q = 0; q < PQ->npre; ++q)
+        if (q == p && PPRE[q].ncache > 0)
+          for (int32_t x = sh; x >= 0; x = ln_next(x)) heap[x] |= cache_fill(q, x, ln_rec(x));
+#else
+      if (PPRE[p].ncache > 0)
+        for (int32_t x = sh; x >= 0; x = ln_next(x)) heap[x] |= cache_fill(p, x, ln_rec(x));
+#endif
+    }
     int32_t dt = ltail(p, dst);
     if (dt < 0) lset(p, dst, sh, ltail(p, src));
     else {
@@ -403,6 +443,24 @@ struct Lane {
     return truthy(eval_prog(PCODE + P.progOff, P.progLen, PCONSTS, ld));
 #endif
   }
+  // trial_pass with the other states' operands from the list node's cache (DPre.ncache > 0)
+  SM_JIT_INL __device__ bool trial_cached(int p, int32_t ln, const int64_t* evr) const {
+#ifdef SM_NFA_JIT_INLINE_ALL
+    bool pass = true;
+#pragma unroll
+    for (int q = 0; q < PQ->npre; ++q)
+      if (q == p && PPRE[q].progLen != 0 && PPRE[q].ncache > 0) {  // the only pres that call it
+        CachedTrialLoader ld{this, ln, PPRE[q].stateId, q, evr};
+        pass = truthy(eval_prog(PCODE + PPRE[q].progOff, PPRE[q].progLen, PCONSTS, ld));
+      }
+    return pass;
+#else
+    const DPre& P = PPRE[p];
+    if (P.progLen == 0) return true;
+    CachedTrialLoader ld{this, ln, P.stateId, p, evr};
+    return truthy(eval_prog(PCODE + P.progOff, P.progLen, PCONSTS, ld));
+#endif
+  }
   // filter_pass for a trialCur state with the incoming event in place of its own slot's CURRENT: nothing is added to
   // the partial, so a partial that fails costs only the loads of the other slots' values
   SM_JIT_INL __device__ bool trial_pass(int p, int32_t rec, const int64_t* evr) const {
@@ -410,7 +468,7 @@ struct Lane {
     bool pass = true;
 #pragma unroll
     for (int q = 0; q < PQ->npre; ++q)
-      if (q == p && PPRE[q].progLen != 0) {
+      if (q == p && PPRE[q].progLen != 0 && PPRE[q].ncache == 0) {  // pres with a cache use trial_cached
         TrialLoader ld{this, rec, PPRE[q].stateId, evr};
         pass = truthy(eval_prog(PCODE + PPRE[q].progOff, PPRE[q].progLen, PCONSTS, ld));
       }
@@ -712,7 +770,7 @@ struct Lane {
           if (trial) {
             bool pass;
             if (P.trialCur) {
-              pass = trial_pass(p, s, evr);
+              pass = P.ncache > 0 ? trial_cached(p, ln, evr) : trial_pass(p, s, evr);
               // the reference sets the slot to the event and back to null on a rejection: an every-copy that
               // arrived with the slot filled leaves it null
               if (!pass) set_slot(s, sid, -1);
@@ -767,16 +825,29 @@ struct Lane {
         int32_t prev = -1;
         const bool trial = P.progLen != 0;  // as for PK_STREAM: a failing partial keeps nothing of the event
         int32_t shared = -1;
+        // with an operand cache the trial comes first and the run record is read only for a partial that passes
+        // (lazy removal): a partial whose next state is already filled is removed by the first event that would
+        // otherwise act on it, and until then nothing reads it, so every output and list order is the reference's
+        const bool lazy = trial && P.trialCur && P.ncache > 0;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
           int32_t s = ln_rec(ln);
-          if ((PQ->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (PQ->nslots > sid + 2 && slot(s, sid + 2) >= 0)) {
+          auto next_filled = [&]() {
+            return (PQ->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (PQ->nslots > sid + 2 && slot(s, sid + 2) >= 0);
+          };
+          if (!lazy && next_filled()) {
             ln = lerase(p, 0, prev, ln);
             continue;
           }
           if (trial) {
             bool pass;
-            if (P.trialCur) {
+            if (lazy) {
+              pass = trial_cached(p, ln, evr);
+              if (pass && next_filled()) {
+                ln = lerase(p, 0, prev, ln);
+                continue;
+              }
+            } else if (P.trialCur) {
               pass = trial_pass(p, s, evr);
             } else {
               if (shared < 0) shared = copy_event(evr);
@@ -1103,7 +1174,7 @@ struct Lane {
     if (o < 0) return o;
     int k = kind_of(o);
     if (k == K_FWD) return hi(o);
-    int words = (k == K_REC) ? PQ->rec_words : (k == K_NODE) ? PQ->node_words : 2;
+    int words = SM_OBJ_WORDS(k);
     int32_t n = (int32_t)top;
     SM_COUNT(3, words);
     for (int w = 0; w < words; ++w) heap[n + w] = heap[o + w];
@@ -1121,7 +1192,7 @@ struct Lane {
     const int64_t h0 = heap[o];
     const int k = (int)(h0 & 0xFF);
     if (k == K_FWD) return (int32_t)(h0 >> 32);
-    const int words = (k == K_REC) ? PQ->rec_words : (k == K_NODE) ? PQ->node_words : 2;
+    const int words = SM_OBJ_WORDS(k);
     const int32_t n = (int32_t)top;
     SM_COUNT(3, words);
     for (int w = 0; w < words; ++w) dst[n + w] = heap[o + w];
@@ -1145,10 +1216,10 @@ struct Lane {
       const int32_t o = (int32_t)scan;
       const int64_t h0 = dst[o];
       const int k = (int)(h0 & 0xFF);
-      if (k == K_LNODE) {
+      if (k == K_LNODE || k == K_LNODE4) {
         dst[o] = with_hi(h0, fwd_to(hi_of(h0), top, dst));
         dst[o + 1] = fwd_to((int32_t)dst[o + 1], top, dst);
-        scan += 2;
+        scan += k == K_LNODE4 ? 4 : 2;
       } else if (k == K_REC) {
         for (int s = 0; s < PQ->nslots; ++s) {
           int64_t& w = dst[o + 2 + (s >> 1)];
@@ -1214,11 +1285,11 @@ struct Lane {
     while (scan < top) {
       int32_t o = (int32_t)scan;
       int k = kind_of(o);
-      if (k == K_LNODE) {
+      if (k == K_LNODE || k == K_LNODE4) {
         set_hi(o, fwd(hi(o), top));
         int32_t nx = (int32_t)heap[o + 1];
         heap[o + 1] = fwd(nx, top);
-        scan += 2;
+        scan += k == K_LNODE4 ? 4 : 2;
       } else if (k == K_REC) {
         for (int s = 0; s < PQ->nslots; ++s) set_slot(o, s, fwd(slot(o, s), top));
         scan += PQ->rec_words;
@@ -1337,6 +1408,24 @@ __device__ StackVal TrialLoader::var(const Instr& in) const {
   v.null = 0;
   if (in.t0 == T_FLOAT || in.t0 == T_DOUBLE) v.d = __longlong_as_double(w);
   else v.i = w;
+  return v;
+}
+
+__device__ StackVal CachedTrialLoader::var(const Instr& in) const {
+  if (in.a == sid) return TrialLoader{L, -1, sid, evr}.var(in);
+#ifdef SM_NFA_JIT
+  const DPre* PP = PPRE;
+  const Instr* PC = PCODE;
+#else
+  const DPre* PP = L->PPRE;
+  const Instr* PC = L->PCODE;
+#endif
+  // operand k of this pre's cache (DPre.cacheIns; plan constants in the query-specialised build)
+  const Instr& c0 = PC[PP[pre].cacheIns[0]];
+  const int k = (c0.op == in.op && c0.a == in.a && c0.b == in.b && c0.c == in.c) ? 0 : 1;
+  StackVal v;
+  v.i = L->heap[ln + 2 + k];
+  v.null = (int)((L->heap[ln] >> (8 + k)) & 1);
   return v;
 }
 

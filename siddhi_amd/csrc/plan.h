@@ -78,7 +78,12 @@ struct DPre {
   int32_t ksOff;             // first of its per-key state words (kPreWords, or kPreWordsAbsent for an absent pre)
   int32_t trialCur;          // 1: the filter reads its own state's chain only at CURRENT (the incoming event), so a
                              // partial can be tried against the incoming event without adding it to the chain
-  int32_t pad0;
+  // operand cache of the pending / newAndEvery list nodes (round 5): the filter's loads of other states (at most 2
+  // distinct (state, index, attribute) operands, each of an earlier single-event stream state, whose chain no longer
+  // changes once the partial reaches this state) are evaluated when a partial joins the list and kept in its node, so
+  // a trial reads the node only. cacheIns[k] = index into the code of a load of operand k; ncache 0 = none.
+  int32_t ncache;
+  int32_t cacheIns[2];
   int64_t waitingTime;       // absent: 'for' time, -1 when absent (logical 'and not X' without for)
 };
 
