@@ -529,13 +529,35 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
     const int64_t G = gridDim.x, q = G >> 3, r = G & 7, x = blk & 7, i = blk >> 3;
     blk = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
   }
-  for (int64_t tb = blk * kGT; tb < a.ntiles; tb += (int64_t)gridDim.x * kGT) {
-  const int64_t te = tb + kGT < a.ntiles ? tb + kGT : a.ntiles;
-  uint32_t ms = a.mt[tb * kBins + tid];
-  uint32_t tot;
-  (void)block_excl(ms, lw, &tot);
-  int64_t out = tot;  // matches whose j precedes the tile
-  for (int64_t t = tb; t < te; ++t) {
+  // SM_ORDER_XCD == 2: a cohort of kCoh XCD-consecutive workgroups (about the 32 an XCD runs at once) takes kCoh * kGT
+  // consecutive tiles, member m every kCoh-th of them: at each step the cohort orders kCoh adjacent tiles, whose
+  // shared segment lines its L2 fetches once, and each workgroup still orders kGT tiles
+  constexpr int64_t kCoh = 32;
+  const int64_t coh = blk / kCoh, mem = blk % kCoh;
+  // members of this cohort (the last one may be partial; the grid covers ntiles <= gridDim.x * kGT, so its members
+  // still reach every tile of its range in kGT steps)
+  const int64_t cw = (int64_t)gridDim.x - coh * kCoh < kCoh ? (int64_t)gridDim.x - coh * kCoh : kCoh;
+  auto tile_at = [&](int64_t base, int64_t k) {
+    return SM_ORDER_XCD == 2 ? coh * kCoh * kGT + mem + cw * k : base + k;
+  };
+  for (int64_t tb = SM_ORDER_XCD == 2 ? 0 : blk * kGT; tb < a.ntiles; tb += (int64_t)gridDim.x * kGT) {
+  const int64_t te = SM_ORDER_XCD == 2 ? kGT : (tb + kGT < a.ntiles ? tb + kGT : a.ntiles) - tb;
+  uint32_t ms = 0, tot = 0;
+  int64_t out = 0;  // matches whose j precedes the tile
+  if (SM_ORDER_XCD != 2) {
+    ms = a.mt[tb * kBins + tid];
+    (void)block_excl(ms, lw, &tot);
+    out = tot;
+  }
+  for (int64_t k = 0; k < te; ++k) {
+    const int64_t t = tile_at(tb, k);
+    if (t >= a.ntiles) break;
+    if (SM_ORDER_XCD == 2) {  // not the previous tile's successor: this tile's own prefix over the buckets
+      lds_barrier();          // lw's previous readers are done
+      ms = a.mt[t * kBins + tid];
+      (void)block_excl(ms, lw, &tot);
+      out = tot;
+    }
     const uint32_t me = a.mt[(t + 1) * kBins + tid];
     const uint32_t j0 = (uint32_t)(t << kTB);
     lds_barrier();  // previous tile's readers are done
