@@ -256,12 +256,21 @@ struct Lane {
     for (int w = 1; w < PQ->node_words; ++w) heap[n + w] = le_node(*b, r, w);
     return n;
   }
-  // StateEvent.addEvent :212-222
-  SM_INL_SMALL __device__ void add_event(int32_t r, int s, int32_t n) {
+  // StateEvent.addEvent :212-222; returns the chain's length afterwards (its last node is n), which the count post
+  // processor that runs right after it would otherwise walk the chain again for (post_process: chain_n)
+  SM_INL_SMALL __device__ int add_event(int32_t r, int s, int32_t n) {
     int32_t a = slot(r, s);
-    if (a < 0) { set_slot(r, s, n); return; }
-    while (nnext(a) >= 0) a = nnext(a);
+    if (a < 0) {
+      set_slot(r, s, n);
+      return 1;
+    }
+    int len = 2;
+    while (nnext(a) >= 0) {
+      a = nnext(a);
+      ++len;
+    }
     set_nnext(a, n);
+    return len;
   }
   // StateEvent.removeLastEvent :224-235
   SM_INL_SMALL __device__ void remove_last_event(int32_t r, int s) {
@@ -737,10 +746,10 @@ struct Lane {
   __device__ void count_startStateReset(int p) { setfl(p, F_START_RESET, true); }
 
   // StreamPreStateProcessor.process(StateEvent) :123-129 → FilterProcessor → post
-  SM_INL_PRE __device__ void pre_process(int p, int32_t r) {
+  SM_INL_PRE __device__ void pre_process(int p, int32_t r, int chain_n = 0, int32_t chain_last = -1) {
     setfl(p, F_STATE_CHANGED, false);
     if (!filter_pass(p, r)) return;
-    post_process(PPRE[p].post, r);
+    post_process(PPRE[p].post, r, chain_n, chain_last);
   }
 
   // processAndReturn of every pre kind; returned records are appended to the temporary list `ret`
@@ -866,16 +875,20 @@ struct Lane {
               }
               continue;
             }
+            int cn = 0;
+            int32_t cl = -1;
             if (P.trialCur) {
               if (shared < 0) shared = copy_event(evr);
-              add_event(s, sid, shared);
+              cn = add_event(s, sid, shared);
+              cl = shared;
             }
             shared = -1;  // the partial keeps the copy
-            post_process(P.post, s);  // pre_process after its filter
+            post_process(P.post, s, cn, cl);  // pre_process after its filter
           } else {
-            add_event(s, sid, copy_event(evr));
+            const int32_t ev = copy_event(evr);
+            const int cn = add_event(s, sid, ev);
             setfl(p, F_SUCCESS, false);
-            pre_process(p, s);
+            pre_process(p, s, cn, ev);
           }
           int tl = P.thisLast;
           if (returned(tl)) {
@@ -1025,16 +1038,24 @@ struct Lane {
     }
     return slot(r, P.stateId) >= 0;
   }
-  SM_JIT_INL __device__ void post_process(int o, int32_t r) {
+  // chain_n > 0: a count state's chain has just been appended to (add_event), its length and last node known
+  SM_JIT_INL __device__ void post_process(int o, int32_t r, int chain_n = 0, int32_t chain_last = -1) {
     const DPost& O = PPOST[o];
     switch (O.kind) {
       case PK_STREAM: stream_post(o, r); break;
       case PK_COUNT: {  // CountPostStateProcessor.process :45-71
-        int32_t e = slot(r, O.stateId);
-        int n = 1;
-        while (nnext(e) >= 0) {
-          ++n;
-          e = nnext(e);
+        int32_t e;
+        int n;
+        if (chain_n > 0) {
+          e = chain_last;
+          n = chain_n;
+        } else {
+          e = slot(r, O.stateId);
+          n = 1;
+          while (nnext(e) >= 0) {
+            ++n;
+            e = nnext(e);
+          }
         }
         setfl(O.thisPre, F_SUCCESS, true);
         rts(r) = nts(e);
