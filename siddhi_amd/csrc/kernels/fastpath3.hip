@@ -116,9 +116,7 @@ __device__ unsigned long long sm_stamps[16];
 // Tiles of kTile events (kItems per thread, every load of the tile issued before any is used).
 // EXTRA: an ordinal column or a LONG compared attribute is read too (without them, their registers are not held:
 // 134 -> fewer VGPRs, two workgroups per CU instead of one)
-// TS = false (round 5, the keyed bucket-stack batches of config 4): the event-time column is not read here; key pass 0
-// reads it anyway and checks its monotonicity there (OrigSrc::chk), so prep reads 4 B per event instead of 12
-template <typename KT, bool MASK, bool EXTRA, bool TS = true>
+template <typename KT, bool MASK, bool EXTRA>
 __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kcol, const int64_t* __restrict__ vlong,
                                                       const int64_t* __restrict__ ts, const int64_t* __restrict__ ord,
                                                       int64_t obase, int64_t n, int64_t per, int G,
@@ -143,15 +141,11 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
       const int64_t p = base + w * 64 * kItems + k * 64 + lane;
       if (p < hi0) {
         if (kcol) kk[k] = __builtin_nontemporal_load(kcol + p);
-        if (TS) tt[k] = __builtin_nontemporal_load(ts + p);
+        tt[k] = __builtin_nontemporal_load(ts + p);
         if (EXTRA && ord) oo[k] = ord[p];
         if (EXTRA && vlong) vv[k] = vlong[p];
-        if (!TS && lane == 0 && (p & 255) == 0 && p > 0) {  // lean: the pass-0 wave-block boundaries (OrigSrc::check)
-          tt[k] = ts[p];
-          tp[k] = ts[p - 1];
-        }
         if (lane == 0 && p > 0) {  // the element before each wave-item (other lanes take it from lane - 1)
-          if (TS) tp[k] = ts[p - 1];
+          tp[k] = ts[p - 1];
           if (EXTRA && ord) op[k] = ord[p - 1];
         }
       }
@@ -160,13 +154,9 @@ __global__ void __launch_bounds__(kBlock) prep_kernel(const KT* __restrict__ kco
     for (int k = 0; k < kItems; ++k) {
       const int64_t p = base + w * 64 * kItems + k * 64 + lane;
       const bool in = p < hi0;
-      if (TS) {
-        int64_t pt = __shfl_up(tt[k], 1, 64);
-        if (lane == 0) pt = p > 0 ? tp[k] : tt[k];
-        if (in && tt[k] < pt) bad = 1;
-      } else if (in && lane == 0 && (p & 255) == 0 && p > 0 && tt[k] < tp[k]) {
-        bad = 1;
-      }
+      int64_t pt = __shfl_up(tt[k], 1, 64);
+      if (lane == 0) pt = p > 0 ? tp[k] : tt[k];
+      if (in && tt[k] < pt) bad = 1;
       if (EXTRA && ord) {
         int64_t po = __shfl_up(oo[k], 1, 64);
         if (lane == 0) po = p > 0 ? op[k] : oo[k] - 1;
@@ -393,8 +383,6 @@ struct OrigSrc {
   const DVal* consts;
   bool c1_inline;
   Cond c1;
-  Ctrl* chk;  // non-null: prep did not read the event times (TS = false); pass 0 checks they do not decrease
-  bool bad = false;
   __device__ void init() {
     if (c1_inline) c1 = make_cond(c1code, c1len, consts);
   }
@@ -436,18 +424,6 @@ struct OrigSrc {
     r.m = c1_inline ? 0ull : c1mask[p >> 6];
     return r;
   }
-  // pass0_kernel, chk set: element p (wave-item k of a 256-event wave block) against element p - 1 from registers:
-  // lane - 1, or lane 63 of item k - 1 for lane 0. The first element of a wave block (p % 256 == 0) is checked by
-  // the lean prep instead (prep_kernel TS = false), so no load is added here. Reported once, at flush().
-  static_assert(kP0Items * 64 == 256 && kP0Tile % 256 == 0 && kTile % kP0Tile == 0,
-                "pass-0 wave blocks of 256 events on 256-aligned chunk tiles (the lean prep checks their boundaries)");
-  __device__ void check(const Raw& r, const Raw& rp, int k, bool valid) {
-    if (!chk) return;
-    int64_t pt = __shfl_up(r.t, 1, 64);
-    const int64_t p63 = __shfl(rp.t, 63, 64);
-    if ((threadIdx.x & 63) == 0) pt = k > 0 ? p63 : r.t;
-    bad |= valid && r.t < pt;
-  }
   __device__ void split(const Raw& r, int64_t p, uint64_t& a, uint64_t& b) const {
     const uint32_t c1 = c1_bit(r.v, r.m, p);
     a = (uint64_t)((uint32_t)((int64_t)r.k - kmin) | (c1 << 31)) | ((uint64_t)(uint32_t)r.o << 32);
@@ -458,9 +434,7 @@ struct OrigSrc {
     return make_uint4((uint32_t)((int64_t)r.k - kmin) | (c1 << 31), (uint32_t)r.o, vcode<VT>(r.v, vmode, vmin),
                       (uint32_t)(r.t - ts0));
   }
-  __device__ void flush() {
-    if (chk && __any(bad) && (threadIdx.x & 63) == 0) atomicOr(&chk->bad_ts, 1u);
-  }
+  __device__ void flush() {}
 };
 
 struct RecSrc {
@@ -1347,19 +1321,14 @@ bool c1_inline(const FastHostInfo& hi, const FastArgs& a) {
   return true;
 }
 
-// key pass 0 runs pass0_kernel (pass0_dev.h), which also checks the event times when prep did not (OrigSrc::chk)
-bool pass0_v2() {
-  static const bool p0v2 = !(getenv("SM_PASS0_V2") && getenv("SM_PASS0_V2")[0] == '0');
-  return sort_wc() && p0v2;
-}
-
 template <typename KT, typename VT>
 void launch_down0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int vmode, int64_t vmin,
                     const uint64_t* c1mask, int64_t ts0, int G, int64_t per, hipStream_t s, uint4* dst,
-                    const uint32_t* cnt, const uint32_t* dbase, Ctrl* chk) {
+                    const uint32_t* cnt, const uint32_t* dbase) {
   OrigSrc<KT, VT> os{a.st, (const KT*)kcol, (const VT*)hi.cols[hi.vattr], kmin, vmode, vmin, c1mask, a.ts, ts0,
-                     a.ordinals, a.ordinal_base, a.code + a.c1_off, a.c1_len, a.consts, c1_inline(hi, a), {}, chk};
-  if (pass0_v2())  // pass0_dev.h (A/B: SM_PASS0_V2=0 runs the generic write-combining down-sweep)
+                     a.ordinals, a.ordinal_base, a.code + a.c1_off, a.c1_len, a.consts, c1_inline(hi, a)};
+  static const bool p0v2 = !(getenv("SM_PASS0_V2") && getenv("SM_PASS0_V2")[0] == '0');
+  if (sort_wc() && p0v2)  // pass0_dev.h (A/B: SM_PASS0_V2=0 runs the generic write-combining down-sweep)
     hipLaunchKernelGGL((pass0_kernel<OrigSrc<KT, VT>>), dim3(G), dim3(kP0Block), 0, s, os, dst, a.n, per, G, cnt, dbase);
   else if (sort_wc())
     hipLaunchKernelGGL((downsweep_wc_kernel<0, OrigSrc<KT, VT>>), dim3(G), dim3(kWcBlock), 0, s, os, dst, nullptr, a.n,
@@ -1372,12 +1341,12 @@ void launch_down0_t(const FastHostInfo& hi, const FastArgs& a, const void* kcol,
 template <typename KT>
 void launch_down0_k(const FastHostInfo& hi, const FastArgs& a, const void* kcol, int64_t kmin, int vmode, int64_t vmin,
                     const uint64_t* m, int64_t ts0, int G, int64_t per, hipStream_t s, uint4* dst,
-                    const uint32_t* cnt, const uint32_t* dbase, Ctrl* chk) {
+                    const uint32_t* cnt, const uint32_t* dbase) {
   switch (hi.vtype) {
-    case T_INT: launch_down0_t<KT, int32_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase, chk); break;
-    case T_LONG: launch_down0_t<KT, int64_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase, chk); break;
-    case T_FLOAT: launch_down0_t<KT, float>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase, chk); break;
-    case T_DOUBLE: launch_down0_t<KT, double>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase, chk); break;
+    case T_INT: launch_down0_t<KT, int32_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_LONG: launch_down0_t<KT, int64_t>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_FLOAT: launch_down0_t<KT, float>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
+    case T_DOUBLE: launch_down0_t<KT, double>(hi, a, kcol, kmin, vmode, vmin, m, ts0, G, per, s, dst, cnt, dbase); break;
     default: throw std::runtime_error("fast path: unsupported compared-attribute type");
   }
 }
@@ -1639,22 +1608,15 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
 
   // column facts + c1 mask + pass-0 digit counts, one pass
   const bool mask = !keyed || !c1_inline(hi, a);
-  // lean prep (round 5): a keyed batch with c1 evaluated in pass 0 and no ordinal / LONG columns reads only its key
-  // column here (4 B per event instead of 12); key pass 0 (pass0_kernel) checks the event times it reads anyway.
-  // SM_LEAN_PREP=0: the full prep (A/B)
-  static const bool lean_env = !(getenv("SM_LEAN_PREP") && getenv("SM_LEAN_PREP")[0] == '0');
-  const bool lean = lean_env && keyed && !mask && !a.ordinals && !vlong && a.within >= 0 && pass0_v2();
-#define SM_PREP2(KT, M, X, T)                                                                                          \
-  hipLaunchKernelGGL((prep_kernel<KT, M, X, T>), dim3(G), dim3(kBlock), 0, s, (const KT*)kcol, vlong, a.ts,            \
-                     a.ordinals, a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt, c)
+#define SM_PREP2(KT, M, X)                                                                                          \
+  hipLaunchKernelGGL((prep_kernel<KT, M, X>), dim3(G), dim3(kBlock), 0, s, (const KT*)kcol, vlong, a.ts, a.ordinals, \
+                     a.ordinal_base, n, per, G, a.st, a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt, c)
 #define SM_PREP(KT, M)                  \
   do {                                  \
     if (a.ordinals || vlong)            \
-      SM_PREP2(KT, M, true, true);      \
-    else if (lean)                      \
-      SM_PREP2(KT, M, false, false);    \
+      SM_PREP2(KT, M, true);            \
     else                                \
-      SM_PREP2(KT, M, false, true);     \
+      SM_PREP2(KT, M, false);           \
   } while (0)
   if (key_type == T_LONG && keyed) {
     if (mask) SM_PREP(int64_t, true);
@@ -1664,35 +1626,18 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     else SM_PREP(int32_t, false);
   }
 #undef SM_PREP
+#undef SM_PREP2
   tmark("prep");
   Ctrl hc;
   SM_HIP(hipMemcpyAsync(&hc, c, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));
-  // lean prep did not look at the event times: before any early return whose reason ranks below a decreasing event
-  // time (the full prep reports FAST_NON_MONOTONE first), read them once (prep over the event-time column only)
-  auto settle_ts = [&]() {
-    if (!lean) return;
-    hipLaunchKernelGGL((prep_kernel<int32_t, false, false, true>), dim3(G), dim3(kBlock), 0, s, (const int32_t*)nullptr,
-                       (const int64_t*)nullptr, a.ts, (const int64_t*)nullptr, a.ordinal_base, n, per, G, a.st,
-                       a.code + a.c1_off, a.c1_len, a.consts, c1mask, cnt, c);  // no key column: event times only
-    SM_HIP(hipMemcpyAsync(&hc.bad_ts, &c->bad_ts, sizeof(hc.bad_ts), hipMemcpyDeviceToHost, s));
-    SM_HIP(hipStreamSynchronize(s));
-  };
-#undef SM_PREP2
   if (a.within >= 0) {
     // the closed form needs non-decreasing event time, inside the batch and after the carried state
     if (hc.bad_ts || (carry.active && hc.ts0 < carry.ts_last)) {
       sc.used = mark;
       return FAST_NON_MONOTONE;
     }
-    if ((unsigned long long)(hc.ts_last - hc.ts0) >= 0xffffffffull) {
-      settle_ts();
-      if (hc.bad_ts) {
-        sc.used = mark;
-        return FAST_NON_MONOTONE;
-      }
-      return bail();
-    }
+    if ((unsigned long long)(hc.ts_last - hc.ts0) >= 0xffffffffull) return bail();
   }
   if (hc.omax >= 0x7fffffffull || hc.bad_ord) return bail();
   int kbits = 0;
@@ -1704,9 +1649,8 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     kspan = (uint64_t)((int64_t)(hc.kmax ^ 0x8000000000000000ull) - kmin);
     kbits = std::max(1, bits_for(kspan));
     if (kbits > 30 || (hi.remap_span > 0 && kspan > (uint64_t)hi.remap_span)) {
-      settle_ts();
       sc.used = mark;
-      return hc.bad_ts ? FAST_NON_MONOTONE : FAST_KEY_SPAN;
+      return FAST_KEY_SPAN;
     }
   }
   // value code of the compared attribute
@@ -1770,18 +1714,9 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     // key pass 0 from the original columns (its digit counts came from prep)
     scan_counts(G);
     if (key_type == T_INT)
-      launch_down0_k<int32_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase, lean ? c : nullptr);
-    else launch_down0_k<int64_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase,
-                                 lean ? c : nullptr);
+      launch_down0_k<int32_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
+    else launch_down0_k<int64_t>(hi, a, kcol, kmin, vmode, vmin, c1mask, hc.ts0, G, per, s, A, cnt, dbase);
     tmark("key_pass0");
-    if (lean) {  // pass 0 checked the event times (OrigSrc::check): a decreasing one ends the closed form here
-      SM_HIP(hipMemcpyAsync(&hc.bad_ts, &c->bad_ts, sizeof(hc.bad_ts), hipMemcpyDeviceToHost, s));
-      SM_HIP(hipStreamSynchronize(s));
-      if (hc.bad_ts) {
-        sc.used = mark;
-        return FAST_NON_MONOTONE;
-      }
-    }
     // bucket-stack pipeline when the per-bucket keys fill a workgroup (stack.hip); it falls back here otherwise
     const int H = (int)std::min<uint64_t>(kspan >> kRB, 1ull << 20) + 1;
     const bool order_op = spec >= 0 && (spec >> 1) != CMP_EQ && (spec >> 1) != CMP_NE;

@@ -114,7 +114,6 @@ __global__ void __launch_bounds__(kP0Block) pass0_kernel(Src src, uint4* __restr
 #pragma unroll
     for (int k = 0; k < kP0Items; ++k) {
       const int e = w * 64 * kP0Items + k * 64 + lane;
-      src.check(raw[k], raw[k > 0 ? k - 1 : 0], k, e < tile_n);  // whole-wave (OrigSrc: event times)
       if (e < tile_n) rec[k] = src.record(raw[k], base + e);
     }
     // (the previous tile's readers of xb / tstart / run / cst / carry finished before its closing barrier)

@@ -256,10 +256,9 @@ def test_non_monotone_batch_hands_over_to_nfa(stack):
 
 @pytest.mark.parametrize("wide", [False, True])
 def test_non_monotone_first_batch_hands_over(wide):
-    """Round 5: the keyed closed form's prep no longer reads the event times (key pass 0 checks them). A first batch
-    whose times decrease must still reach the NFA with the reference's outputs, also when its keys span more than the
-    bucket-stack window (wide: the key-span answer must not win over the time check, so no dense ids are assigned to
-    a batch the closed form never takes)."""
+    """A first batch whose event times decrease reaches the NFA with the reference's outputs, also when its keys span
+    more than the bucket-stack window (wide: the time check ranks before the key-span answer, so no dense ids are
+    assigned to a batch the closed form never takes)."""
     n, K, div = 40000, 300, 5
     cols, ts = stock(n, K, div, key_dtype=np.int64)
     if wide:
@@ -273,8 +272,8 @@ def test_non_monotone_first_batch_hands_over(wide):
 
 @pytest.mark.parametrize("at", [8192, 8192 + 77, 255, 256, 4095, 37 * 256])
 def test_single_time_step_back_is_found(at):
-    """One event time lower than its predecessor's, at a pass-0 wave-block boundary (multiples of 256, checked by the
-    lean prep) or inside a block (checked by key pass 0): the batch goes to the NFA, outputs stay the reference's."""
+    """One event time lower than its predecessor's, at or off the prep kernel's wave-item and tile boundaries: the
+    batch goes to the NFA, outputs stay the reference's."""
     n, K, div = 20000, 100, 4
     cols, ts = stock(n, K, div)
     ts = ts.copy()
