@@ -439,6 +439,8 @@ def build_parser():
                     help="device-batch pipeline for configs 3/4: 0 automatic, 1 bucket stack, 2 sort / walk")
     ap.add_argument("--variant", default=None, choices=sorted(VARIANTS5),
                     help="config 5: the named emitting variant of the query")
+    ap.add_argument("--query5", default=None,
+                    help="config 5 diagnostic: this pattern / sequence body instead of the query (a side line only)")
     ap.add_argument("--ih-events", type=float, default=1e8,
                     help="config 4: events of the input-handler variant (host columns through sm_input_send_columns)")
     ap.add_argument("--via-input-handler", action="store_true",
@@ -477,6 +479,14 @@ def main():
         cfg["workload"] = f"config 5 variant {args.variant}: @app:playback partition with (symbol of A..E) " \
                           f"{VARIANTS5[args.variant]}"
         # a pattern keeps every A's partial until it completes (no `within`): a larger per-key arena
+        cfg["options"] = {"heap_words": 4096}
+    if args.query5:
+        if args.config != 5:
+            ap.error("--query5 applies to config 5")
+        cfg["app"] = app5_variant(args.query5).replace(
+            "select e1.timestamp as a, e2[0].timestamp as b0, e2[last].timestamp as bl, e3.timestamp as c, "
+            "e4.timestamp as d", "select e1.timestamp as a")
+        cfg["workload"] = f"config 5 diagnostic query: {args.query5}"
         cfg["options"] = {"heap_words": 4096}
 
     import torch

@@ -125,9 +125,19 @@ struct CachedTrialLoader {
 // [0] key-state word accesses, [1] heap word accesses, [2] words allocated, [3] words copied by collections
 // (gc + promote), [4] collections, [5] events delivered, [6] run records allocated, [7] chain nodes allocated
 extern int64_t g_access[8];
+// per phase of the lane's work (SM_PHASE): key-state / heap word accesses ([0][ph] / [1][ph])
+extern int g_phase;
+extern int64_t g_phase_acc[2][16];
+struct PhaseScope {
+  int prev;
+  explicit PhaseScope(int ph) : prev(g_phase) { g_phase = ph; }
+  ~PhaseScope() { g_phase = prev; }
+};
 #define SM_COUNT(i, v) (::sm::g_access[i] += (v))
+#define SM_PHASE(ph) ::sm::PhaseScope sm_phase_scope_(ph)
 #else
 #define SM_COUNT(i, v) ((void)0)
+#define SM_PHASE(ph) ((void)0)
 #endif
 struct LaneWords {
   int64_t* p;      // &base[lane]
@@ -135,6 +145,7 @@ struct LaneWords {
 #ifdef SM_COUNT_ACCESS  // CPU debug build only (tests/native): per-event access mix of key-state words vs heap words
   int64_t& operator[](int64_t w) const {
     ++g_access[stride == 1 ? 1 : 0];
+    ++g_phase_acc[stride == 1 ? 1 : 0][g_phase];
     return p[w * stride];
   }
 #else
@@ -518,6 +529,7 @@ struct Lane {
 
   // ------------------------------------------------------------ selector (QuerySelector.processNoGroupBy)
   SM_JIT_INL __device__ void emit(int32_t rec) {
+    SM_PHASE(12);
     if (PQ->having_len > 0) {  // QuerySelector.processNoGroupBy :138-139: the having condition drops the output
       StateLoader hl{this, rec};
       if (!truthy(eval_prog(PCODE + PQ->having_off, PQ->having_len, PCONSTS, hl))) return;
@@ -689,6 +701,7 @@ struct Lane {
   }
 
   SM_JIT_INL __device__ void updateState(int p) {
+    SM_PHASE(14);
     const DPre& P = PPRE[p];
     if (P.kind == PK_COUNT && fl(p, F_START_RESET)) {  // CountPreStateProcessor.updateState :145-151
       setfl(p, F_START_RESET, false);
@@ -755,6 +768,7 @@ struct Lane {
   // processAndReturn of every pre kind; returned records are appended to the temporary list `ret`
   // (the pre's list word 3: the selector runs after the loop, as in the receivers).
   SM_INL_PAR __device__ void processAndReturn(int p, const int64_t* __restrict__ evr, int64_t now) {
+    SM_PHASE(1 + p);
     const DPre& P = PPRE[p];
     const int sid = P.stateId;
     lclear(p, 3);
@@ -1323,6 +1337,7 @@ struct Lane {
     misc(1) = top;
   }
   SM_JIT_INL __device__ void safe_point() {
+    SM_PHASE(15);
     int64_t used = misc(1) - misc(2) * half;
     if (used * 2 > half) {
       gc();
@@ -1373,6 +1388,7 @@ struct Lane {
 
   // Playback listeners: every scheduler of this key drains its FIFO while head <= now (Scheduler.sendTimerEvents)
   SM_INL_FIRE __device__ void fire_all(int64_t now, int64_t at_pos, int64_t step_time) {
+    SM_PHASE(13);
     clock = now;
     for (int p = 0; p < PQ->npre; ++p) {
       if (!is_absent(p)) continue;

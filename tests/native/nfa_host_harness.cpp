@@ -340,10 +340,15 @@ void flush(HApp* a) {
 namespace sm {
 namespace {
 int64_t g_access[8];
+int g_phase;
+int64_t g_phase_acc[2][16];
 }
 }  // namespace sm
 extern "C" void h_access(int64_t* out) {
   for (int i = 0; i < 8; ++i) out[i] = sm::g_access[i];
+}
+extern "C" void h_access_phases(int64_t* out) {  // [kind][phase], kind 0 key-state, 1 heap
+  for (int i = 0; i < 32; ++i) out[i] = sm::g_phase_acc[i / 16][i % 16];
 }
 #endif
 

@@ -65,3 +65,11 @@ names = ["key-state word accesses", "heap word accesses", "words allocated", "wo
 print(f"N = {N:.0e}, key subsample sym % 1009 == 5: {n_ev} events, {n_hb} heartbeats, heap_half {half}")
 for k, name in enumerate(names):
     print(f"  {name:30s} {c[k]:12d}   {c[k] / max(n_ev, 1):8.2f} per event")
+ph = (ctypes.c_int64 * 32)()
+L.h_access_phases(ph)
+pn = {0: "other", 12: "emit (selector)", 13: "timers (fire_all)", 14: "updateState", 15: "safe point / gc"}
+print("  per phase (key-state / heap word accesses per event):")
+for k in range(16):
+    if ph[k] or ph[16 + k]:
+        name = pn.get(k, f"processAndReturn pre {k - 1}")
+        print(f"    {name:32s} {ph[k] / max(n_ev, 1):8.2f} {ph[16 + k] / max(n_ev, 1):8.2f}")
