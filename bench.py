@@ -441,6 +441,8 @@ def build_parser():
                     help="config 5: the named emitting variant of the query")
     ap.add_argument("--query5", default=None,
                     help="config 5 diagnostic: this pattern / sequence body instead of the query (a side line only)")
+    ap.add_argument("--select5", default="select e1.timestamp as a",
+                    help="config 5 diagnostic: the select clause of --query5")
     ap.add_argument("--ih-events", type=float, default=1e8,
                     help="config 4: events of the input-handler variant (host columns through sm_input_send_columns)")
     ap.add_argument("--via-input-handler", action="store_true",
@@ -485,7 +487,7 @@ def main():
             ap.error("--query5 applies to config 5")
         cfg["app"] = app5_variant(args.query5).replace(
             "select e1.timestamp as a, e2[0].timestamp as b0, e2[last].timestamp as bl, e3.timestamp as c, "
-            "e4.timestamp as d", "select e1.timestamp as a")
+            "e4.timestamp as d", args.select5)
         cfg["workload"] = f"config 5 diagnostic query: {args.query5}"
         cfg["options"] = {"heap_words": 4096}
 
