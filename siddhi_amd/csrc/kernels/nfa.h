@@ -56,6 +56,10 @@ struct NfaBatch {
   const int64_t* adv_upto;   // per record position: advance points at positions <= it (nullable)
   int64_t nadv;
   int64_t clock_in;          // clock before the batch
+  // clock index of the advance points (round 5; nullable): adv_cidx[c - adv_cmin] = the first advance point whose
+  // clock is >= c, for c in [adv_cmin, adv_cmin + adv_cspan), so a timer's due point is one load (timer_fire)
+  const int32_t* adv_cidx;
+  int64_t adv_cmin, adv_cspan;
   // this query's records grouped by key slot: key_pos[key_off[k] .. key_off[k+1]) ascending
   const int64_t* key_off;
   const int64_t* key_pos;
@@ -122,6 +126,9 @@ static_assert(sizeof(NfaStream) % 8 == 0, "stream descriptors are copied as 8-by
 // as many events each: a wave runs as long as its longest lane. perm must hold nkeys uint32.
 struct Scratch;
 void launch_lane_balance(const int64_t* key_off, int32_t nkeys, uint32_t* perm, Scratch& sc, hipStream_t s);
+// The clock index of a batch's advance points (NfaBatch::adv_cidx): idx[c] = first advance point whose clock is
+// >= cmin + c, for c in [0, span). One thread per clock value, a binary search over adv_clock (non-decreasing).
+void launch_clock_index(const int64_t* adv_clock, int64_t nadv, int64_t cmin, int64_t span, int32_t* idx, hipStream_t s);
 // Whether this batch's LaneEv records can take the compact form: node images of at most 8 words, positions and
 // advance points below 2^31, stream indices in int8, and the data events' ordinals within a 2^48 - 1 range (a
 // reduction over ev_ord; *ord_base = their minimum).

@@ -118,7 +118,28 @@ __global__ void lane_count_kernel(const int64_t* __restrict__ key_off, int32_t n
   slot[k] = (uint32_t)k;
 }
 
+__global__ void clock_index_kernel(const int64_t* __restrict__ clk, int64_t n, int64_t cmin, int64_t span,
+                                   int32_t* __restrict__ idx) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= span) return;
+  const int64_t x = cmin + c;
+  int64_t lo = 0, hi = n;  // first a with clk[a] >= x
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (clk[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  idx[c] = (int32_t)lo;
+}
+
 }  // namespace
+
+void launch_clock_index(const int64_t* adv_clock, int64_t nadv, int64_t cmin, int64_t span, int32_t* idx,
+                        hipStream_t s) {
+  if (span <= 0) return;
+  hipLaunchKernelGGL(clock_index_kernel, dim3((unsigned)((span + 255) / 256)), dim3(256), 0, s, adv_clock, nadv, cmin,
+                     span, idx);
+}
 
 void launch_lane_balance(const int64_t* key_off, int32_t nkeys, uint32_t* perm, Scratch& sc, hipStream_t s) {
   if (nkeys <= 0) return;

@@ -1594,7 +1594,18 @@ __device__ __forceinline__ int64_t adv_after(const NfaBatch& b, int64_t from, in
 #endif
 SM_TIMER_ATTR __device__ bool timer_fire(Lane& L, const NfaBatch& b, int64_t a1, int64_t t, int64_t next_pos,
                                          int64_t& search_from) {
-  const int64_t a2 = gallop<false>(b.adv_clock, search_from, b.nadv, t);
+  // the first advance point at or after search_from whose clock reaches t: one load of the clock index (the clock
+  // only moves forward, so it is the later of search_from and the first point overall); a gallop without the index.
+  // (The gallop was a chain of about 26 dependent loads per firing, which the lane's whole wave waits for: the
+  // emitting config-5 variant fires about 13 timers per key)
+  int64_t a2;
+  if (b.adv_cidx) {
+    const int64_t c = t - b.adv_cmin;
+    const int64_t g = c <= 0 ? 0 : (c >= b.adv_cspan ? b.nadv : (int64_t)b.adv_cidx[c]);
+    a2 = g > search_from ? g : search_from;
+  } else {
+    a2 = gallop<false>(b.adv_clock, search_from, b.nadv, t);
+  }
   const int64_t a = a1 < a2 ? a1 : a2;
   if (a >= b.nadv || b.adv_pos[a] > next_pos) {
     search_from = a;

@@ -1122,6 +1122,23 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.adv_upto = ev.adv_upto;
   b.nadv = ev.nadv;
   b.clock_in = ev.clock_in;
+  if (h.nsched > 0 && ev.nadv > 0 && ev.nadv < INT32_MAX) {
+    // timers: the clock index of the advance points (timer_fire finds a timer's due point with one load instead of a
+    // gallop), for a clock span of at most 2^26 values (256 MB of int32); wider spans keep the gallop
+    int64_t ends[2];
+    SM_HIP(hipMemcpyAsync(&ends[0], ev.adv_clock, 8, hipMemcpyDeviceToHost, hs));
+    SM_HIP(hipMemcpyAsync(&ends[1], ev.adv_clock + ev.nadv - 1, 8, hipMemcpyDeviceToHost, hs));
+    SM_HIP(hipStreamSynchronize(hs));
+    const int64_t span = ends[1] - ends[0] + 1;
+    static const bool cidx_on = !(getenv("SM_NFA_CLOCK_INDEX") && getenv("SM_NFA_CLOCK_INDEX")[0] == '0');
+    if (cidx_on && span > 0 && span <= ((int64_t)1 << 26) && a->sc.used + (size_t)span * 4 + (64 << 20) < a->sc.cap) {
+      int32_t* cidx = (int32_t*)a->sc.take((size_t)span * 4);
+      launch_clock_index(ev.adv_clock, ev.nadv, ends[0], span, cidx, hs);
+      b.adv_cidx = cidx;
+      b.adv_cmin = ends[0];
+      b.adv_cspan = span;
+    }
+  }
   b.key_off = key_off;
   b.key_pos = key_pos;
   b.lane_compact = lane_compact_ok(b, N, h.node_words, (int)a->ast.streams.size(), a->sc, hs, &b.lane_ord_base) ? 1 : 0;
