@@ -1685,9 +1685,6 @@ SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ 
 #endif
 }
 
-#ifndef SM_NFA_ROUNDS
-#define SM_NFA_ROUNDS 1  // A/B build flag: stream rounds in the lane loop (nfa_lane_run)
-#endif
 // A lane's event run (after its Lane is set up): lane creation, then its events in arrival order with the timers
 // due before each.
 SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key, int32_t* err_out) {
@@ -1736,31 +1733,6 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
   for (;;) {
     // this key's events are consecutive LaneEv records (key order): one contiguous read per event
     const int64_t* __restrict__ r = b.lane_ev + k * W;
-#if SM_NFA_ROUNDS && defined(__HIP_DEVICE_COMPILE__)
-    // Stream rounds: the lanes of a wave hold different keys, and each lane's next event may be of any stream, so one
-    // step of the wave ran every receiver's path that some lane needed, one after the other. Per round the wave now
-    // takes only the lanes whose next event comes from the stream most of its lanes wait on (ballot per receiver of
-    // the plan; `other` = markers, a stream no receiver reads, or the final timers after the last event); the others
-    // wait for a later round. Each lane still walks its own events in order, so the results are unchanged.
-    // (Simulated: 64 lanes x 100 events of 5 streams, 579 path runs per wave step by step, 353 in greedy rounds.)
-    {
-      int cand = PQ->nrecv;  // other
-      if (k < eend) {
-        const int st = le_stream(b, r);
-        for (int q = 0; q < PQ->nrecv; ++q)
-          if (PRECV[q].stream == st) cand = q;
-      }
-      int best = 0, bestn = -1;
-      for (int q = 0; q <= PQ->nrecv; ++q) {
-        const int c = __popcll(__ballot(cand == q));
-        if (c > bestn) {
-          bestn = c;
-          best = q;
-        }
-      }
-      if (cand != best) continue;
-    }
-#endif
     const int64_t next_pos = (k < eend) ? le_pos(b, r) : INT64_MAX;
     if (has_timers) {
       for (;;) {

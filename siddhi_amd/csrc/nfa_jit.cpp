@@ -110,7 +110,6 @@ std::string nfa_jit_source(const std::vector<char>& blob, bool lds, int compact)
   const char* e = getenv("SM_NFA_JIT_INLINE_ALL");
   if (!e || atoi(e)) src += "#define SM_NFA_JIT_INLINE_ALL 1\n";
   if (lds) src += "#define SM_NFA_LDS 1\n";
-  if (const char* r = getenv("SM_NFA_ROUNDS")) src += std::string("#define SM_NFA_ROUNDS ") + (atoi(r) ? "1" : "0") + "\n";
   if (compact >= 0) src += "#define SM_LANE_COMPACT_CONST " + std::to_string(compact ? 1 : 0) + "\n";
   src += blob_array(blob);
   src += kNfaJitBody;
