@@ -181,6 +181,10 @@ struct Lane {
   int32_t seq;
   int32_t err;
   int64_t clock;  // EventTimeBasedMillisTimestampGenerator.currentTime() as seen by this lane
+  // the earliest head of the lane's timer queues (min_head), INT64_MAX when all are empty: kept in a register, so the
+  // per-event "is a timer due" check reads no timer-queue word (they live in HBM); set at lane start, lowered by
+  // notifyAt when it gives an empty queue its head, recomputed after timers fire (round 5)
+  int64_t due;
 
   // ------------------------------------------------------------ heap
   // misc words: create position, heap bump, semispace, state-id counter, initialised. Staged (SM_NFA_LDS), they sit
@@ -425,12 +429,14 @@ struct Lane {
   __device__ LaneWords sq(int s) const { return ksh.at(PQ->ks_sched + s * (2 + kSchedCap)); }
   SM_JIT_INL __device__ void notifyAt(int s, int64_t t) {  // Scheduler.notifyAt :66-74
     LaneWords S = sq(s);
-    if (S[1] >= kSchedCap) {
+    const int64_t n = S[1];
+    if (n >= kSchedCap) {
       err |= NFA_ERR_TIMERS;
       return;
     }
-    S[2 + (S[0] + S[1]) % kSchedCap] = t;
-    S[1]++;
+    S[2 + (S[0] + n) % kSchedCap] = t;
+    S[1] = n + 1;
+    if (n == 0 && t < due) due = t;  // a new head (FIFO: a later entry never is one)
   }
   __device__ bool qempty(int s) const { return sq(s)[1] == 0; }
   __device__ int64_t qhead(int s) const {
@@ -1403,6 +1409,8 @@ struct Lane {
         absent_timer(p, t);
       }
     }
+    int64_t h;
+    due = min_head(h) ? h : INT64_MAX;
   }
   SM_JIT_INL __device__ bool min_head(int64_t& t) const {
     bool any = false;
@@ -1664,6 +1672,7 @@ SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ 
   L.err = 0;
   L.seq = 0;
   L.clock = b.clock_in;
+  L.due = INT64_MAX;
 
 #ifdef SM_NFA_LDS
   // LDS staging of the lane's per-key state words (north_star: "LDS staging of active partial matches per
@@ -1723,6 +1732,10 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
   if (ebeg == eend && !has_timers) {
     return;
   }
+  if (has_timers) {  // timers left by earlier batches (a lane created just now has only what pre_init scheduled)
+    int64_t h;
+    L.due = L.min_head(h) ? h : INT64_MAX;
+  }
   // Walk this key's events; before each, fire timers due at clock-advance points (playback) in order.
   // (Measured and not kept, round 5: greedy stream rounds, where per round a wave ran only the lanes whose next event
   // came from its most common receiver stream, to cut divergent path runs: emitting variant NFA 108.4 -> 120.8 ms,
@@ -1737,8 +1750,8 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
     if (has_timers) {
       for (;;) {
         if (L.err) break;
-        int64_t t;
-        if (!L.min_head(t)) break;
+        const int64_t t = L.due;  // the earliest timer (Lane::due, kept up to date by notifyAt / fire_all)
+        if (t == INT64_MAX) break;
         // first advance point at or after search_from whose position <= next_pos and (clock >= t or wall tick)
         // (both arrays are non-decreasing: positions ascend and the playback clock only moves forward)
         const int64_t a1 = adv_after(b, search_from, next_pos, k < eend ? le_upto(b, r) : -1);
