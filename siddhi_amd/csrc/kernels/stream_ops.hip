@@ -1215,7 +1215,9 @@ const char* order_outputs(const char* recs, int64_t n, uint32_t stride, const in
     uint64_t* kalt = k == k2 ? keys : k2;
     if (radix_sort_pairs<uint64_t>(k, kalt, cur, alt, (size_t)n, 0, bits, sc, s)) std::swap(cur, alt);
   };
-  pass(kc, 41, false);
+  // creation ordinals: batch-history ordinals within one app fit 41 bits; the multi-GPU merge (no ev_clock) sorts
+  // global ordinals, as wide as the trigger ordinals
+  pass(kc, ev_clock ? 41 : std::min(64, pos_bits + 1), false);
   if (hflag) pass(kt, 64, true);
   pass(kp, pos_bits + 1, true);  // batch positions < 2^32 (build_event_index); trigger ordinals: 63 bits
   const uint32_t words = stride / 8;
