@@ -130,6 +130,13 @@ struct DevOut {
   int64_t base;
   const int64_t* hw = nullptr;  // compact form: one 64-bit word per value ...
   const uint8_t* hn = nullptr;  // ... and one byte of null flags per output (bit a: value a)
+  // segments still in flight (round 5): outputs [seg_end[i-1], seg_end[i]) are in host memory once seg_ev[i] has
+  // completed, so deliver_direct prepares the Events of a segment while later segments cross PCIe; empty = all copied
+  std::vector<int64_t> seg_end;
+  std::vector<hipEvent_t> seg_ev;
+  void wait_all() const {
+    for (hipEvent_t e : seg_ev) SM_HIP(hipEventSynchronize(e));
+  }
 };
 
 struct Callback {
@@ -400,6 +407,23 @@ struct sm_app {
         if (b.p) (void)hipHostFree(b.p);
     }
   } out_arena;
+  // completion events of the output segments of the current call (DevOut::seg_ev), reused across calls
+  struct EvPool {
+    std::vector<hipEvent_t> evs;
+    size_t next = 0;
+    hipEvent_t take() {
+      if (next == evs.size()) {
+        hipEvent_t e;
+        SM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        evs.push_back(e);
+      }
+      return evs[next++];
+    }
+    void clear() { next = 0; }
+    ~EvPool() {
+      for (auto e : evs) (void)hipEventDestroy(e);
+    }
+  } out_events;
   // no JSON dump, no callback, no chaining: outputs are counted and stay in device memory, no HostOut is built
   bool outputs_unconsumed() const;
   bool need_outs = false;  // set while a caller reads the output records itself (nfa_device_batch)
@@ -413,6 +437,7 @@ struct sm_app {
   hipStream_t copy_stream = nullptr;
   std::vector<sm::DBuf> bulk[2];
   bool bulk_active = false;  // a bulk send is in progress (a callback's own large send is staged instead)
+  bool defer_outputs = false;  // device_outputs leaves its copies in flight (DevOut segments): bulk sends only
   // host-side time of the output path since the last reset (stat "host_ms:<phase>"): 0 device batches (including
   // 1), 1 device projections copied out as records, 2 deliver (ordering + Event preparation), 3 callbacks of bulk
   // sends, 4 bulk sends waiting for their next chunk's upload
@@ -1413,8 +1438,13 @@ void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<DevOut>& outs
   char* hvals = hb + (size_t)m * 8;  // DVal array, or words then null bytes
   q.proj_desc_dev.ensure(sizeof(NfaStream));
   SM_HIP(hipMemcpyAsync(q.proj_desc_dev.p, &q.proj_desc, sizeof(NfaStream), hipMemcpyHostToDevice, hs));
-  const int64_t chunk = std::min<int64_t>(m, (int64_t)1 << 22);
+  // deferred (bulk sends, round 5): segments of 2^20 outputs, each with a completion event instead of one final
+  // synchronisation, so that deliver_direct prepares the Events of a segment while the later ones are copied
+  const bool defer = a->defer_outputs;
+  const int64_t chunk = std::min<int64_t>(m, (int64_t)1 << (defer ? 20 : 22));
   q.proj_out.ensure((size_t)chunk * (vbytes + 8) + 16);
+  std::vector<int64_t> seg_end;
+  std::vector<hipEvent_t> seg_ev;
   int64_t* dts = (int64_t*)q.proj_out.p;
   char* dvals = (char*)q.proj_out.p + (size_t)chunk * 8;
   for (int64_t k0 = 0; k0 < m; k0 += chunk) {
@@ -1433,13 +1463,20 @@ void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<DevOut>& outs
                             hipMemcpyDeviceToHost, hs));
     }
     SM_HIP(hipMemcpyAsync(hts + k0, dts, (size_t)c * 8, hipMemcpyDeviceToHost, hs));
+    if (defer) {
+      seg_end.push_back(k0 + c);
+      seg_ev.push_back(a->out_events.take());
+      SM_HIP(hipEventRecord(seg_ev.back(), hs));
+    }
   }
-  SM_HIP(hipStreamSynchronize(hs));
+  if (!defer) SM_HIP(hipStreamSynchronize(hs));
   DevOut d{qi, m, hp, compact ? nullptr : (const DVal*)hvals, hts, rows, q.proj_base};
   if (compact) {
     d.hw = (const int64_t*)hvals;
     d.hn = (const uint8_t*)(hvals + (size_t)m * ns * 8);
   }
+  d.seg_end.swap(seg_end);
+  d.seg_ev.swap(seg_ev);
   outs.push_back(d);
   q.n_out += m;
   a->host_ms[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1502,42 +1539,60 @@ void deliver_direct(sm_app* a, const DevOut& d) {
   const int ns = cq.hdr.nsel;
   Pending& pd = a->pending;
   const std::array<int64_t, 3> at = query_callbacks(a, cq);
-  if (at[2] == 0) return;
+  if (at[2] == 0) {
+    d.wait_all();  // the copies in flight land in buffers the next call reuses
+    return;
+  }
   const size_t m = (size_t)d.m;
   auto trig = [&](size_t k) { return d.rows ? d.hp[k] : d.hp[2 * k + 1]; };
-  // chunk starts: counted per thread range, then written at their ranks
-  const size_t T = std::min<size_t>((size_t)host_threads(), std::max<size_t>(m >> 16, 1));
-  std::vector<size_t> cnt(T + 1, 0);
-  parallel_for(T, 1, [&](size_t lo, size_t hi) {
-    for (size_t t = lo; t < hi; ++t) {
-      size_t c = 0;
-      for (size_t k = m * t / T; k < m * (t + 1) / T; ++k) c += k == 0 || trig(k) != trig(k - 1);
-      cnt[t + 1] = c;
-    }
-  });
-  for (size_t t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
   const size_t c0 = pd.chunks.size(), e0 = pd.evs.size(), v0 = pd.vals.size();
-  pd.chunks.resize(c0 + cnt[T]);
   pd.evs.resize(e0 + m);
   pd.vals.resize(v0 + m * ns);
-  parallel_for(T, 1, [&](size_t lo, size_t hi) {
-    for (size_t t = lo; t < hi; ++t) {
-      size_t c = c0 + cnt[t];
-      const size_t kb = m * t / T, ke = m * (t + 1) / T;
-      for (size_t k = kb; k < ke; ++k) {
-        if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
-        else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
-        pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
-        if (k == 0 || trig(k) != trig(k - 1)) {
-          PreparedChunk& ch = pd.chunks[c++];
-          ch.cb_off = (uint32_t)at[0];
-          ch.n_cbs = (uint32_t)at[2];
-          ch.n_stream_cbs = (uint32_t)at[1];
-          ch.ev_off = e0 + k;
+  // segment by segment as their copies complete (DevOut::seg_ev; one segment when the copies were synchronised):
+  // chunk starts counted per thread range, then written at their ranks
+  auto segment = [&](size_t sb, size_t se) {
+    const size_t n = se - sb;
+    const size_t T = std::min<size_t>((size_t)host_threads(), std::max<size_t>(n >> 16, 1));
+    std::vector<size_t> cnt(T + 1, 0);
+    parallel_for(T, 1, [&](size_t lo, size_t hi) {
+      for (size_t t = lo; t < hi; ++t) {
+        size_t c = 0;
+        for (size_t k = sb + n * t / T; k < sb + n * (t + 1) / T; ++k) c += k == 0 || trig(k) != trig(k - 1);
+        cnt[t + 1] = c;
+      }
+    });
+    for (size_t t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+    const size_t cb = pd.chunks.size();
+    pd.chunks.resize(cb + cnt[T]);
+    parallel_for(T, 1, [&](size_t lo, size_t hi) {
+      for (size_t t = lo; t < hi; ++t) {
+        size_t c = cb + cnt[t];
+        const size_t kb = sb + n * t / T, ke = sb + n * (t + 1) / T;
+        for (size_t k = kb; k < ke; ++k) {
+          if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
+          else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
+          pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
+          if (k == 0 || trig(k) != trig(k - 1)) {
+            PreparedChunk& ch = pd.chunks[c++];
+            ch.cb_off = (uint32_t)at[0];
+            ch.n_cbs = (uint32_t)at[2];
+            ch.n_stream_cbs = (uint32_t)at[1];
+            ch.ev_off = e0 + k;
+          }
         }
       }
+    });
+  };
+  if (d.seg_end.empty()) {
+    segment(0, m);
+  } else {
+    size_t sb = 0;
+    for (size_t i = 0; i < d.seg_end.size(); ++i) {
+      SM_HIP(hipEventSynchronize(d.seg_ev[i]));  // outputs [sb, seg_end[i]) are on the host (and the pairs before)
+      segment(sb, (size_t)d.seg_end[i]);
+      sb = (size_t)d.seg_end[i];
     }
-  });
+  }
   const size_t nch = pd.chunks.size();
   parallel_for(nch - c0, (size_t)1 << 16, [&](size_t lo, size_t hi) {  // sizes and timestamps (the last event's)
     for (size_t c = c0 + lo; c < c0 + hi; ++c) {
@@ -2222,11 +2277,15 @@ void deliver_device(sm_app* a, std::vector<HostOut>& douts, std::vector<DevOut>&
     if (douts.empty() && draw.size() == 1 && !a->collect) {
       deliver_direct(a, draw[0]);
     } else {
-      for (const DevOut& d : draw) materialize(a, d, douts);
+      for (const DevOut& d : draw) {
+        d.wait_all();
+        materialize(a, d, douts);
+      }
       deliver(a, douts);
     }
   }
   a->out_arena.clear();
+  a->out_events.clear();
 }
 
 // Whether a host-API batch (the staged events of sm_input_send / sm_input_send_columns) can take the device-batch
@@ -2369,6 +2428,15 @@ int bulk_send_device(sm_app* a, int s, size_t n, const int64_t* ts, const void* 
         a->out_arena.clear();
         try {
           const auto td = clk::now();
+          // outputs cross PCIe in segments while the first ones become Events (DevOut::seg_ev, deliver_direct)
+          a->defer_outputs = true;
+          struct Undefer {
+            sm_app* a;
+            ~Undefer() {
+              if (a->defer_outputs) (void)hipStreamSynchronize(a->stream);  // no copy outlives the call
+              a->defer_outputs = false;
+            }
+          } undefer{a};
           device_batch_stream(a, s, len, (const int64_t*)a->bulk[b][nattr].p, dc.data(), nullptr, a->next_ordinal,
                               a->stream, douts, draw);
           a->host_ms[0] += ms_since(td);
