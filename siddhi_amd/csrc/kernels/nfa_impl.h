@@ -185,9 +185,6 @@ struct Lane {
   // per-event "is a timer due" check reads no timer-queue word (they live in HBM); set at lane start, lowered by
   // notifyAt when it gives an empty queue its head, recomputed after timers fire (round 5)
   int64_t due;
-  // event time of the event being delivered (deliver): a stream / logical / absent post processor's slot holds a
-  // copy of exactly that event, so its timestamp needs no read of the copy (round 5)
-  int64_t ev_now;
 
   // ------------------------------------------------------------ heap
   // misc words: create position, heap bump, semispace, state-id counter, initialised. Staged (SM_NFA_LDS), they sit
@@ -786,12 +783,10 @@ struct Lane {
       case PK_ABSENT_STREAM: {
         if (P.kind == PK_ABSENT_STREAM && !fl(p, F_ACTIVE)) return;
         int32_t prev = -1;
-        // One copy of the event serves every partial of this state (round 5). The reference clones the event per
-        // partial (StreamEventCloner.copyStreamEvent), but a single-event state's copy is never changed afterwards:
-        // its `next` stays null (only count states chain events) and no other field of a stream event is written
-        // again, so the clones are indistinguishable and sharing one is exact (the collector forwards a node
-        // reachable from several records once, as it does for shallow copies). A partial whose filter fails
-        // keeps nothing of the event.
+        // A partial whose filter fails keeps nothing of this event (its copy is garbage): the filter is tried
+        // against one copy of the event shared by the failing partials; the first partial that passes keeps that
+        // copy as its own (StreamEventCloner.copyStreamEvent: one clone per partial) and the next trial makes a
+        // fresh one.
         const bool trial = P.kind == PK_STREAM && P.progLen != 0;
         int32_t shared = -1;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
@@ -828,10 +823,10 @@ struct Lane {
             }
             if (shared < 0) shared = copy_event(evr);
             set_slot(s, sid, shared);
+            shared = -1;
             post_process(P.post, s);  // pre_process after its filter
           } else {
-            if (shared < 0) shared = copy_event(evr);
-            set_slot(s, sid, shared);
+            set_slot(s, sid, copy_event(evr));
             pre_process(p, s);
           }
           int tl = P.thisLast;
@@ -944,7 +939,7 @@ struct Lane {
         return;
       }
       case PK_LOGICAL: {  // LogicalPreStateProcessor.processAndReturn :125-163
-        int32_t prev = -1, shared = -1;
+        int32_t prev = -1;
         const int psid = PPRE[P.partner].stateId;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
@@ -957,8 +952,7 @@ struct Lane {
             ln = lerase(p, 0, prev, ln);
             continue;
           }
-          if (shared < 0) shared = copy_event(evr);  // one copy for every partial (PK_STREAM case above)
-          set_slot(s, sid, shared);
+          set_slot(s, sid, copy_event(evr));
           pre_process(p, s);
           int tl = P.thisLast;
           if (returned(tl)) {
@@ -980,7 +974,7 @@ struct Lane {
       }
       default: {  // PK_ABSENT_LOGICAL: AbsentLogicalPreStateProcessor.processAndReturn (always returns empty)
         if (!fl(p, F_ACTIVE)) return;
-        int32_t prev = -1, shared = -1;
+        int32_t prev = -1;
         const int psid = PPRE[P.partner].stateId;
         for (int32_t ln = lhead(p, 0); ln >= 0;) {
           if (err) return;
@@ -994,8 +988,7 @@ struct Lane {
             continue;
           }
           int32_t current = slot(s, sid);
-          if (shared < 0) shared = copy_event(evr);  // one copy for every partial (PK_STREAM case above)
-          set_slot(s, sid, shared);
+          set_slot(s, sid, copy_event(evr));
           pre_process(p, s);
           if (P.waitingTime != -1 || (P.sequence && P.ltype == LT_AND && PPOST[P.post].nextEveryPre >= 0))
             set_slot(s, sid, current);
@@ -1030,20 +1023,10 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ post-state processors
-  // the timestamp of the event in the slot a post processor reads: the delivered event (ev_now); the host build of
-  // this code checks that against the slot's copy on every call (tests/native: all KATs)
-  __device__ int64_t slot_ts_now(int32_t r, int sid) const {
-#if !defined(__HIP_DEVICE_COMPILE__) && !defined(SM_NFA_JIT)
-    if (nts(slot(r, sid)) != ev_now) __builtin_trap();
-#endif
-    (void)r;
-    (void)sid;
-    return ev_now;
-  }
   SM_JIT_INL __device__ void stream_post(int o, int32_t r) {  // StreamPostStateProcessor.process :53-72
     const DPost& O = PPOST[o];
     setfl(O.thisPre, F_STATE_CHANGED, true);
-    rts(r) = slot_ts_now(r, O.stateId);
+    rts(r) = nts(slot(r, O.stateId));
     if (O.hasNext) set_returned(o, 1);
     if (O.nextPre >= 0) addState(O.nextPre, r);
     if (O.nextEveryPre >= 0) addEveryState(O.nextEveryPre, r);
@@ -1122,12 +1105,12 @@ struct Lane {
       }
       case PK_ABSENT_STREAM: {  // AbsentStreamPostStateProcessor.process :36-55
         setfl(O.thisPre, F_STATE_CHANGED, true);
-        const int64_t se_ts = slot_ts_now(r, O.stateId);
-        rts(r) = se_ts;
+        int32_t se = slot(r, O.stateId);
+        rts(r) = nts(se);
         set_returned(o, 1);
         if (PPRE[O.thisPre].isStart && O.nextEveryPre >= 0 && O.nextEveryPre == O.thisPre)
           addEveryState(O.nextEveryPre, r);
-        lastArrival(O.thisPre) = se_ts;
+        lastArrival(O.thisPre) = nts(se);
         break;
       }
       default: {  // AbsentLogicalPostStateProcessor.process :37-50
@@ -1384,7 +1367,6 @@ struct Lane {
     phase = 1;
     sched = -1;
     int64_t now = le_node(*b, r, 1);
-    ev_now = now;
     // stabilizeStates
     if (PQ->kind == 2) {
       for (int k = 0; k < PQ->nreset; ++k) resetState(PQ->reset_seq[k]);  // inner reset(), flattened (plan.h)
