@@ -134,6 +134,7 @@ struct DevOut {
   // completed, so deliver_direct prepares the Events of a segment while later segments cross PCIe; empty = all copied
   std::vector<int64_t> seg_end;
   std::vector<hipEvent_t> seg_ev;
+  hipEvent_t pairs_ev = nullptr;  // the (e1, e2) tuples (hp) are on the host
   void wait_all() const {
     for (hipEvent_t e : seg_ev) SM_HIP(hipEventSynchronize(e));
   }
@@ -1428,6 +1429,11 @@ void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<DevOut>& outs
   const size_t np = (size_t)m * (rows ? 1 : 2);
   uint32_t* hp = (uint32_t*)a->out_arena.take(np * 4);
   SM_HIP(hipMemcpyAsync(hp, q.dev_pairs.p, np * 4, hipMemcpyDeviceToHost, hs));
+  hipEvent_t pairs_ev = nullptr;
+  if (a->defer_outputs) {
+    pairs_ev = a->out_events.take();
+    SM_HIP(hipEventRecord(pairs_ev, hs));
+  }
   // values, then timestamps: pinned, reused across calls (sm_app::out_arena), not zero-filled. Up to 8 select
   // values cross PCIe in the compact form (8 bytes per value + one byte of null flags per output instead of a
   // 16-byte DVal per value)
@@ -1477,6 +1483,7 @@ void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<DevOut>& outs
   }
   d.seg_end.swap(seg_end);
   d.seg_ev.swap(seg_ev);
+  d.pairs_ev = pairs_ev;
   outs.push_back(d);
   q.n_out += m;
   a->host_ms[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1548,51 +1555,48 @@ void deliver_direct(sm_app* a, const DevOut& d) {
   const size_t c0 = pd.chunks.size(), e0 = pd.evs.size(), v0 = pd.vals.size();
   pd.evs.resize(e0 + m);
   pd.vals.resize(v0 + m * ns);
-  // segment by segment as their copies complete (DevOut::seg_ev; one segment when the copies were synchronised):
-  // chunk starts counted per thread range, then written at their ranks
-  auto segment = [&](size_t sb, size_t se) {
-    const size_t n = se - sb;
-    const size_t T = std::min<size_t>((size_t)host_threads(), std::max<size_t>(n >> 16, 1));
-    std::vector<size_t> cnt(T + 1, 0);
-    parallel_for(T, 1, [&](size_t lo, size_t hi) {
-      for (size_t t = lo; t < hi; ++t) {
-        size_t c = 0;
-        for (size_t k = sb + n * t / T; k < sb + n * (t + 1) / T; ++k) c += k == 0 || trig(k) != trig(k - 1);
-        cnt[t + 1] = c;
-      }
-    });
-    for (size_t t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
-    const size_t cb = pd.chunks.size();
-    pd.chunks.resize(cb + cnt[T]);
-    parallel_for(T, 1, [&](size_t lo, size_t hi) {
-      for (size_t t = lo; t < hi; ++t) {
-        size_t c = cb + cnt[t];
-        const size_t kb = sb + n * t / T, ke = sb + n * (t + 1) / T;
-        for (size_t k = kb; k < ke; ++k) {
-          if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
-          else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
-          pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
-          if (k == 0 || trig(k) != trig(k - 1)) {
-            PreparedChunk& ch = pd.chunks[c++];
-            ch.cb_off = (uint32_t)at[0];
-            ch.n_cbs = (uint32_t)at[2];
-            ch.n_stream_cbs = (uint32_t)at[1];
-            ch.ev_off = e0 + k;
-          }
+  // chunk starts (one per trigger) from the tuples, which cross PCIe first: counted per thread range, then the
+  // Events written at their ranks; with deferred copies (DevOut segments) each thread waits only for the segments
+  // of its own range, so the Events of the first outputs are built while the later ones are still being copied
+  if (d.pairs_ev) SM_HIP(hipEventSynchronize(d.pairs_ev));
+  const size_t T = std::min<size_t>((size_t)host_threads(), std::max<size_t>(m >> 16, 1));
+  std::vector<size_t> cnt(T + 1, 0);
+  parallel_for(T, 1, [&](size_t lo, size_t hi) {
+    for (size_t t = lo; t < hi; ++t) {
+      size_t c = 0;
+      for (size_t k = m * t / T; k < m * (t + 1) / T; ++k) c += k == 0 || trig(k) != trig(k - 1);
+      cnt[t + 1] = c;
+    }
+  });
+  for (size_t t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+  pd.chunks.resize(c0 + cnt[T]);
+  parallel_for(T, 1, [&](size_t lo, size_t hi) {
+    for (size_t t = lo; t < hi; ++t) {
+      size_t c = c0 + cnt[t];
+      const size_t kb = m * t / T, ke = m * (t + 1) / T;
+      size_t ready = d.seg_end.empty() ? m : 0;  // outputs known to be on the host
+      for (size_t k = kb; k < ke; ++k) {
+        if (k >= ready) {
+          for (size_t i = 0; i < d.seg_end.size(); ++i)
+            if ((size_t)d.seg_end[i] > k) {
+              SM_HIP(hipEventSynchronize(d.seg_ev[i]));
+              ready = (size_t)d.seg_end[i];
+              break;
+            }
+        }
+        if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
+        else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
+        pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
+        if (k == 0 || trig(k) != trig(k - 1)) {
+          PreparedChunk& ch = pd.chunks[c++];
+          ch.cb_off = (uint32_t)at[0];
+          ch.n_cbs = (uint32_t)at[2];
+          ch.n_stream_cbs = (uint32_t)at[1];
+          ch.ev_off = e0 + k;
         }
       }
-    });
-  };
-  if (d.seg_end.empty()) {
-    segment(0, m);
-  } else {
-    size_t sb = 0;
-    for (size_t i = 0; i < d.seg_end.size(); ++i) {
-      SM_HIP(hipEventSynchronize(d.seg_ev[i]));  // outputs [sb, seg_end[i]) are on the host (and the pairs before)
-      segment(sb, (size_t)d.seg_end[i]);
-      sb = (size_t)d.seg_end[i];
     }
-  }
+  });
   const size_t nch = pd.chunks.size();
   parallel_for(nch - c0, (size_t)1 << 16, [&](size_t lo, size_t hi) {  // sizes and timestamps (the last event's)
     for (size_t c = c0 + lo; c < c0 + hi; ++c) {
