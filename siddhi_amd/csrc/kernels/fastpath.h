@@ -138,6 +138,11 @@ void build_carry(const int64_t* cand, int64_t ncand, const NfaStream* st, int na
 void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, const int64_t* ord, int64_t n,
                   int64_t base, const int64_t* ts, const int64_t* prev_carry, int64_t nc, int cw, const char* blob_dev,
                   DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s, bool rows = false,
-                  int64_t* words = nullptr, uint8_t* nulls = nullptr);  // words / nulls: compact form (nsel <= 8)
+                  int64_t* words = nullptr, uint8_t* nulls = nullptr,  // words / nulls: compact form (nsel <= 8)
+                  const uint32_t* carry_keys = nullptr, const uint32_t* carry_idx = nullptr, bool sync = true);
+// The carried partials' e1 ordinals sorted for pair_project (carry_keys / carry_idx, nc each, in sc): a caller
+// projecting one batch's outputs in several launches sorts them once (round 5: device_outputs' segments)
+void pair_project_carry_order(const int64_t* prev_carry, int64_t nc, int cw, int64_t base, Scratch& sc, hipStream_t s,
+                              const uint32_t** carry_keys, const uint32_t** carry_idx);
 
 }  // namespace sm

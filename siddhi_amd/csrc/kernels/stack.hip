@@ -1139,29 +1139,36 @@ __global__ void pair_project_kernel(const uint32_t* __restrict__ pairs, int64_t 
 }
 }  // namespace
 
+void pair_project_carry_order(const int64_t* prev_carry, int64_t nc, int cw, int64_t base, Scratch& sc, hipStream_t s,
+                              const uint32_t** carry_keys, const uint32_t** carry_idx) {
+  uint32_t* ck = (uint32_t*)sc.take((size_t)nc * 4);
+  uint32_t* ci = (uint32_t*)sc.take((size_t)nc * 4);
+  uint32_t* ck2 = (uint32_t*)sc.take((size_t)nc * 4);
+  uint32_t* ci2 = (uint32_t*)sc.take((size_t)nc * 4);
+  hipLaunchKernelGGL(carry_ord_keys_kernel, grid_of(nc), dim3(256), 0, s, prev_carry, nc, cw, base, ck, ci);
+  if (radix_sort_pairs<uint32_t>(ck, ck2, ci, ci2, (size_t)nc, 0, 32, sc, s)) {
+    ck = ck2;
+    ci = ci2;
+  }
+  *carry_keys = ck;
+  *carry_idx = ci;
+}
+
 void pair_project(const uint32_t* pairs, int64_t m, const NfaStream* st_dev, const int64_t* ord, int64_t n,
                   int64_t base, const int64_t* ts, const int64_t* prev_carry, int64_t nc, int cw, const char* blob_dev,
                   DVal* out, int64_t* ts_out, Scratch& sc, hipStream_t s, bool rows, int64_t* words,
-                  uint8_t* nulls) {
+                  uint8_t* nulls, const uint32_t* carry_keys, const uint32_t* carry_idx, bool sync) {
   if (m <= 0) return;
   const size_t mark = sc.used;
-  uint32_t *ck = nullptr, *ci = nullptr;
-  if (nc > 0 && !rows) {
-    ck = (uint32_t*)sc.take((size_t)nc * 4);
-    ci = (uint32_t*)sc.take((size_t)nc * 4);
-    uint32_t* ck2 = (uint32_t*)sc.take((size_t)nc * 4);
-    uint32_t* ci2 = (uint32_t*)sc.take((size_t)nc * 4);
-    hipLaunchKernelGGL(carry_ord_keys_kernel, grid_of(nc), dim3(256), 0, s, prev_carry, nc, cw, base, ck, ci);
-    if (radix_sort_pairs<uint32_t>(ck, ck2, ci, ci2, (size_t)nc, 0, 32, sc, s)) {
-      ck = ck2;
-      ci = ci2;
-    }
-  }
+  const uint32_t *ck = carry_keys, *ci = carry_idx;
+  if (nc > 0 && !rows && !ck) pair_project_carry_order(prev_carry, nc, cw, base, sc, s, &ck, &ci);
   hipLaunchKernelGGL(pair_project_kernel, grid_of(m), dim3(256), 0, s, pairs, m, st_dev, ord, n, base, ts, prev_carry,
                      cw, ck, ci, nc, blob_dev, rows, out, ts_out, words, nulls);
   SM_HIP(hipGetLastError());
-  SM_HIP(hipStreamSynchronize(s));
-  sc.used = mark;
+  if (sync) {
+    SM_HIP(hipStreamSynchronize(s));
+    sc.used = mark;
+  }
 }
 
 }  // namespace sm

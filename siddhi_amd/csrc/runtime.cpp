@@ -1453,14 +1453,23 @@ void device_outputs(sm_app* a, int qi, hipStream_t hs, std::vector<DevOut>& outs
   std::vector<hipEvent_t> seg_ev;
   int64_t* dts = (int64_t*)q.proj_out.p;
   char* dvals = (char*)q.proj_out.p + (size_t)chunk * 8;
+  // the carried partials' e1 order, once for every segment (pair_project_carry_order)
+  a->sc.used = 0;
+  const uint32_t *ck = nullptr, *ci = nullptr;
+  if (q.prev_carry_n > 0 && !rows)
+    pair_project_carry_order((const int64_t*)q.prev_carry.p, q.prev_carry_n, q.prev_carry_w, q.proj_base, a->sc, hs,
+                             &ck, &ci);
+  const size_t sc_base = a->sc.used;
   for (int64_t k0 = 0; k0 < m; k0 += chunk) {
     const int64_t c = std::min(chunk, m - k0);
-    a->sc.used = 0;
+    a->sc.used = sc_base;
     int64_t* dw = compact ? (int64_t*)dvals : nullptr;
     uint8_t* dn = compact ? (uint8_t*)(dvals + (size_t)chunk * ns * 8) : nullptr;
+    // stream order keeps segment k's copies ahead of segment k + 1's projection into the same device buffers
     pair_project((const uint32_t*)q.dev_pairs.p + (rows ? k0 : 2 * k0), c, (const NfaStream*)q.proj_desc_dev.p,
                  q.proj_ord, q.proj_n, q.proj_base, q.proj_ts, (const int64_t*)q.prev_carry.p, q.prev_carry_n,
-                 q.prev_carry_w, (const char*)q.blob.p, compact ? nullptr : (DVal*)dvals, dts, a->sc, hs, rows, dw, dn);
+                 q.prev_carry_w, (const char*)q.blob.p, compact ? nullptr : (DVal*)dvals, dts, a->sc, hs, rows, dw, dn,
+                 ck, ci, !defer);
     if (compact) {
       SM_HIP(hipMemcpyAsync(hvals + (size_t)k0 * ns * 8, dw, (size_t)c * ns * 8, hipMemcpyDeviceToHost, hs));
       SM_HIP(hipMemcpyAsync(hvals + (size_t)m * ns * 8 + k0, dn, (size_t)c, hipMemcpyDeviceToHost, hs));
