@@ -203,6 +203,12 @@ struct Pending {
   RawVec<sm_value> vals;
   std::vector<std::unique_ptr<std::string>> strs;  // owned STRING values (stable addresses)
   bool final_ = false;
+  // uniform form (round 5, deliver_direct): every chunk of the call goes to the same callbacks (proto's cb fields), so
+  // a chunk is only its first event's index (starts); its size is the distance to the next start and its timestamp
+  // the last event's. 8 bytes per chunk instead of a 40-byte PreparedChunk, written and then read by the callbacks.
+  bool uniform = false;
+  PreparedChunk proto;
+  RawVec<uint64_t> starts;
   void swap(Pending& o) {
     chunks.swap(o.chunks);
     cbs.swap(o.cbs);
@@ -210,6 +216,9 @@ struct Pending {
     vals.swap(o.vals);
     strs.swap(o.strs);
     std::swap(final_, o.final_);
+    std::swap(uniform, o.uniform);
+    std::swap(proto, o.proto);
+    starts.swap(o.starts);
   }
   void clear() {  // keeps the capacity (a bulk send reuses it chunk after chunk)
     chunks.clear();
@@ -218,6 +227,24 @@ struct Pending {
     vals.clear();
     strs.clear();
     final_ = false;
+    uniform = false;
+    starts.clear();
+  }
+  // the uniform form as PreparedChunks (before a general deliver appends chunks of other callbacks)
+  void expand() {
+    if (!uniform) return;
+    const size_t n = starts.size();
+    chunks.resize(n);
+    for (size_t c = 0; c < n; ++c) {
+      PreparedChunk ch = proto;
+      ch.ev_off = starts[c];
+      const size_t end = c + 1 < n ? starts[c + 1] : evs.size();
+      ch.n_ev = end - ch.ev_off;
+      ch.ts = evs[end - 1].timestamp;
+      chunks[c] = ch;
+    }
+    starts.clear();
+    uniform = false;
   }
   void finalise() {
     if (final_) return;
@@ -915,7 +942,10 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
       eoff[k] = (int64_t)nevs++;
       nvals += nsel;
     }
-    if (ch.n_cbs) pd.chunks.push_back(ch);
+    if (ch.n_cbs) {
+      pd.expand();
+      pd.chunks.push_back(ch);
+    }
     i = j;
   }
   pd.vals.resize(nvals);
@@ -945,7 +975,7 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
 // callback that throws (caught and logged, StreamCallback.java:92-99) is the binding's business: C callbacks
 // cannot throw across the ABI.
 void run_callbacks(Pending& out) {
-  if (out.chunks.empty()) return;
+  if (out.chunks.empty() && !(out.uniform && !out.starts.empty())) return;
   if (!out.final_) {  // Pending::finalise on the host threads
     sm_value* vals = out.vals.data();
     sm_event* evs = out.evs.data();
@@ -953,6 +983,21 @@ void run_callbacks(Pending& out) {
       for (size_t k = lo; k < hi; ++k) evs[k].data = vals + (uintptr_t)evs[k].data;
     });
     out.final_ = true;
+  }
+  if (out.uniform) {
+    const PreparedChunk& p = out.proto;
+    const size_t n = out.starts.size(), ne = out.evs.size();
+    const uint64_t* st = out.starts.data();
+    const sm_event* ev0 = out.evs.data();
+    for (size_t k = 0; k < n; ++k) {
+      const size_t b = st[k], e = k + 1 < n ? st[k + 1] : ne;
+      for (uint32_t c = 0; c < p.n_cbs; ++c) {
+        const Callback& cb = out.cbs[p.cb_off + c];
+        if (c < p.n_stream_cbs) cb.scb(cb.user, ev0 + b, e - b);
+        else cb.qcb(cb.user, ev0[e - 1].timestamp, ev0 + b, e - b, nullptr, 0);
+      }
+    }
+    return;
   }
   for (auto& ch : out.chunks) {
     const sm_event* evs = out.evs.data() + ch.ev_off;
@@ -1561,6 +1606,9 @@ void deliver_direct(sm_app* a, const DevOut& d) {
   }
   const size_t m = (size_t)d.m;
   auto trig = [&](size_t k) { return d.rows ? d.hp[k] : d.hp[2 * k + 1]; };
+  // the call's only outputs: the uniform chunk form (Pending::starts); otherwise PreparedChunks after what is there
+  const bool uni = pd.chunks.empty() && !pd.uniform && pd.evs.size() == 0;
+  if (!uni) pd.expand();
   const size_t c0 = pd.chunks.size(), e0 = pd.evs.size(), v0 = pd.vals.size();
   pd.evs.resize(e0 + m);
   pd.vals.resize(v0 + m * ns);
@@ -1578,7 +1626,16 @@ void deliver_direct(sm_app* a, const DevOut& d) {
     }
   });
   for (size_t t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
-  pd.chunks.resize(c0 + cnt[T]);
+  if (uni) {
+    pd.uniform = true;
+    pd.proto = PreparedChunk{};
+    pd.proto.cb_off = (uint32_t)at[0];
+    pd.proto.n_cbs = (uint32_t)at[2];
+    pd.proto.n_stream_cbs = (uint32_t)at[1];
+    pd.starts.resize(cnt[T]);
+  } else {
+    pd.chunks.resize(c0 + cnt[T]);
+  }
   parallel_for(T, 1, [&](size_t lo, size_t hi) {
     for (size_t t = lo; t < hi; ++t) {
       size_t c = c0 + cnt[t];
@@ -1597,6 +1654,10 @@ void deliver_direct(sm_app* a, const DevOut& d) {
         else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
         pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
         if (k == 0 || trig(k) != trig(k - 1)) {
+          if (uni) {
+            pd.starts[c++] = k;
+            continue;
+          }
           PreparedChunk& ch = pd.chunks[c++];
           ch.cb_off = (uint32_t)at[0];
           ch.n_cbs = (uint32_t)at[2];
@@ -1606,7 +1667,7 @@ void deliver_direct(sm_app* a, const DevOut& d) {
       }
     }
   });
-  const size_t nch = pd.chunks.size();
+  const size_t nch = uni ? c0 : pd.chunks.size();
   parallel_for(nch - c0, (size_t)1 << 16, [&](size_t lo, size_t hi) {  // sizes and timestamps (the last event's)
     for (size_t c = c0 + lo; c < c0 + hi; ++c) {
       PreparedChunk& ch = pd.chunks[c];
