@@ -115,3 +115,25 @@ def test_bench_two_ranks_report_the_one_stream():
     assert two["config"]["events"] == one["config"]["events"] == 2_000_000
     assert abs(two["value"] - 2e6 / (two["ms_per_step"] * 1e-3)) < 1e-6 * two["value"]
     assert one["config"]["rccl_world"] is None and two["config"]["rccl_world"] is None  # gloo rehearsal
+
+
+@pytest.mark.timeout(900)
+def test_bench_config5_two_ranks_merge_to_one_stream():
+    """bench.py --config 5 --gpus 2 (its own launcher, over gloo on the one GPU): the key exchange, the global clock
+    heartbeats (sm_merge_heartbeats) and the output merge (shard.merge_outputs / sm_order_outputs) inside the timed
+    step, with the HIP NFA kernel on each rank; the emitting variant must report the same output count as one rank."""
+    common = ["--config", "5", "--variant", "pattern_count_not5s", "--events", "3e5", "--keys", "3000", "--ts-div", "1",
+              "--steps", "1", "--warmup", "1", "--no-cpu"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    lines = []
+    for g, extra in ((1, {}), (2, {"SM_BENCH_BACKEND": "gloo"})):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(g)] + common,
+                           env={**env, **extra}, capture_output=True, text=True, timeout=800)
+        assert r.returncode == 0, r.stderr[-3000:]
+        js = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+        assert len(js) == 1
+        lines.append(js[0])
+    one, two = lines
+    assert two["n_gpus"] == 2 and two["config"]["events"] == one["config"]["events"] == 300_000
+    assert two["config"]["matches"] == one["config"]["matches"] > 100

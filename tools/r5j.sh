@@ -1,6 +1,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
-bash tools/step.sh j_hcf 900 python -u -m pytest tests/test_host_closed_form.py tests/test_device_callbacks.py tests/test_device_project.py -x -q --timeout 600 --timeout-method thread || exit 1
+bash tools/step.sh j_hcf 900 python -u -m pytest tests/test_host_closed_form.py tests/test_device_callbacks.py tests/test_device_project.py tests/test_callbacks.py -x -q --timeout 600 --timeout-method thread || exit 1
 timeout -k 10 500 python -u bench.py --no-cpu --no-e2e --no-sparse --steps 3 --warmup 1 > gpurun_out/j_ih.log 2>&1 || { tail -5 gpurun_out/j_ih.log; exit 1; }
 python3 -c "
 import json
