@@ -8,6 +8,7 @@
 // Outputs of all queries are ordered as the reference emits them (trigger position, timer phase, listener
 // order, query order, emission order) and delivered to StreamCallback / QueryCallback on the calling thread.
 #include <hip/hip_runtime.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <array>
@@ -233,6 +234,10 @@ struct Pending {
   // the uniform form as PreparedChunks (before a general deliver appends chunks of other callbacks)
   void expand() {
     if (!uniform) return;
+    if (final_) {  // deliver_direct's streamed form holds pointers already: offsets again, vals may grow
+      for (auto& e : evs) e.data = (const sm_value*)(uintptr_t)(e.data - vals.data());
+      final_ = false;
+    }
     const size_t n = starts.size();
     chunks.resize(n);
     for (size_t c = 0; c < n; ++c) {
@@ -989,6 +994,16 @@ void run_callbacks(Pending& out) {
     const size_t n = out.starts.size(), ne = out.evs.size();
     const uint64_t* st = out.starts.data();
     const sm_event* ev0 = out.evs.data();
+    if (p.n_cbs == 1 && p.n_stream_cbs == 1) {  // one StreamCallback (the common case): no per-chunk dispatch
+      const Callback& cb = out.cbs[p.cb_off];
+      const sm_stream_callback f = cb.scb;
+      void* const u = cb.user;
+      for (size_t k = 0; k < n; ++k) {
+        const size_t b = st[k], e = k + 1 < n ? st[k + 1] : ne;
+        f(u, ev0 + b, e - b);
+      }
+      return;
+    }
     for (size_t k = 0; k < n; ++k) {
       const size_t b = st[k], e = k + 1 < n ? st[k + 1] : ne;
       for (uint32_t c = 0; c < p.n_cbs; ++c) {
@@ -1626,6 +1641,18 @@ void deliver_direct(sm_app* a, const DevOut& d) {
     }
   });
   for (size_t t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+  bool strings = false;
+  for (int t : cq.sel_types) strings |= t == T_STRING;
+  // the streamed form: one query's compact values without strings are written with non-temporal stores (gigabytes
+  // of Events that the next accesses read from DRAM anyway: no read-for-ownership of every line), the events holding
+  // their final pointers (the call's vals do not grow again before the callbacks; Pending::expand undoes it)
+  const bool streamed = uni && d.hw && !strings && ns <= 8;
+  int64_t w0[8] = {0};
+  bool isf[8] = {false};
+  for (int j = 0; j < ns && streamed; ++j) {
+    w0[j] = (int64_t)(uint32_t)cq.sel_types[j];
+    isf[j] = cq.sel_types[j] == T_FLOAT || cq.sel_types[j] == T_DOUBLE;
+  }
   if (uni) {
     pd.uniform = true;
     pd.proto = PreparedChunk{};
@@ -1650,9 +1677,27 @@ void deliver_direct(sm_app* a, const DevOut& d) {
               break;
             }
         }
-        if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
-        else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
-        pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
+        if (streamed) {
+          sm_value* v = pd.vals.data() + v0 + k * ns;
+          long long* vw = (long long*)v;
+          const uint8_t nb = d.hn[k];
+          for (int j = 0; j < ns; ++j) {
+            const bool nul = (nb >> j) & 1;
+            const long long x = nul ? 0 : (long long)d.hw[k * ns + j];
+            _mm_stream_si64(vw + 4 * j, (long long)(w0[j] | ((int64_t)nul << 32)));  // type, is_null
+            _mm_stream_si64(vw + 4 * j + 1, isf[j] ? 0 : x);                        // i
+            _mm_stream_si64(vw + 4 * j + 2, isf[j] ? x : 0);                        // d (the double's bits)
+            _mm_stream_si64(vw + 4 * j + 3, 0);                                     // s
+          }
+          long long* ew = (long long*)(pd.evs.data() + e0 + k);
+          _mm_stream_si64(ew, (long long)d.hts[k]);
+          _mm_stream_si64(ew + 1, (long long)(uintptr_t)v);
+          _mm_stream_si64(ew + 2, (long long)(uint32_t)ns);
+        } else {
+          if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
+          else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
+          pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
+        }
         if (k == 0 || trig(k) != trig(k - 1)) {
           if (uni) {
             pd.starts[c++] = k;
@@ -1665,8 +1710,10 @@ void deliver_direct(sm_app* a, const DevOut& d) {
           ch.ev_off = e0 + k;
         }
       }
+      if (streamed) _mm_sfence();  // the streamed lines are visible before the callbacks read them
     }
   });
+  if (streamed) pd.final_ = true;
   const size_t nch = uni ? c0 : pd.chunks.size();
   parallel_for(nch - c0, (size_t)1 << 16, [&](size_t lo, size_t hi) {  // sizes and timestamps (the last event's)
     for (size_t c = c0 + lo; c < c0 + hi; ++c) {
@@ -1676,8 +1723,6 @@ void deliver_direct(sm_app* a, const DevOut& d) {
       ch.ts = pd.evs[end - 1].timestamp;
     }
   });
-  bool strings = false;
-  for (int t : cq.sel_types) strings |= t == T_STRING;
   if (strings)  // STRING values are owned by the pending outputs (the dictionary may change before the callbacks)
     for (size_t k = v0; k < pd.vals.size(); ++k) {
       sm_value& v = pd.vals[k];
