@@ -1627,20 +1627,23 @@ void deliver_direct(sm_app* a, const DevOut& d) {
   const size_t c0 = pd.chunks.size(), e0 = pd.evs.size(), v0 = pd.vals.size();
   pd.evs.resize(e0 + m);
   pd.vals.resize(v0 + m * ns);
-  // chunk starts (one per trigger) from the tuples, which cross PCIe first: counted per thread range, then the
-  // Events written at their ranks; with deferred copies (DevOut segments) each thread waits only for the segments
-  // of its own range, so the Events of the first outputs are built while the later ones are still being copied
+  // chunk starts (one per trigger) from the tuples, which cross PCIe first: counted per unit (a slice of the outputs),
+  // then the Events written at their ranks. With deferred copies (DevOut segments) every segment is cut into one unit
+  // per thread and thread t takes units t, t + T, ...: all threads build the Events of a segment as soon as it has
+  // landed, while the later segments are still being copied (a thread waits only for the segment of its next unit)
   if (d.pairs_ev) SM_HIP(hipEventSynchronize(d.pairs_ev));
   const size_t T = std::min<size_t>((size_t)host_threads(), std::max<size_t>(m >> 16, 1));
-  std::vector<size_t> cnt(T + 1, 0);
+  const size_t U = T * std::max<size_t>(d.seg_end.size(), 1);
+  std::vector<size_t> cnt(U + 1, 0);
   parallel_for(T, 1, [&](size_t lo, size_t hi) {
-    for (size_t t = lo; t < hi; ++t) {
-      size_t c = 0;
-      for (size_t k = m * t / T; k < m * (t + 1) / T; ++k) c += k == 0 || trig(k) != trig(k - 1);
-      cnt[t + 1] = c;
-    }
+    for (size_t t = lo; t < hi; ++t)
+      for (size_t u = t; u < U; u += T) {
+        size_t c = 0;
+        for (size_t k = m * u / U; k < m * (u + 1) / U; ++k) c += k == 0 || trig(k) != trig(k - 1);
+        cnt[u + 1] = c;
+      }
   });
-  for (size_t t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+  for (size_t u = 0; u < U; ++u) cnt[u + 1] += cnt[u];
   bool strings = false;
   for (int t : cq.sel_types) strings |= t == T_STRING;
   // the streamed form: one query's compact values without strings are written with non-temporal stores (gigabytes
@@ -1659,59 +1662,61 @@ void deliver_direct(sm_app* a, const DevOut& d) {
     pd.proto.cb_off = (uint32_t)at[0];
     pd.proto.n_cbs = (uint32_t)at[2];
     pd.proto.n_stream_cbs = (uint32_t)at[1];
-    pd.starts.resize(cnt[T]);
+    pd.starts.resize(cnt[U]);
   } else {
-    pd.chunks.resize(c0 + cnt[T]);
+    pd.chunks.resize(c0 + cnt[U]);
   }
   parallel_for(T, 1, [&](size_t lo, size_t hi) {
     for (size_t t = lo; t < hi; ++t) {
-      size_t c = c0 + cnt[t];
-      const size_t kb = m * t / T, ke = m * (t + 1) / T;
       size_t ready = d.seg_end.empty() ? m : 0;  // outputs known to be on the host
-      for (size_t k = kb; k < ke; ++k) {
-        if (k >= ready) {
-          for (size_t i = 0; i < d.seg_end.size(); ++i)
-            if ((size_t)d.seg_end[i] > k) {
-              SM_HIP(hipEventSynchronize(d.seg_ev[i]));
-              ready = (size_t)d.seg_end[i];
-              break;
+      for (size_t u = t; u < U; u += T) {
+        size_t c = c0 + cnt[u];
+        const size_t kb = m * u / U, ke = m * (u + 1) / U;
+        for (size_t k = kb; k < ke; ++k) {
+          if (k >= ready) {
+            for (size_t i = 0; i < d.seg_end.size(); ++i)
+              if ((size_t)d.seg_end[i] > k) {
+                SM_HIP(hipEventSynchronize(d.seg_ev[i]));
+                ready = (size_t)d.seg_end[i];
+                break;
+              }
+          }
+          if (streamed) {
+            sm_value* v = pd.vals.data() + v0 + k * ns;
+            long long* vw = (long long*)v;
+            const uint8_t nb = d.hn[k];
+            for (int j = 0; j < ns; ++j) {
+              const bool nul = (nb >> j) & 1;
+              const long long x = nul ? 0 : (long long)d.hw[k * ns + j];
+              _mm_stream_si64(vw + 4 * j, (long long)(w0[j] | ((int64_t)nul << 32)));  // type, is_null
+              _mm_stream_si64(vw + 4 * j + 1, isf[j] ? 0 : x);                        // i
+              _mm_stream_si64(vw + 4 * j + 2, isf[j] ? x : 0);                        // d (the double's bits)
+              _mm_stream_si64(vw + 4 * j + 3, 0);                                     // s
             }
-        }
-        if (streamed) {
-          sm_value* v = pd.vals.data() + v0 + k * ns;
-          long long* vw = (long long*)v;
-          const uint8_t nb = d.hn[k];
-          for (int j = 0; j < ns; ++j) {
-            const bool nul = (nb >> j) & 1;
-            const long long x = nul ? 0 : (long long)d.hw[k * ns + j];
-            _mm_stream_si64(vw + 4 * j, (long long)(w0[j] | ((int64_t)nul << 32)));  // type, is_null
-            _mm_stream_si64(vw + 4 * j + 1, isf[j] ? 0 : x);                        // i
-            _mm_stream_si64(vw + 4 * j + 2, isf[j] ? x : 0);                        // d (the double's bits)
-            _mm_stream_si64(vw + 4 * j + 3, 0);                                     // s
+            long long* ew = (long long*)(pd.evs.data() + e0 + k);
+            _mm_stream_si64(ew, (long long)d.hts[k]);
+            _mm_stream_si64(ew + 1, (long long)(uintptr_t)v);
+            _mm_stream_si64(ew + 2, (long long)(uint32_t)ns);
+          } else {
+            if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
+            else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
+            pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
           }
-          long long* ew = (long long*)(pd.evs.data() + e0 + k);
-          _mm_stream_si64(ew, (long long)d.hts[k]);
-          _mm_stream_si64(ew + 1, (long long)(uintptr_t)v);
-          _mm_stream_si64(ew + 2, (long long)(uint32_t)ns);
-        } else {
-          if (d.hw) to_sm_values_compact(a, d.hw + k * ns, d.hn[k], ns, cq, pd.vals.data() + v0 + k * ns);
-          else to_sm_values(a, d.hv + k * ns, ns, cq, pd.vals.data() + v0 + k * ns);
-          pd.evs[e0 + k] = sm_event{d.hts[k], (const sm_value*)(uintptr_t)(v0 + k * ns), (int32_t)ns};
-        }
-        if (k == 0 || trig(k) != trig(k - 1)) {
-          if (uni) {
-            pd.starts[c++] = k;
-            continue;
+          if (k == 0 || trig(k) != trig(k - 1)) {
+            if (uni) {
+              pd.starts[c++] = k;
+              continue;
+            }
+            PreparedChunk& ch = pd.chunks[c++];
+            ch.cb_off = (uint32_t)at[0];
+            ch.n_cbs = (uint32_t)at[2];
+            ch.n_stream_cbs = (uint32_t)at[1];
+            ch.ev_off = e0 + k;
           }
-          PreparedChunk& ch = pd.chunks[c++];
-          ch.cb_off = (uint32_t)at[0];
-          ch.n_cbs = (uint32_t)at[2];
-          ch.n_stream_cbs = (uint32_t)at[1];
-          ch.ev_off = e0 + k;
         }
       }
-      if (streamed) _mm_sfence();  // the streamed lines are visible before the callbacks read them
     }
+    if (streamed) _mm_sfence();  // the streamed lines are visible before the callbacks read them
   });
   if (streamed) pd.final_ = true;
   const size_t nch = uni ? c0 : pd.chunks.size();
