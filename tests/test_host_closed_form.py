@@ -156,6 +156,41 @@ def test_filter_and_pattern_bulk_interleave():
     assert got == [[r[0], r[1]] for r in exp]
 
 
+@pytest.mark.parametrize("reenter", [False, True])
+def test_bulk_host_gather_mixed_select(reenter):
+    """A bulk send whose select list mixes plain e1 / e2 attributes with expressions over both, in chunks of 33,333
+    events with partials carried between them. With `reenter` the callback sends an event into another stream during
+    the call, which takes an ordinal between two chunks. The Events equal the oracle's either way."""
+    import siddhi_amd
+    from siddhi_amd import SiddhiManager, StreamCallback
+    n, K, div = 200_000, 900, 10
+    cols, ts = stock(n, K, div)
+    sel = ("select e1.price * 2 as a, e2.symbol as s, e1.volume as v, e2.price + e1.price as d, e1.timestamp as i, "
+           "e2.timestamp as j")
+    pat = PAT.format(within=" within 1 sec")
+    pat = pat[:pat.index("select")] + sel + " insert into OutputStream;"
+    text = SCHEMA + "define stream Other (x int); " + part(pat)
+    exp = oracle_rows(text, cols, ts, "OutputStream")
+    calls = []
+    rt = SiddhiManager().createSiddhiAppRuntime(text)
+    ih_other = rt.getInputHandler("Other")
+
+    class SC(StreamCallback):
+        def receive(self, events):
+            if reenter and len(calls) == 0:
+                ih_other.send(int(events[0].timestamp), [7])
+            calls.append([[e.timestamp, e.data] for e in events])
+
+    for k, v in (("bulk_min", 1000), ("bulk_chunk", 33333)):
+        siddhi_amd.check(siddhi_amd.lib().sm_app_set_option(rt._h, k.encode(), v))
+    rt.addCallback("OutputStream", SC())
+    rt.start()
+    rt.getInputHandler("StockStream").send_columns(ts, cols)
+    rt.shutdown()
+    assert len(exp) > 1000
+    assert calls == chunks_of(exp, lambda r: r[1][5])
+
+
 def test_send_device_batch_validates_tensors():
     """SiddhiAppRuntime.sendDeviceBatch refuses tensors the device pipeline would misread: host
     tensors, int32 event times or ordinals, misaligned lengths, a column whose width is not its attribute's."""
