@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstring>
 #include <deque>
+#include <exception>
 #include <functional>
 #include <future>
 #include <limits>
@@ -763,11 +764,27 @@ void parallel_for(size_t n, size_t grain, F&& f) {
     f((size_t)0, n);
     return;
   }
+  // an exception in a worker (a failed HIP call while it waits for an output segment) is rethrown on the calling
+  // thread after every worker has joined, so the entry point reports it instead of the process terminating
+  std::vector<std::exception_ptr> err(t);
   std::vector<std::thread> th;
   th.reserve(t - 1);
-  for (size_t w = 1; w < t; ++w) th.emplace_back([&, w] { f(n * w / t, n * (w + 1) / t); });
-  f((size_t)0, n / t);
+  for (size_t w = 1; w < t; ++w)
+    th.emplace_back([&, w] {
+      try {
+        f(n * w / t, n * (w + 1) / t);
+      } catch (...) {
+        err[w] = std::current_exception();
+      }
+    });
+  try {
+    f((size_t)0, n / t);
+  } catch (...) {
+    err[0] = std::current_exception();
+  }
   for (auto& x : th) x.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
 }
 
 void to_sm_values(const sm_app* a, const DVal* vals, int nvals, const CompiledQuery& cq, sm_value* out) {
