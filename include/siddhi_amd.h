@@ -37,7 +37,9 @@
  *
  * Threading / delivery: an app handle is single-owner (calls are serialised internally). Events are
  * staged on send and processed on the GPU at sm_app_flush (also at shutdown and when the staging buffer
- * fills); callbacks run on the calling thread at that point, in the reference's emission order. Event
+ * fills); callbacks run on the calling thread at that point, in the reference's emission order (per output
+ * chunk the query's QueryCallbacks, then its output stream's StreamCallbacks: OutputRateLimiter.sendToCallBacks
+ * :61-73). Event
  * arrays passed to callbacks are valid only during the callback. Errors never cross the ABI as exceptions:
  * every call returns a status and sm_last_error() holds the thread-local message.
  */

@@ -187,11 +187,11 @@ struct RawVec {
 // One output chunk ready for the callbacks: the events one trigger (an input event or a scheduler firing) made
 // one query emit, delivered as one StreamCallback.receive(Event[]) (StreamCallback.java:65-76) and one
 // QueryCallback.receive(timestamp, in, removed) (QueryCallback.java:52-74). The chunks of one call share the arrays
-// of a Pending (no allocation per chunk or per event): its callbacks are cbs[cb_off, cb_off + n_cbs) (stream
-// callbacks of the output stream first, then query callbacks of the query), its events evs[ev_off, ev_off + n_ev).
+// of a Pending (no allocation per chunk or per event): its callbacks are cbs[cb_off, cb_off + n_cbs) (the query's
+// n_query_cbs QueryCallbacks first, then the output stream's StreamCallbacks), its events evs[ev_off, ev_off + n_ev).
 struct PreparedChunk {
   int64_t ts = 0;
-  uint32_t cb_off = 0, n_cbs = 0, n_stream_cbs = 0;
+  uint32_t cb_off = 0, n_cbs = 0, n_query_cbs = 0;
   uint64_t ev_off = 0, n_ev = 0;
 };
 
@@ -867,21 +867,24 @@ bool out_before(const OutRec& x, const OutRec& y) {
   return x.query < y.query;
 }
 
-// The callbacks of one query as a range of pd.cbs, appended once per delivery: [offset, stream callbacks, all].
+// The callbacks one output chunk of query cq goes to, in the reference's order: OutputRateLimiter.sendToCallBacks
+// (core/query/output/ratelimit/OutputRateLimiter.java:61-73) calls the query's QueryCallbacks first, then hands the
+// chunk to the output stream's junction, whose StreamCallbacks receive it. Returns {first index in pd.cbs, number of
+// QueryCallbacks, number of callbacks}.
 std::array<int64_t, 3> query_callbacks(sm_app* a, const CompiledQuery& cq) {
   Pending& pd = a->pending;
   std::array<int64_t, 3> at{(int64_t)pd.cbs.size(), 0, 0};
-  auto it = a->stream_cbs.find(cq.insert_into);
-  if (it != a->stream_cbs.end())
-    for (auto& cb : it->second)
-      if (cb.scb) pd.cbs.push_back(cb);
-  at[1] = (int64_t)pd.cbs.size() - at[0];
   if (cq.partition < 0) {  // partition clones do not inherit QueryCallbacks (PartitionRuntime)
     auto qt = a->query_cbs.find(cq.name);
     if (qt != a->query_cbs.end())
       for (auto& cb : qt->second)
         if (cb.qcb) pd.cbs.push_back(cb);
   }
+  at[1] = (int64_t)pd.cbs.size() - at[0];
+  auto it = a->stream_cbs.find(cq.insert_into);
+  if (it != a->stream_cbs.end())
+    for (auto& cb : it->second)
+      if (cb.scb) pd.cbs.push_back(cb);
   at[2] = (int64_t)pd.cbs.size() - at[0];
   return at;
 }
@@ -927,7 +930,7 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
     ch.ts = outs[j - 1].r.ts;  // QueryCallback.receiveStreamEvent: the chunk's last event's timestamp
     ch.cb_off = (uint32_t)at[0];
     ch.n_cbs = (uint32_t)at[2];
-    ch.n_stream_cbs = (uint32_t)at[1];
+    ch.n_query_cbs = (uint32_t)at[1];
     ch.ev_off = nevs;
     ch.n_ev = j - i;
     if (ch.n_cbs)
@@ -1011,7 +1014,7 @@ void run_callbacks(Pending& out) {
     const size_t n = out.starts.size(), ne = out.evs.size();
     const uint64_t* st = out.starts.data();
     const sm_event* ev0 = out.evs.data();
-    if (p.n_cbs == 1 && p.n_stream_cbs == 1) {  // one StreamCallback (the common case): no per-chunk dispatch
+    if (p.n_cbs == 1 && p.n_query_cbs == 0) {  // one StreamCallback (the common case): no per-chunk dispatch
       const Callback& cb = out.cbs[p.cb_off];
       const sm_stream_callback f = cb.scb;
       void* const u = cb.user;
@@ -1025,8 +1028,8 @@ void run_callbacks(Pending& out) {
       const size_t b = st[k], e = k + 1 < n ? st[k + 1] : ne;
       for (uint32_t c = 0; c < p.n_cbs; ++c) {
         const Callback& cb = out.cbs[p.cb_off + c];
-        if (c < p.n_stream_cbs) cb.scb(cb.user, ev0 + b, e - b);
-        else cb.qcb(cb.user, ev0[e - 1].timestamp, ev0 + b, e - b, nullptr, 0);
+        if (c < p.n_query_cbs) cb.qcb(cb.user, ev0[e - 1].timestamp, ev0 + b, e - b, nullptr, 0);
+        else cb.scb(cb.user, ev0 + b, e - b);
       }
     }
     return;
@@ -1035,8 +1038,8 @@ void run_callbacks(Pending& out) {
     const sm_event* evs = out.evs.data() + ch.ev_off;
     for (uint32_t c = 0; c < ch.n_cbs; ++c) {
       const Callback& cb = out.cbs[ch.cb_off + c];
-      if (c < ch.n_stream_cbs) cb.scb(cb.user, evs, ch.n_ev);
-      else cb.qcb(cb.user, ch.ts, evs, ch.n_ev, nullptr, 0);
+      if (c < ch.n_query_cbs) cb.qcb(cb.user, ch.ts, evs, ch.n_ev, nullptr, 0);
+      else cb.scb(cb.user, evs, ch.n_ev);
     }
   }
 }
@@ -1678,7 +1681,7 @@ void deliver_direct(sm_app* a, const DevOut& d) {
     pd.proto = PreparedChunk{};
     pd.proto.cb_off = (uint32_t)at[0];
     pd.proto.n_cbs = (uint32_t)at[2];
-    pd.proto.n_stream_cbs = (uint32_t)at[1];
+    pd.proto.n_query_cbs = (uint32_t)at[1];
     pd.starts.resize(cnt[U]);
   } else {
     pd.chunks.resize(c0 + cnt[U]);
@@ -1727,7 +1730,7 @@ void deliver_direct(sm_app* a, const DevOut& d) {
             PreparedChunk& ch = pd.chunks[c++];
             ch.cb_off = (uint32_t)at[0];
             ch.n_cbs = (uint32_t)at[2];
-            ch.n_stream_cbs = (uint32_t)at[1];
+            ch.n_query_cbs = (uint32_t)at[1];
             ch.ev_off = e0 + k;
           }
         }

@@ -191,6 +191,44 @@ def test_bulk_host_gather_mixed_select(reenter):
     assert calls == chunks_of(exp, lambda r: r[1][5])
 
 
+def test_bulk_send_stream_and_query_callbacks():
+    """An unpartitioned pattern with a StreamCallback on its output stream and a QueryCallback on the query: a bulk
+    send (chunks of 4,321 events) calls both per trigger, the QueryCallback first (with the chunk's last timestamp),
+    then the StreamCallback, as OutputRateLimiter.sendToCallBacks does (core/query/output/ratelimit/
+    OutputRateLimiter.java:61-73: query callbacks, then the output stream's junction), on the one-query direct path."""
+    import siddhi_amd
+    from siddhi_amd import QueryCallback, SiddhiManager, StreamCallback
+    n = 20000
+    cols, _ = stock(n, 10, 1, config=1)
+    ts = np.arange(n, dtype=np.int64)
+    text = SCHEMA + PAT.format(within=" within 1 sec")
+    exp = oracle_rows(text, cols, ts, "OutputStream")
+    calls = []
+
+    class SC(StreamCallback):
+        def receive(self, events):
+            calls.append(("s", [[e.timestamp, e.data] for e in events]))
+
+    class QC(QueryCallback):
+        def receive(self, timestamp, in_events, remove_events):
+            assert remove_events is None and timestamp == in_events[-1].timestamp
+            calls.append(("q", [[e.timestamp, e.data] for e in in_events]))
+
+    rt = SiddhiManager().createSiddhiAppRuntime(text)
+    for k, v in (("bulk_min", 1000), ("bulk_chunk", 4321)):
+        siddhi_amd.check(siddhi_amd.lib().sm_app_set_option(rt._h, k.encode(), v))
+    rt.addCallback("OutputStream", SC())
+    rt.addCallback("q", QC())
+    rt.start()
+    rt.getInputHandler("StockStream").send_columns(ts, cols)
+    rt.shutdown()
+    assert len(exp) > 1000
+    want = []
+    for c in chunks_of(exp, lambda r: r[1][5]):
+        want += [("q", c), ("s", c)]
+    assert calls == want
+
+
 def test_send_device_batch_validates_tensors():
     """SiddhiAppRuntime.sendDeviceBatch refuses tensors the device pipeline would misread: host
     tensors, int32 event times or ordinals, misaligned lengths, a column whose width is not its attribute's."""
