@@ -139,6 +139,52 @@ def test_one_call_per_output_chunk():
     rt.shutdown()
 
 
+@pytest.mark.parametrize("every", ["every ", ""])
+def test_query_callback_before_stream_callback(every):
+    """Per output chunk the query's QueryCallback runs before the output stream's StreamCallback
+    (OutputRateLimiter.sendToCallBacks core/query/output/ratelimit/OutputRateLimiter.java:61-73: query callbacks, then
+    the output callback into the stream's junction), on the host API path (closed form with `every`, NFA kernel
+    without; a filter query in front of the pattern)."""
+    S, rt = _rt(SCHEMA + "@info(name='f') from S[price > 45] select price insert into H; "
+                "@info(name='q') from " + every + "e1=S[price > 10] -> e2=S[price > e1.price] "
+                "select e1.price as p1, e2.price as p2 insert into O;")
+    calls = []
+
+    def sc(tag):
+        class SC(S.StreamCallback):
+            def receive(self, events):
+                calls.append((tag, [e.data for e in events]))
+        return SC()
+
+    def qc(tag):
+        class QC(S.QueryCallback):
+            def receive(self, ts, ins, rm):
+                calls.append((tag, [e.data for e in ins]))
+        return QC()
+
+    rt.addCallback("O", sc("O"))
+    rt.addCallback("H", sc("H"))
+    rt.addCallback("q", qc("q"))
+    rt.addCallback("f", qc("f"))
+    h = rt.getInputHandler("S")
+    rt.start()
+    for t, p in [(1, 50.0), (2, 40.0), (3, 30.0), (4, 60.0), (5, 70.0)]:
+        h.send(t, ["A", p, 1])
+    rt.flush()
+    rt.shutdown()
+    if every:
+        q4 = [[50.0, 60.0], [40.0, 60.0], [30.0, 60.0]]
+        q5 = [[60.0, 70.0]]
+    else:  # one partial (event 1's), completed by event 4
+        q4, q5 = [[50.0, 60.0]], None
+    want = [("f", [[50.0]]), ("H", [[50.0]]),   # event 1: the filter query's callbacks
+            ("f", [[60.0]]), ("H", [[60.0]]), ("q", q4), ("O", q4),  # event 4: filter first, then the pattern
+            ("f", [[70.0]]), ("H", [[70.0]])]
+    if q5:
+        want += [("q", q5), ("O", q5)]
+    assert calls == want
+
+
 def test_callback_may_send_into_the_same_app():
     """A callback that sends into the runtime it is called from (no deadlock); the nested send's outputs are
     delivered inside it, as the reference's synchronous junctions do."""
