@@ -321,37 +321,50 @@ def via_input_handler(cols_dev, n, expect, chunk=None):
     L = _lib.lib()
     host = [c[:n].cpu().numpy() for c in cols_dev]
     ts_h, cols_h = host[4], host[:4]
-    rt = SiddhiManager().createSiddhiAppRuntime(APP)
-    if chunk:
-        _lib.check(L.sm_app_set_option(rt._h, b"bulk_chunk", int(chunk)))
-    cnt = ct.c_int64(0)
-    cb = _lib.STREAM_CB(("sm_count_events_callback", L))
-    _lib.check(L.sm_app_add_stream_callback(rt._h, b"OutputStream", cb, ct.byref(cnt)))
-    ih = rt.getInputHandler("StockStream")
-    best = None
-    for _ in range(2):
-        _lib.check(L.sm_app_set_option(rt._h, b"reset", 1))
-        cnt.value = 0
-        t0 = time.perf_counter()
-        ih.send_columns(ts_h, cols_h)
-        dt = time.perf_counter() - t0
-        if cnt.value != expect:
-            raise RuntimeError(f"input-handler path delivered {cnt.value} output events, the device batch {expect}")
-        best = dt if best is None else min(best, dt)
-    path = ct.c_double()
-    _lib.check(L.sm_app_get_stat(rt._h, b"fast_path:q", ct.byref(path)))
-    phases = {}
-    for ph in ("device", "outputs", "deliver", "callbacks", "upload_wait"):  # host time of the last run, per phase
-        v = ct.c_double()
-        _lib.check(L.sm_app_get_stat(rt._h, f"host_ms:{ph}".encode(), ct.byref(v)))
-        phases[ph] = v.value
-    rt.shutdown()
-    del cb
+    def one(columns):
+        rt = SiddhiManager().createSiddhiAppRuntime(APP)
+        if chunk:
+            _lib.check(L.sm_app_set_option(rt._h, b"bulk_chunk", int(chunk)))
+        cnt = ct.c_int64(0)
+        if columns:  # the Event[] of each callback call as columns (sm_app_add_stream_columns_callback, round 6)
+            cb = _lib.COLUMNS_CB(("sm_count_columns_callback", L))
+            _lib.check(L.sm_app_add_stream_columns_callback(rt._h, b"OutputStream", cb, ct.byref(cnt)))
+        else:
+            cb = _lib.STREAM_CB(("sm_count_events_callback", L))
+            _lib.check(L.sm_app_add_stream_callback(rt._h, b"OutputStream", cb, ct.byref(cnt)))
+        ih = rt.getInputHandler("StockStream")
+        best = None
+        for _ in range(2):
+            _lib.check(L.sm_app_set_option(rt._h, b"reset", 1))
+            cnt.value = 0
+            t0 = time.perf_counter()
+            ih.send_columns(ts_h, cols_h)
+            dt = time.perf_counter() - t0
+            if cnt.value != expect:
+                raise RuntimeError(f"input-handler path delivered {cnt.value} output events, the device batch {expect}")
+            best = dt if best is None else min(best, dt)
+        path = ct.c_double()
+        _lib.check(L.sm_app_get_stat(rt._h, b"fast_path:q", ct.byref(path)))
+        phases = {}
+        for ph in ("device", "outputs", "deliver", "callbacks", "upload_wait"):  # host time of the last run, per phase
+            v = ct.c_double()
+            _lib.check(L.sm_app_get_stat(rt._h, f"host_ms:{ph}".encode(), ct.byref(v)))
+            phases[ph] = v.value
+        rt.shutdown()
+        del cb
+        return best, int(path.value), phases
+
+    best, path, phases = one(True)
+    ev_best, _, ev_phases = one(False)
     return {"events": n, "value": n / best, "unit": "events/s", "ms": best * 1e3, "output_events": expect,
-            "fast_path": int(path.value), "host_bytes_per_event": 36, "host_ms_last_run": phases,
+            "fast_path": path, "host_bytes_per_event": 36, "host_ms_last_run": phases,
+            "callback": "columns StreamCallback (sm_app_add_stream_columns_callback: each call's Event[] as columns)",
+            "events_form": {"value": n / ev_best, "ms": ev_best * 1e3, "host_ms_last_run": ev_phases,
+                            "callback": "sm_event StreamCallback (sm_app_add_stream_callback)"},
             "note": "host columns -> sm_input_send_columns (InputHandler.send(Event[])) -> bucket-stack closed form in "
-                    "chunks (H2D of the next chunk overlapped) -> StreamCallback counting every output Event; "
-                    "best of 2, fresh runtime each"}
+                    "chunks (H2D of the next chunk overlapped) -> StreamCallback counting every output Event (value: "
+                    "the columns form; events_form: Events as sm_event / sm_value records); best of 2, fresh runtime "
+                    "each"}
 
 
 def launch_command(gpus, argv, env, port=None):
@@ -537,7 +550,11 @@ def main():
     torch.cuda.synchronize()
 
     opts = dict(cfg.get("options", {}))
-    if args.config == 5 and world > 1:
+    # test only (tests/test_exchange_gpu.py, tools/rehearse_world4.sh): SM_BENCH_DUMP=<prefix> saves config 5's output
+    # records of the last step, this rank's part of the delivery order, to <prefix>.rank<r>.pt (outside the timing)
+    dump = os.environ.get("SM_BENCH_DUMP") if args.config == 5 else None
+    last_recs = [None]
+    if args.config == 5 and (world > 1 or dump):
         opts["keep_outputs"] = 1  # the output records of each batch stay on the device for the cross-rank merge
     if args.heap_words:
         opts["heap_words"] = args.heap_words
@@ -568,7 +585,12 @@ def main():
             if world > 1:
                 # the reference's single output order across ranks (shard.merge_outputs): every output record to the
                 # rank that ingested its trigger, ordered there (timers of one clock advance in key creation order)
-                out_local[0] = merge_outputs(app.copy_device_outputs("q"), starts, N, world).shape[0]
+                merged = merge_outputs(app.copy_device_outputs("q"), starts, N, world)
+                out_local[0] = merged.shape[0]
+                if dump:
+                    last_recs[0] = merged
+            elif dump:
+                last_recs[0] = app.copy_device_outputs("q")
             return int(app.get_stat("output_events:q"))
         # a fresh runtime of the app per step: the query's open partials (carried across device batches) dropped
         app.set_option("reset", 0)
@@ -635,6 +657,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if dump and last_recs[0] is not None:
+        torch.save(last_recs[0].cpu(), f"{dump}.rank{rank}.pt")
     path = app.get_stat("fast_path:q")
     nfa_kernel = int(app.get_stat("nfa_kernel:q")) if args.config == 5 else 0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)

@@ -10,6 +10,7 @@
  *   sm_app_add_stream_callback      SiddhiAppRuntime.addCallback(String, StreamCallback)  :243
  *   sm_count_events_callback        the counting StreamCallback of the reference's performance samples
  *   sm_app_add_query_callback       SiddhiAppRuntime.addCallback(String, QueryCallback)   :254
+ *   sm_app_add_stream_columns_callback  SiddhiAppRuntime.addCallback(String, StreamCallback), Event[] as columns
  *   sm_app_start / sm_app_shutdown  SiddhiAppRuntime.start / shutdown       :353 / :396
  *   sm_app_advance_time             @app:playback heartbeat (EventTimeBasedMillisTimestampGenerator.java:99)
  *   sm_app_process_device_batch     StreamJunction.sendData over a device-resident columnar batch (no Java
@@ -83,6 +84,12 @@ typedef struct sm_app sm_app;
 typedef struct sm_input sm_input;
 
 typedef void (*sm_stream_callback)(void* user, const sm_event* events, size_t n);
+/* A StreamCallback taking its Event[] as columns (round 6): n events, ts[k] the timestamp of event k, values[k * nsel +
+ * a] its attribute a as an 8-byte word (INT / LONG / BOOL as the integer, FLOAT / DOUBLE as the double's bits, FLOAT
+ * widened), bit a of null_bits[k] set when that attribute is null. The same chunks, in the same order and among the
+ * same other callbacks as sm_stream_callback receives them; the arrays are valid during the call only. */
+typedef void (*sm_stream_columns_callback)(void* user, size_t n, const int64_t* ts, const int64_t* values,
+                                           const uint8_t* null_bits, int32_t nsel);
 typedef void (*sm_query_callback)(void* user, int64_t timestamp, const sm_event* in_events, size_t n_in,
                                   const sm_event* removed_events, size_t n_removed);
 
@@ -134,6 +141,15 @@ int sm_app_add_stream_callback(sm_app* app, const char* stream_id, sm_stream_cal
  * StreamCallback of the reference's performance samples, e.g. PartitionPerformance.java). */
 void sm_count_events_callback(void* user, const sm_event* events, size_t n);
 int sm_app_add_query_callback(sm_app* app, const char* query_name, sm_query_callback cb, void* user);
+/* StreamCallback.receive(Event[]) (stream/output/StreamCallback.java:65-76) in the columns form above, for output streams
+ * of at most 8 attributes and none STRING (SM_E_UNSUPPORTED otherwise). When every callback of a query's outputs takes
+ * columns, the outputs of the device-batch pipelines reach them as views of the outputs' host copies: no per-Event
+ * record is written (8 bytes per value and one null byte per event, against a 24-byte sm_event and a 32-byte sm_value
+ * per value). */
+int sm_app_add_stream_columns_callback(sm_app* app, const char* stream_id, sm_stream_columns_callback cb, void* user);
+/* The counting callback in the columns form: adds n to the int64 `user` points at. */
+void sm_count_columns_callback(void* user, size_t n, const int64_t* ts, const int64_t* values, const uint8_t* null_bits,
+                               int32_t nsel);
 
 /* Parity/diagnostics: collect every output as JSON
  * {"streams": {"<id>": [[ts, [values], [refs]], ...]}, "queries": {"<name>": [[ts, [[values]...]], ...]}}

@@ -51,6 +51,15 @@ class StreamCallback:
         raise NotImplementedError
 
 
+class ColumnsStreamCallback(StreamCallback):
+    """A StreamCallback taking each chunk as columns (sm_app_add_stream_columns_callback): override
+    receive_columns(timestamps, values, null_bits), values[k][a] the 8-byte word of attribute a of event k (FLOAT /
+    DOUBLE as the double's bits)."""
+
+    def receive_columns(self, timestamps, values, null_bits):
+        raise NotImplementedError
+
+
 class QueryCallback:
     """Subclass and override receive(timestamp, in_events, remove_events)."""
 
@@ -177,7 +186,13 @@ class SiddhiAppRuntime:
         return [types[k] for k in range(n.value)]
 
     def addCallback(self, name, callback):
-        if isinstance(callback, StreamCallback):
+        if isinstance(callback, ColumnsStreamCallback):
+            def tramp(user, n, ts, vals, nb, ns, cb=callback):
+                cb.receive_columns([ts[k] for k in range(n)], [[vals[k * ns + a] for a in range(ns)] for k in range(n)],
+                                   [nb[k] for k in range(n)])
+            f = _lib.COLUMNS_CB(tramp)
+            check(lib().sm_app_add_stream_columns_callback(self._h, name.encode(), f, None))
+        elif isinstance(callback, StreamCallback):
             def tramp(user, evs, n, cb=callback):
                 cb.receive(_events(evs, n))
             f = _lib.STREAM_CB(tramp)

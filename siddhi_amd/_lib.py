@@ -23,6 +23,7 @@ EXPORTS = [
     "sm_app_snapshot", "sm_app_restore", "sm_partition_by_owner", "sm_order_matches", "sm_app_copy_device_matches",
     "sm_app_get_stat", "sm_compile_dump", "sm_nfa_jit_compile", "sm_app_device_project", "sm_merge_heartbeats",
     "sm_unpack_records", "sm_count_events_callback", "sm_app_copy_device_outputs", "sm_order_outputs",
+    "sm_app_add_stream_columns_callback", "sm_count_columns_callback",
 ]
 
 
@@ -36,6 +37,8 @@ class SmEvent(ctypes.Structure):
 
 
 STREAM_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(SmEvent), ctypes.c_size_t)
+COLUMNS_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64),
+                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32)
 QUERY_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(SmEvent), ctypes.c_size_t,
                             ctypes.POINTER(SmEvent), ctypes.c_size_t)
 
@@ -66,6 +69,7 @@ def lib():
         L.sm_app_advance_wallclock.argtypes = [vp, i64]
         L.sm_app_add_stream_callback.argtypes = [vp, cp, STREAM_CB, vp]
         L.sm_app_add_query_callback.argtypes = [vp, cp, QUERY_CB, vp]
+        L.sm_app_add_stream_columns_callback.argtypes = [vp, cp, COLUMNS_CB, vp]
         L.sm_app_set_collect.argtypes = [vp, ctypes.c_int]
         L.sm_app_dump_outputs.argtypes = [vp, ctypes.c_char_p, sz]
         L.sm_app_dump_outputs.restype = sz

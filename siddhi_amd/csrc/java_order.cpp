@@ -51,8 +51,10 @@ int32_t java_string_hash(const std::string& s) {
 }
 
 namespace {
-// Double.toString / Float.toString: the shortest digits that round-trip, laid out as Java does (plain decimal
-// for 1e-3 <= |v| < 1e7 with at least one fraction digit, else d.dddE<exp>)
+// Double.toString / Float.toString approximated by the shortest digits that round-trip, laid out as Java does (plain
+// decimal for 1e-3 <= |v| < 1e7 with at least one fraction digit, else d.dddE<exp>). Java 8's FloatingDecimal is not
+// always shortest, so this is not used for broadcast order: runtime.cpp refuses apps whose broadcasts would order
+// float / double keys; it remains for diagnostics only.
 template <typename F>
 std::string java_fp_string(F v) {
   if (v != v) return "NaN";

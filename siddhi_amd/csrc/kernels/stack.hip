@@ -54,9 +54,22 @@ constexpr int kOvf = 1024;     // ... and a shared overflow (more: the batch tak
 // 2^15 ordinals, whose direct writes land in a ~190 KB window that the L2 combines)
 // (tiles of 2^14 ordinals counted in packed u16 pairs, to keep the image in LDS, were exact and ran 22.9 ms against
 // 6.5: adjacent ordinals' atomics then hit one LDS word)
-constexpr int kOCap = kOT * 4 + 12288 * 8 <= 160 * 1024 ? 12288 : 0;
+// Round 6, measured and not kept: tiles of 2^14 ordinals (SM_ORDER_TB=14) with u32 counts, placed into the LDS image one
+// half (2^13 ordinals) at a time (kSplit passes of the placement), so that a bucket's segment of a tile is twice as long
+// (about 11 matches) and the line it shares with the next tile's segment, which comes back from HBM (VERDICT r05 #2:
+// the kernel reads 3.8x its staged bytes), is read half as often per match: exact (order tiles, device stream / batch,
+// sparse keys, bench-shape tests green), but 9.6 against 6.7 ms on the same box (the second placement pass over the
+// segments costs more than the boundary lines it saves; a 64 KB count array leaves one workgroup per CU).
+#ifndef SM_ORDER_SPLIT
+#define SM_ORDER_SPLIT (SM_ORDER_TB >= 14 ? 2 : 1)
+#endif
+constexpr int kSplit = SM_ORDER_SPLIT;  // placement passes per tile, each into the image
+constexpr int kOHB = kTB - (kSplit == 2 ? 1 : 0);  // log2 of the ordinals per placement pass
+static_assert(kSplit == 1 || kSplit == 2, "one or two placement passes");
+constexpr int kOCapMax = (160 * 1024 - kOT * 4 - 2 * kBins * 4 - 256) / 8;
+constexpr int kOCap = kOCapMax >= 12288 ? 12288 : (kOCapMax >= 8192 ? kOCapMax : 0);
 #ifndef SM_ORDER_GT
-#define SM_ORDER_GT (SM_ORDER_TB >= 15 ? 4 : 16)  // A/B build flag
+#define SM_ORDER_GT (SM_ORDER_TB >= 15 ? 4 : SM_ORDER_TB == 14 ? 8 : 16)  // A/B build flag
 #endif
 constexpr int kGT = SM_ORDER_GT;  // consecutive tiles per order workgroup
 #ifndef SM_ORDER_XCD
@@ -513,7 +526,7 @@ struct OrderArgs {
 // contiguous, coalesced run (its base = matches whose j precedes the tile, summed over buckets). A tile whose
 // output exceeds the LDS image writes its matches to their places directly.
 __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
-  __shared__ uint32_t cnt[kOT];
+  __shared__ __attribute__((aligned(16))) uint32_t cnt[kOT];
   __shared__ uint64_t obuf[kOCap > 0 ? kOCap : 1];
   __shared__ uint32_t sst[kBins], slen[kBins];
   __shared__ uint32_t lw[kOB / 64];
@@ -592,21 +605,35 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
     {  // exclusive scan of the counts, kPer ordinals per thread (read again from LDS rather than held in registers:
        // holding them spilled 4 VGPRs; 6.75 -> 6.5 ms)
       constexpr int kPer = kOT / kOB;
+      static_assert(kPer % 4 == 0, "16-byte count reads");
+      uint4* c4 = (uint4*)(cnt + tid * kPer);
       uint32_t sum = 0;
 #pragma unroll
-      for (int k = 0; k < kPer; ++k) sum += cnt[tid * kPer + k];
+      for (int k = 0; k < kPer / 4; ++k) {
+        const uint4 c = c4[k];
+        sum += c.x + c.y + c.z + c.w;
+      }
       uint32_t r = block_excl(sum, lw, &tot);
 #pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        const uint32_t c = cnt[tid * kPer + k];
-        cnt[tid * kPer + k] = r;
-        r += c;
+      for (int k = 0; k < kPer / 4; ++k) {
+        const uint4 c = c4[k];
+        uint4 o;
+        o.x = r;
+        o.y = o.x + c.x;
+        o.z = o.y + c.y;
+        o.w = o.z + c.z;
+        r = o.w + c.w;
+        c4[k] = o;
       }
     }
     lds_barrier();
-    const bool staged = kOCap > 0 && tot <= (uint32_t)kOCap;
-    // pass B: rank of each match among its j's matches = its segment position - the position where its j's run
-    // starts (runs may continue from the previous 16-match chunk of the segment)
+    // pass B, once per part of the tile (kSplit): rank of each match among its j's matches = its segment position -
+    // the position where its j's run starts (runs may continue from the previous 16-match chunk of the segment); the
+    // part's matches go to the LDS image (a j's run lies in one part)
+    for (int h = 0; h < kSplit; ++h) {
+    const uint32_t hb = h == 0 ? 0u : cnt[h << kOHB];  // the part's first output offset within the tile
+    const uint32_t he = h + 1 < kSplit ? cnt[(h + 1) << kOHB] : tot;
+    const bool staged = kOCap > 0 && he - hb <= (uint32_t)kOCap;
     auto place = [&](uint64_t v, bool valid, uint32_t c, uint32_t& cj, uint32_t& cstart) {
       const uint32_t j = (uint32_t)(v >> 32);
       uint32_t jp = __shfl_up(j, 1, 16);
@@ -615,9 +642,9 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
       const uint32_t sm = (uint32_t)((__ballot(start) & gmask) >> (g * 16));
       const uint32_t upto = sm & ((2u << l16) - 1u);
       const uint32_t rs = upto ? c + 31u - (uint32_t)__clz(upto) : cstart;
-      if (valid) {
+      if (valid && (kSplit == 1 || (int)((j - j0) >> kOHB) == h)) {
         const uint32_t pos = cnt[j - j0] + (c + l16 - rs);
-        if (staged) obuf[pos] = v;
+        if (staged) obuf[pos - hb] = v;
         else a.out[out + pos] = v;
       }
       const uint32_t vm = (uint32_t)((__ballot(valid) & gmask) >> (g * 16));
@@ -637,7 +664,9 @@ __global__ void __launch_bounds__(kOB) order_kernel(OrderArgs a) {
     }
     lds_barrier();
     if (staged)
-      for (uint32_t k = tid; k < tot; k += kOB) a.out[out + k] = obuf[k];
+      for (uint32_t k = tid; k < he - hb; k += kOB) a.out[out + hb + k] = obuf[k];
+    if (kSplit > 1) lds_barrier();  // the image's readers are done before the next part's placement
+    }
     out += tot;
   }
   }

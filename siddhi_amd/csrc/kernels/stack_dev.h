@@ -16,8 +16,8 @@ constexpr int kC = SM_STACK_KC;  // stack entries held in registers
 constexpr int kQ = 32;           // spilled entries per thread (HBM ring)
 constexpr int kOB = 1024;        // order workgroup: thread d owns bucket d
 #ifndef SM_ORDER_TB
-#define SM_ORDER_TB 13  // A/B build flag (config 4 order kernel: 13 -> 6.65 ms, 15 (direct writes) -> 9.8 ms)
-#endif
+#define SM_ORDER_TB 13  // A/B build flag (config 4 order kernel: 13 -> 6.65 ms, 15 (direct writes) -> 9.8 ms; round 6:
+#endif                  // 14 with two placement passes per tile (stack.hip kSplit) 9.6 against 6.7 ms, same box)
 constexpr int kTB = SM_ORDER_TB;  // order tile: 2^kTB consecutive relative ordinals
 constexpr int kOT = 1 << kTB;
 

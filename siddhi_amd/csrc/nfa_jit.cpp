@@ -12,9 +12,13 @@
 #include "nfa_jit.h"
 
 #include <hip/hiprtc.h>
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -100,8 +104,10 @@ std::string nfa_jit_source(const std::vector<char>& blob, bool lds, int compact)
   // reach HBM, and under rocprofv3 the kernel ran 27 ms against 18 ms), 2 waves = 256 VGPRs + 32 spilled (144 B),
   // 1 wave = 288 with no scratch; NFA kernel 19.1 / 18.1 / 19.2 ms, 4 waves 20.4 ms. Default 2.
   // A/B: SM_NFA_JIT_WAVES=<n> (0 = no hint).
+  // (A workgroup LDS above 20 KiB, SM_NFA_PA_KB, leaves one wave per SIMD: the hint is then 1, 512 VGPRs.)
+  const int pa = lds ? nfa_jit_pa_cap(blob) : 0;
   const char* w = getenv("SM_NFA_JIT_WAVES");
-  const int waves = w ? atoi(w) : 2;
+  const int waves = w ? atoi(w) : (lds && nfa_jit_lds_bytes(blob) > 20 * 1024 ? 1 : 2);
   if (waves > 0)
     src += "#define SM_NFA_JIT_ATTR __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))\n";
   else
@@ -110,6 +116,7 @@ std::string nfa_jit_source(const std::vector<char>& blob, bool lds, int compact)
   const char* e = getenv("SM_NFA_JIT_INLINE_ALL");
   if (!e || atoi(e)) src += "#define SM_NFA_JIT_INLINE_ALL 1\n";
   if (lds) src += "#define SM_NFA_LDS 1\n";
+  if (pa > 0) src += "#define SM_NFA_PA 1\n#define SM_NFA_PA_CAP " + std::to_string(pa) + "\n";
   if (compact >= 0) src += "#define SM_LANE_COMPACT_CONST " + std::to_string(compact ? 1 : 0) + "\n";
   src += blob_array(blob);
   src += kNfaJitBody;
@@ -136,13 +143,39 @@ int64_t device_lds_limit() {
 }
 }  // namespace
 
+namespace {
+int64_t staged_bytes(const DQuery* q) { return (int64_t)(q->ks_sched + 3) * 64 * 8; }  // pre + post + misc words x 64
+}  // namespace
+
+int nfa_jit_pa_cap(const std::vector<char>& blob) {
+  // LDS heads of the pending arrays (nfa_impl.h SM_NFA_PA): as many entries per pre with an operand cache as fit a
+  // workgroup LDS budget beside the staged key state (SM_NFA_PA_KB, default 20 KiB per 64-lane workgroup: eight
+  // workgroups, two waves per SIMD, per CU, the occupancy the kernel's registers allow); none below 2 entries.
+  // SM_NFA_PA=0 keeps the arrays in HBM only (A/B), SM_NFA_PA=<n> fixes the capacity.
+  static const char* env = getenv("SM_NFA_PA");
+  static const char* kb = getenv("SM_NFA_PA_KB");
+  if (env && atoi(env) == 0) return 0;
+  const DQuery* q = (const DQuery*)blob.data();
+  const DPre* pres = (const DPre*)(blob.data() + q->off_pre);
+  if (nfa_pa_words(pres, q->npre, 1) == 0) return 0;
+  if (env && atoi(env) > 0) return std::min(atoi(env), 255);
+  static const int64_t limit = device_lds_limit();
+  int64_t budget = (kb ? atoi(kb) : 20) * (int64_t)1024;
+  if (limit > 0 && budget > limit) budget = limit;
+  for (int cap = 64; cap >= 2; --cap)
+    if (staged_bytes(q) + (int64_t)nfa_pa_words(pres, q->npre, cap) * 64 * 8 <= budget) return cap;
+  return 0;
+}
+
 int64_t nfa_jit_lds_bytes(const std::vector<char>& blob) {
   if (!nfa_jit_lds()) return 0;
   const DQuery* q = (const DQuery*)blob.data();
-  const int64_t need = (int64_t)(q->ks_sched + 3) * 64 * 8;  // (pre words + post bits word + kNfaLdsMisc) x 64 lanes
+  const int64_t need = staged_bytes(q);
   static const int64_t limit = device_lds_limit();
   // a plan whose staged key state exceeds the workgroup's LDS keeps it in HBM (the interpreter's layout)
-  return limit > 0 && need > limit ? 0 : need;
+  if (limit > 0 && need > limit) return 0;
+  const DPre* pres = (const DPre*)(blob.data() + q->off_pre);
+  return need + (int64_t)nfa_pa_words(pres, q->npre, nfa_jit_pa_cap(blob)) * 64 * 8;
 }
 
 bool nfa_jit_wanted(int option, int64_t records) {
@@ -164,6 +197,28 @@ std::string nfa_jit_arch() {
   return SM_ARCH;
 }
 
+namespace {
+// Code-object cache on disk: a plan's kernel takes minutes to compile (hiprtc, one thread), and every process that
+// runs the plan (a test run, the bench, a profiler pass) would compile it again. The file name is a hash of
+// everything the code depends on (HIP version, target, options, the whole source with the plan and the knobs), so
+// a stale file is never picked up. Directory: SM_NFA_JIT_CACHE ("" = off), else jit_cache/ next to the library's
+// lib/ directory (in-tree, so code objects compiled on the build host travel with the tree like the library).
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+std::string jit_cache_dir() {
+  if (const char* e = getenv("SM_NFA_JIT_CACHE")) return e;
+  Dl_info info;
+  if (!dladdr((void*)&fnv1a, &info) || !info.dli_fname) return "";
+  std::string lib = info.dli_fname;
+  const size_t slash = lib.rfind('/');
+  if (slash == std::string::npos) return "";
+  return lib.substr(0, slash) + "/../jit_cache";
+}
+}  // namespace
+
 std::vector<char> nfa_jit_compile(const std::vector<char>& blob, int compact) {
   const std::string src = nfa_jit_source(blob, compact);
   if (const char* dump = getenv("SM_NFA_JIT_DUMP")) {
@@ -172,11 +227,28 @@ std::vector<char> nfa_jit_compile(const std::vector<char>& blob, int compact) {
       fclose(f);
     }
   }
+  const std::string arch = "--offload-arch=" + nfa_jit_arch();
+  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17", "-Wno-pass-failed"};
+  const std::string dir = jit_cache_dir();
+  std::string file;
+  if (!dir.empty()) {
+    char name[32];
+    snprintf(name, sizeof name, "%016llx.co",
+             (unsigned long long)fnv1a(std::to_string(HIP_VERSION) + "|" + opts[0] + "|" + opts[1] + "|" + opts[2] +
+                                       "|" + opts[3] + "|" + src));
+    file = dir + "/" + name;
+    if (FILE* f = fopen(file.c_str(), "rb")) {
+      std::vector<char> code;
+      char buf[1 << 16];
+      size_t r;
+      while ((r = fread(buf, 1, sizeof buf, f)) > 0) code.insert(code.end(), buf, buf + r);
+      fclose(f);
+      if (!code.empty()) return code;
+    }
+  }
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "sm_nfa_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     throw std::runtime_error("nfa jit: hiprtcCreateProgram failed");
-  const std::string arch = "--offload-arch=" + nfa_jit_arch();
-  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17", "-Wno-pass-failed"};
   const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
   if (rc != HIPRTC_SUCCESS) {
     size_t ls = 0;
@@ -191,6 +263,15 @@ std::vector<char> nfa_jit_compile(const std::vector<char>& blob, int compact) {
   std::vector<char> code(cs);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
+  if (!file.empty()) {  // written under a private name, then renamed: readers never see a partial file
+    mkdir(dir.c_str(), 0775);
+    const std::string tmp = file + "." + std::to_string((long)getpid()) + ".tmp";
+    if (FILE* f = fopen(tmp.c_str(), "wb")) {
+      const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
+      if (fclose(f) == 0 && ok) rename(tmp.c_str(), file.c_str());
+      else remove(tmp.c_str());
+    }
+  }
   return code;
 }
 

@@ -145,7 +145,17 @@ struct DevOut {
 struct Callback {
   sm_stream_callback scb = nullptr;
   sm_query_callback qcb = nullptr;
+  sm_stream_columns_callback ccb = nullptr;  // a StreamCallback taking columns (sm_app_add_stream_columns_callback)
   void* user = nullptr;
+};
+
+template <typename F>
+void parallel_for(size_t n, size_t grain, F&& f);
+
+// A pinned host buffer (the app's output arena; a Pending in the views form owns the ones its views point into)
+struct PinnedBuf {
+  char* p = nullptr;
+  size_t cap = 0;
 };
 
 // A growable array of trivially copyable elements whose growth does not initialise them (the Event arrays of a large
@@ -211,6 +221,22 @@ struct Pending {
   bool uniform = false;
   PreparedChunk proto;
   RawVec<uint64_t> starts;
+  // views form (round 6; uniform, and every callback of the call takes columns): no Events are built at all. Output
+  // k's timestamp is cts[k], its select values cvals[k * cns ..] (8-byte words), its null bits cnul[k]: views of the
+  // device outputs' pinned host copies, whose buffers this Pending owns until the callbacks have run (taken from the
+  // app's output arena, given back afterwards: a callback's own send into the app gets buffers of its own)
+  bool views = false;
+  const int64_t* cts = nullptr;
+  const int64_t* cvals = nullptr;
+  const uint8_t* cnul = nullptr;
+  int32_t cns = 0;
+  int32_t ctypes[8] = {0};
+  size_t cn = 0;
+  std::vector<PinnedBuf> owned;
+  ~Pending() {
+    for (auto& b : owned)
+      if (b.p) (void)hipHostFree(b.p);
+  }
   void swap(Pending& o) {
     chunks.swap(o.chunks);
     cbs.swap(o.cbs);
@@ -221,8 +247,16 @@ struct Pending {
     std::swap(uniform, o.uniform);
     std::swap(proto, o.proto);
     starts.swap(o.starts);
+    std::swap(views, o.views);
+    std::swap(cts, o.cts);
+    std::swap(cvals, o.cvals);
+    std::swap(cnul, o.cnul);
+    std::swap(cns, o.cns);
+    std::swap(ctypes, o.ctypes);
+    std::swap(cn, o.cn);
+    owned.swap(o.owned);
   }
-  void clear() {  // keeps the capacity (a bulk send reuses it chunk after chunk)
+  void clear() {  // keeps the capacity (a bulk send reuses it chunk after chunk); owned buffers were given back
     chunks.clear();
     cbs.clear();
     evs.clear();
@@ -231,9 +265,38 @@ struct Pending {
     final_ = false;
     uniform = false;
     starts.clear();
+    views = false;
+    cts = cvals = nullptr;
+    cnul = nullptr;
+    cn = 0;
+  }
+  // the views as Events (uniform form kept): before another delivery of the same call needs them
+  void devolve() {
+    if (!views) return;
+    evs.resize(cn);
+    vals.resize(cn * (size_t)cns);
+    parallel_for(cn, (size_t)1 << 16, [&](size_t lo, size_t hi) {
+      for (size_t k = lo; k < hi; ++k) {
+        for (int j = 0; j < cns; ++j) {
+          sm_value& v = vals[k * cns + j];
+          v.type = ctypes[j];
+          v.is_null = (cnul[k] >> j) & 1;
+          const int64_t w = v.is_null ? 0 : cvals[k * cns + j];
+          v.i = 0;
+          v.d = 0;
+          if (ctypes[j] == T_FLOAT || ctypes[j] == T_DOUBLE) memcpy(&v.d, &w, 8);
+          else v.i = w;
+          v.s = nullptr;
+        }
+        evs[k] = sm_event{cts[k], (const sm_value*)(uintptr_t)(k * cns), (int32_t)cns};
+      }
+    });
+    final_ = false;
+    views = false;
   }
   // the uniform form as PreparedChunks (before a general deliver appends chunks of other callbacks)
   void expand() {
+    devolve();
     if (!uniform) return;
     if (final_) {  // deliver_direct's streamed form holds pointers already: offsets again, vals may grow
       for (auto& e : evs) e.data = (const sm_value*)(uintptr_t)(e.data - vals.data());
@@ -417,16 +480,22 @@ struct sm_app {
   std::map<std::string, std::vector<std::string>> collected_streams;  // JSON fragments
   std::map<std::string, std::vector<std::string>> collected_queries;
   // output record buffers of the current call (HostOut points into them): pinned host memory, reused across calls
-  struct Pinned {
-    char* p = nullptr;
-    size_t cap = 0;
-  };
   struct OutArena {
-    std::vector<Pinned> bufs;
+    std::vector<sm::PinnedBuf> bufs;
     size_t next = 0;  // buffers in use by the current call
+    // the buffers in use go to a Pending in the views form (its callbacks read them after the app lock is released)
+    void lend(std::vector<sm::PinnedBuf>& to) {
+      for (size_t i = 0; i < next; ++i) to.push_back(bufs[i]);
+      bufs.erase(bufs.begin(), bufs.begin() + (ptrdiff_t)next);
+      next = 0;
+    }
+    void give_back(std::vector<sm::PinnedBuf>& from) {
+      for (auto& b : from) bufs.push_back(b);
+      from.clear();
+    }
     char* take(size_t bytes) {
       if (next == bufs.size()) bufs.emplace_back();
-      Pinned& b = bufs[next++];
+      sm::PinnedBuf& b = bufs[next++];
       if (b.cap < bytes) {
         if (b.p) SM_HIP(hipHostFree(b.p));
         b.p = nullptr;
@@ -509,6 +578,7 @@ int guarded(F&& f) {
 }
 
 void run_callbacks(Pending& out);
+void give_back(sm_app* a, Pending& out);
 
 // Entry points that can produce outputs: run f under the app lock, then the callbacks of what it produced
 // without it.
@@ -525,6 +595,7 @@ int locked(sm_app* a, F&& f) {
     out.swap(a->pending);
   }
   run_callbacks(out);
+  give_back(a, out);
   return rc;
 }
 
@@ -605,6 +676,16 @@ void build_app(sm_app* a) {
           for (size_t k = 0; k < cpm.key_code.size(); ++k)
             if (cpm.key_code[k].size() != 1 || cpm.key_code[k][0].op != OP_COL)
               throw sql::UnsupportedError("a partition whose queries read an unkeyed stream needs columns as keys");
+          // The instances receive the event in the iteration order of a map keyed by streamId + String.valueOf(key)
+          // (java_order.h). For an INT / LONG / STRING / BOOL key that string is exact; for FLOAT / DOUBLE it is
+          // Java 8's Double.toString / Float.toString (sun.misc.FloatingDecimal), which is not always the shortest
+          // round-trip digit string java_order.cpp writes, and no JVM here pins where they differ:
+          // such an app is refused rather than given an order that cannot be pinned.
+          for (int32_t kt : cpm.key_type)
+            if (kt == T_FLOAT || kt == T_DOUBLE)
+              throw sql::UnsupportedError(
+                  "a partition keyed by a float / double attribute whose queries read an unkeyed stream (broadcast "
+                  "order over Double.toString keys is not supported)");
           q->bcast = true;
           if (!a->part_bcast_group[pi].count(s)) a->part_bcast_group[pi][s] = q->cq.hdr.query_order;
           if (std::find(a->part_bcast[pi].begin(), a->part_bcast[pi].end(), s) == a->part_bcast[pi].end()) {
@@ -884,7 +965,7 @@ std::array<int64_t, 3> query_callbacks(sm_app* a, const CompiledQuery& cq) {
   auto it = a->stream_cbs.find(cq.insert_into);
   if (it != a->stream_cbs.end())
     for (auto& cb : it->second)
-      if (cb.scb) pd.cbs.push_back(cb);
+      if (cb.scb || cb.ccb) pd.cbs.push_back(cb);
   at[2] = (int64_t)pd.cbs.size() - at[0];
   return at;
 }
@@ -999,8 +1080,46 @@ void deliver(sm_app* a, std::vector<HostOut>& outs) {
 // the same app (its outputs are delivered inside that send, as in the reference). Reference behaviour for a
 // callback that throws (caught and logged, StreamCallback.java:92-99) is the binding's business: C callbacks
 // cannot throw across the ABI.
+// A columns StreamCallback on a chunk of Events (the forms other than the views): the chunk's columns built for the call
+void call_columns(const Callback& cb, const sm_event* evs, size_t n) {
+  const int32_t ns = n ? evs[0].n : 0;
+  std::vector<int64_t> ts(n), w((size_t)n * ns);
+  std::vector<uint8_t> nb(n, 0);
+  for (size_t k = 0; k < n; ++k) {
+    ts[k] = evs[k].timestamp;
+    for (int j = 0; j < ns; ++j) {
+      const sm_value& v = evs[k].data[j];
+      if (v.is_null) nb[k] |= (uint8_t)(1u << j);
+      if (v.type == T_FLOAT || v.type == T_DOUBLE) memcpy(&w[k * ns + j], &v.d, 8);
+      else w[k * ns + j] = v.is_null ? 0 : v.i;
+    }
+  }
+  cb.ccb(cb.user, n, ts.data(), w.data(), nb.data(), ns);
+}
+
+// the pinned buffers a views-form Pending held go back to the app's output arena
+void give_back(sm_app* a, Pending& out) {
+  if (out.owned.empty()) return;
+  std::lock_guard<std::mutex> g(a->mu);
+  a->out_arena.give_back(out.owned);
+}
+
 void run_callbacks(Pending& out) {
   if (out.chunks.empty() && !(out.uniform && !out.starts.empty())) return;
+  if (out.views) {  // every callback takes columns: views of the outputs, chunk by chunk (Pending::views)
+    const PreparedChunk& p = out.proto;
+    const size_t n = out.starts.size(), ne = out.cn;
+    const uint64_t* st = out.starts.data();
+    const int32_t ns = out.cns;
+    for (size_t k = 0; k < n; ++k) {
+      const size_t b = st[k], e = k + 1 < n ? st[k + 1] : ne;
+      for (uint32_t c = 0; c < p.n_cbs; ++c) {
+        const Callback& cb = out.cbs[p.cb_off + c];
+        cb.ccb(cb.user, e - b, out.cts + b, out.cvals + b * ns, out.cnul + b, ns);
+      }
+    }
+    return;
+  }
   if (!out.final_) {  // Pending::finalise on the host threads
     sm_value* vals = out.vals.data();
     sm_event* evs = out.evs.data();
@@ -1014,7 +1133,7 @@ void run_callbacks(Pending& out) {
     const size_t n = out.starts.size(), ne = out.evs.size();
     const uint64_t* st = out.starts.data();
     const sm_event* ev0 = out.evs.data();
-    if (p.n_cbs == 1 && p.n_query_cbs == 0) {  // one StreamCallback (the common case): no per-chunk dispatch
+    if (p.n_cbs == 1 && p.n_query_cbs == 0 && !out.cbs[p.cb_off].ccb) {  // one StreamCallback: no per-chunk dispatch
       const Callback& cb = out.cbs[p.cb_off];
       const sm_stream_callback f = cb.scb;
       void* const u = cb.user;
@@ -1029,6 +1148,7 @@ void run_callbacks(Pending& out) {
       for (uint32_t c = 0; c < p.n_cbs; ++c) {
         const Callback& cb = out.cbs[p.cb_off + c];
         if (c < p.n_query_cbs) cb.qcb(cb.user, ev0[e - 1].timestamp, ev0 + b, e - b, nullptr, 0);
+        else if (cb.ccb) call_columns(cb, ev0 + b, e - b);
         else cb.scb(cb.user, ev0 + b, e - b);
       }
     }
@@ -1039,6 +1159,7 @@ void run_callbacks(Pending& out) {
     for (uint32_t c = 0; c < ch.n_cbs; ++c) {
       const Callback& cb = out.cbs[ch.cb_off + c];
       if (c < ch.n_query_cbs) cb.qcb(cb.user, ch.ts, evs, ch.n_ev, nullptr, 0);
+      else if (cb.ccb) call_columns(cb, evs, ch.n_ev);
       else cb.scb(cb.user, evs, ch.n_ev);
     }
   }
@@ -1666,6 +1787,39 @@ void deliver_direct(sm_app* a, const DevOut& d) {
   for (size_t u = 0; u < U; ++u) cnt[u + 1] += cnt[u];
   bool strings = false;
   for (int t : cq.sel_types) strings |= t == T_STRING;
+  // the views form (round 6): every callback of the chunks takes columns (sm_app_add_stream_columns_callback), so
+  // no Event is built: the chunk starts only, and the callbacks get views of the pinned copies, whose buffers the
+  // Pending takes from the output arena until they have run (Pending::views)
+  bool cols_only = uni && d.hw && !strings && ns <= 8 && at[1] == 0;
+  for (int64_t c = at[0]; c < at[0] + at[2] && cols_only; ++c) cols_only = pd.cbs[(size_t)c].ccb != nullptr;
+  if (cols_only) {
+    pd.evs.resize(e0);
+    pd.vals.resize(v0);
+    pd.uniform = true;
+    pd.proto = PreparedChunk{};
+    pd.proto.cb_off = (uint32_t)at[0];
+    pd.proto.n_cbs = (uint32_t)at[2];
+    pd.starts.resize(cnt[U]);
+    parallel_for(T, 1, [&](size_t lo, size_t hi) {
+      for (size_t t = lo; t < hi; ++t)
+        for (size_t u = t; u < U; u += T) {
+          size_t c = cnt[u];
+          for (size_t k = m * u / U; k < m * (u + 1) / U; ++k)
+            if (k == 0 || trig(k) != trig(k - 1)) pd.starts[c++] = k;
+        }
+    });
+    d.wait_all();
+    pd.views = true;
+    pd.cts = d.hts;
+    pd.cvals = d.hw;
+    pd.cnul = d.hn;
+    pd.cns = ns;
+    for (int j = 0; j < ns; ++j) pd.ctypes[j] = cq.sel_types[j];
+    pd.cn = m;
+    a->out_arena.lend(pd.owned);
+    a->host_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return;
+  }
   // the streamed form: one query's compact values without strings are written with non-temporal stores (gigabytes
   // of Events that the next accesses read from DRAM anyway: no read-for-ownership of every line), the events holding
   // their final pointers (the call's vals do not grow again before the callbacks; Pending::expand undoes it)
@@ -2601,6 +2755,7 @@ int bulk_send_device(sm_app* a, int s, size_t n, const int64_t* ts, const void* 
     }
     const auto tc = clk::now();
     run_callbacks(out);
+    give_back(a, out);
     a->host_ms[3] += ms_since(tc);
   }
   return rc;
@@ -2825,7 +2980,10 @@ int sm_nfa_jit_compile(const char* siddhiql, int query, char* log, size_t cap, s
     auto [pi, qi] = ast.order[query];
     const sql::Query& qd = pi < 0 ? ast.queries[qi] : ast.partitions[pi].queries[qi];
     const CompiledQuery cq = compile_query(ast, qd, query, pi, dict);
-    const std::vector<char> code = nfa_jit_compile(cq.blob);
+    // SM_NFA_JIT_COMPACT=0/1: compile for that LaneEv form as a constant, as a batch launch does (tools/jit_precompile.py
+    // fills the code-object cache this way on the build host); unset: the form is read at run time
+    const char* cf = getenv("SM_NFA_JIT_COMPACT");
+    const std::vector<char> code = nfa_jit_compile(cq.blob, cf && *cf ? (atoi(cf) ? 1 : 0) : -1);
     if (code_size) *code_size = code.size();
     if (const char* path = getenv("SM_NFA_JIT_CO")) {
       if (FILE* f = fopen(path, "wb")) {
@@ -2981,6 +3139,33 @@ int sm_app_add_stream_callback(sm_app* a, const char* stream_id, sm_stream_callb
     c.user = user;
     a->stream_cbs[stream_id].push_back(c);
   });
+}
+
+int sm_app_add_stream_columns_callback(sm_app* a, const char* stream_id, sm_stream_columns_callback cb, void* user) {
+  std::lock_guard<std::mutex> g(a->mu);
+  return guarded([&] {
+    const int s = sm::stream_index(a->ast, stream_id);
+    if (s >= 0) {
+      const auto& attrs = a->ast.streams[s].attrs;
+      if (attrs.size() > 8) throw sql::UnsupportedError("columns callbacks take streams of at most 8 attributes");
+      for (auto& at : attrs)
+        if (at.type == sql::AttrType::STRING)
+          throw sql::UnsupportedError("columns callbacks take streams without STRING attributes");
+    }
+    Callback c;
+    c.ccb = cb;
+    c.user = user;
+    a->stream_cbs[stream_id].push_back(c);
+  });
+}
+
+void sm_count_columns_callback(void* user, size_t n, const int64_t* ts, const int64_t* values, const uint8_t* null_bits,
+                               int32_t nsel) {
+  (void)ts;
+  (void)values;
+  (void)null_bits;
+  (void)nsel;
+  *(int64_t*)user += (int64_t)n;
 }
 
 int sm_app_add_query_callback(sm_app* a, const char* query_name, sm_query_callback cb, void* user) {

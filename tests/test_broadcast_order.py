@@ -195,3 +195,17 @@ def test_product_broadcast_hand_order(hand, attr):
     keys, want = hand
     out = drive(ProductApp, app(attr), creating_then_broadcast(keys, attr))
     assert [r[1][0] if attr == "symbol" else str(r[1][2]) for r in out] == want
+
+
+@pytest.mark.gpu
+def test_product_refuses_float_key_broadcast():
+    """a partition keyed by a float / double attribute whose query reads an unkeyed stream would order
+    its broadcasts by Java 8 Double.toString strings (core/partition/executor/ValuePartitionExecutor.java:34-39), which
+    nothing here pins: the product refuses the app (SM_E_UNSUPPORTED) instead of guessing the order. The same app
+    keyed by an int or string attribute is accepted."""
+    from siddhi_amd import _lib
+    from siddhi_amd.testing import EngineError, ProductApp
+    with pytest.raises(EngineError) as e:
+        ProductApp(app("price"))
+    assert e.value.code == _lib.SM_E_UNSUPPORTED and "float / double" in str(e.value)
+    ProductApp(app("quantity")).close()

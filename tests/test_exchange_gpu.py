@@ -117,8 +117,20 @@ def test_bench_two_ranks_report_the_one_stream():
     assert one["config"]["rccl_world"] is None and two["config"]["rccl_world"] is None  # gloo rehearsal
 
 
+def assert_rank_records_equal(one_prefix, many_prefix, world, n):
+    """bench.py SM_BENCH_DUMP files: one rank's output records against the concatenation of `world` ranks' (int64
+    words of sm_out_rec + select values + ordinals), all words but the key slot (word 6)."""
+    import torch
+    ref = torch.load(f"{one_prefix}.rank0.pt", weights_only=True)
+    got = torch.cat([torch.load(f"{many_prefix}.rank{r}.pt", weights_only=True) for r in range(world)])
+    assert ref.shape[0] == n and got.shape == ref.shape
+    keep = [w for w in range(ref.shape[1]) if w != 6]
+    bad = (got[:, keep] != ref[:, keep]).any(dim=1).nonzero()
+    assert bad.numel() == 0, f"first differing record {int(bad[0])}: {got[int(bad[0])].tolist()} != {ref[int(bad[0])].tolist()}"
+
+
 @pytest.mark.timeout(900)
-def test_bench_config5_two_ranks_merge_to_one_stream():
+def test_bench_config5_two_ranks_merge_to_one_stream(tmp_path):
     """bench.py --config 5 --gpus 2 (its own launcher, over gloo on the one GPU): the key exchange, the global clock
     heartbeats (sm_merge_heartbeats) and the output merge (shard.merge_outputs / sm_order_outputs) inside the timed
     step, with the HIP NFA kernel on each rank; the emitting variant must report the same output count as one rank."""
@@ -127,9 +139,12 @@ def test_bench_config5_two_ranks_merge_to_one_stream():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                              "MASTER_PORT")}
     lines = []
+    dumps = {}
     for g, extra in ((1, {}), (2, {"SM_BENCH_BACKEND": "gloo"})):
+        dumps[g] = os.path.join(str(tmp_path), f"w{g}")
         r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(g)] + common,
-                           env={**env, **extra}, capture_output=True, text=True, timeout=800)
+                           env={**env, **extra, "SM_BENCH_DUMP": dumps[g]}, capture_output=True, text=True,
+                           timeout=800)
         assert r.returncode == 0, r.stderr[-3000:]
         js = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
         assert len(js) == 1
@@ -137,3 +152,8 @@ def test_bench_config5_two_ranks_merge_to_one_stream():
     one, two = lines
     assert two["n_gpus"] == 2 and two["config"]["events"] == one["config"]["events"] == 300_000
     assert two["config"]["matches"] == one["config"]["matches"] > 100
+    # record for record. The ranks' merged records (bench.py's timed path: merge_outputs) in rank order
+    # are the one-rank delivery order: trigger ordinal, step time, key first-seen ordinal, output timestamp, phase /
+    # query / scheduler / emission rank, every select value with its null flag, every matched event's ordinal. Only
+    # word 6 differs by construction (the key's slot in the rank's own table, a diagnostic).
+    assert_rank_records_equal(dumps[1], dumps[2], 2, one["config"]["matches"])

@@ -249,3 +249,92 @@ def test_send_device_batch_validates_tensors():
             rt.sendDeviceBatch("StockStream", b.get("ts", ts), b.get("cols", good), ordinals=b.get("ordinals"))
     rt.sendDeviceBatch("StockStream", ts, good, ordinals=ts)
     rt.shutdown()
+
+
+def _columns_runtime(text, **opts):
+    import siddhi_amd
+    from siddhi_amd import ColumnsStreamCallback, SiddhiManager
+    got = []
+
+    class CC(ColumnsStreamCallback):
+        def receive_columns(self, timestamps, values, null_bits):
+            got.append([timestamps, values, null_bits])
+
+    rt = SiddhiManager().createSiddhiAppRuntime(text)
+    for k, v in opts.items():
+        siddhi_amd.check(siddhi_amd.lib().sm_app_set_option(rt._h, k.encode(), int(v)))
+    rt.addCallback("OutputStream", CC())
+    rt.start()
+    return rt, got
+
+
+def _as_columns(calls, types):
+    """sm_event callback calls (lists of [ts, data]) in the columns form: 8-byte words (doubles as their bits)."""
+    import struct
+    out = []
+    for call in calls:
+        ts, vals, nb = [], [], []
+        for t, data in call:
+            ts.append(t)
+            row, bits = [], 0
+            for a, (v, ty) in enumerate(zip(data, types)):
+                if v is None:
+                    bits |= 1 << a
+                    row.append(0)
+                elif ty == "d":
+                    row.append(struct.unpack("<q", struct.pack("<d", v))[0])
+                else:
+                    row.append(int(v))
+            vals.append(row)
+            nb.append(bits)
+        out.append([ts, vals, nb])
+    return out
+
+
+@pytest.mark.parametrize("chunk", [77777, 1 << 24])
+def test_columns_callback_equals_event_callback(chunk):
+    """the StreamCallback in the columns form (sm_app_add_stream_columns_callback): on the bulk closed-form
+    path with only columns callbacks the outputs reach it as views of the device outputs' host copies (no Event records
+    built); it must receive exactly the chunks and values the sm_event StreamCallback receives (one call per e2 event,
+    StreamCallback.receive, core/stream/output/StreamCallback.java:65-76), and those equal the oracle's."""
+    n, K, div = 300_000, 1500, 10
+    cols, ts = stock(n, K, div)
+    cols[0] = cols[0] * 466
+    text = SCHEMA + part(PAT.format(within=" within 1 sec"))
+    exp = oracle_rows(text, cols, ts, "OutputStream")
+    rt, calls = runtime(text, bulk_min=1000, bulk_chunk=chunk)
+    rt.getInputHandler("StockStream").send_columns(ts, cols)
+    rt.shutdown()
+    assert calls == chunks_of(exp, lambda r: r[1][5])
+    rt2, got = _columns_runtime(text, bulk_min=1000, bulk_chunk=chunk)
+    rt2.getInputHandler("StockStream").send_columns(ts, cols)
+    assert stat(rt2, "fast_path:q") == 3
+    rt2.shutdown()
+    assert len(got) > 1000
+    assert got == _as_columns(calls, ["i", "d", "d", "i", "i", "i"])
+
+
+def test_columns_callback_beside_event_callback_and_on_the_nfa():
+    """The columns form where Events are built anyway: beside an sm_event StreamCallback on the same stream (each chunk
+    converted for it), and on the general NFA kernel's outputs (a null value hands the query to the NFA)."""
+    from siddhi_amd import ColumnsStreamCallback, StreamCallback
+    n, K, div = 60_000, 300, 10
+    cols, ts = stock(n, K, div)
+    text = SCHEMA + part(PAT.format(within=" within 1 sec"))
+    rt, calls = runtime(text, bulk_min=1000)
+    got = []
+
+    class CC(ColumnsStreamCallback):
+        def receive_columns(self, timestamps, values, null_bits):
+            got.append([timestamps, values, null_bits])
+
+    rt.addCallback("OutputStream", CC())
+    ih = rt.getInputHandler("StockStream")
+    ih.send_columns(ts[:30_000], [c[:30_000] for c in cols])
+    for i in range(30_000, 30_100):  # row sends with a null volume: the query moves to the NFA kernel
+        ih.send(int(ts[i]), [int(cols[0][i]), float(cols[1][i]), None if i % 7 == 0 else int(cols[2][i]), int(cols[3][i])])
+    rt.flush()
+    ih.send_columns(ts[30_100:], [c[30_100:] for c in cols])
+    rt.shutdown()
+    assert len(calls) > 200
+    assert got == _as_columns(calls, ["i", "d", "d", "i", "i", "i"])
