@@ -233,7 +233,17 @@ struct Pending {
   int32_t ctypes[8] = {0};
   size_t cn = 0;
   std::vector<PinnedBuf> owned;
+  // views of a bulk send's deferred copies (DevOut segments): outputs [seg_end[i-1], seg_end[i]) are on the host once
+  // seg_ev[i] has completed, so the callbacks of the first chunks run while later segments still cross PCIe
+  std::vector<int64_t> seg_end;
+  std::vector<hipEvent_t> seg_ev;
+  void wait_segments() {
+    for (hipEvent_t e : seg_ev) SM_HIP(hipEventSynchronize(e));
+    seg_ev.clear();
+    seg_end.clear();
+  }
   ~Pending() {
+    for (hipEvent_t e : seg_ev) (void)hipEventSynchronize(e);  // copies into the owned buffers have landed
     for (auto& b : owned)
       if (b.p) (void)hipHostFree(b.p);
   }
@@ -255,6 +265,8 @@ struct Pending {
     std::swap(ctypes, o.ctypes);
     std::swap(cn, o.cn);
     owned.swap(o.owned);
+    seg_end.swap(o.seg_end);
+    seg_ev.swap(o.seg_ev);
   }
   void clear() {  // keeps the capacity (a bulk send reuses it chunk after chunk); owned buffers were given back
     chunks.clear();
@@ -269,10 +281,13 @@ struct Pending {
     cts = cvals = nullptr;
     cnul = nullptr;
     cn = 0;
+    seg_end.clear();
+    seg_ev.clear();
   }
   // the views as Events (uniform form kept): before another delivery of the same call needs them
   void devolve() {
     if (!views) return;
+    wait_segments();
     evs.resize(cn);
     vals.resize(cn * (size_t)cns);
     parallel_for(cn, (size_t)1 << 16, [&](size_t lo, size_t hi) {
@@ -1100,6 +1115,7 @@ void call_columns(const Callback& cb, const sm_event* evs, size_t n) {
 // the pinned buffers a views-form Pending held go back to the app's output arena
 void give_back(sm_app* a, Pending& out) {
   if (out.owned.empty()) return;
+  out.wait_segments();  // no copy into the buffers is still in flight
   std::lock_guard<std::mutex> g(a->mu);
   a->out_arena.give_back(out.owned);
 }
@@ -1111,8 +1127,13 @@ void run_callbacks(Pending& out) {
     const size_t n = out.starts.size(), ne = out.cn;
     const uint64_t* st = out.starts.data();
     const int32_t ns = out.cns;
+    size_t ready = out.seg_end.empty() ? ne : 0, seg = 0;
     for (size_t k = 0; k < n; ++k) {
       const size_t b = st[k], e = k + 1 < n ? st[k + 1] : ne;
+      while (e > ready) {  // the chunk's outputs are on the host once their segments' copies have completed
+        SM_HIP(hipEventSynchronize(out.seg_ev[seg]));
+        ready = (size_t)out.seg_end[seg++];
+      }
       for (uint32_t c = 0; c < p.n_cbs; ++c) {
         const Callback& cb = out.cbs[p.cb_off + c];
         cb.ccb(cb.user, e - b, out.cts + b, out.cvals + b * ns, out.cnul + b, ns);
@@ -1808,7 +1829,8 @@ void deliver_direct(sm_app* a, const DevOut& d) {
             if (k == 0 || trig(k) != trig(k - 1)) pd.starts[c++] = k;
         }
     });
-    d.wait_all();
+    pd.seg_end = d.seg_end;  // the values may still be crossing PCIe: run_callbacks waits segment by segment
+    pd.seg_ev = d.seg_ev;
     pd.views = true;
     pd.cts = d.hts;
     pd.cvals = d.hw;
@@ -2731,7 +2753,8 @@ int bulk_send_device(sm_app* a, int s, size_t n, const int64_t* ts, const void* 
           struct Undefer {
             sm_app* a;
             ~Undefer() {
-              if (a->defer_outputs) (void)hipStreamSynchronize(a->stream);  // no copy outlives the call
+              // no copy outlives the call, unless the call's Pending holds views of them (it waits for them itself)
+              if (a->defer_outputs && a->pending.seg_ev.empty()) (void)hipStreamSynchronize(a->stream);
               a->defer_outputs = false;
             }
           } undefer{a};
