@@ -45,7 +45,7 @@ constexpr int kPaWin = SM_NFA_PA_WIN;
   const int pn = pa ? pa_n(p) : 0;                                       \
   int pi = 0, pw = 0;                                                    \
   int64_t e0 = 0, v0 = 0, v1 = 0;                                        \
-  int64_t we0[kPaWin], wv0[kPaWin], wv1[kPaWin];                         \
+  int64_t we0[kPaWin > 1 ? kPaWin : 1], wv0[kPaWin > 1 ? kPaWin : 1], wv1[kPaWin > 1 ? kPaWin : 1]; \
   _Pragma("unroll") for (int k_ = 0; k_ < kPaWin; ++k_)                  \
     if (kPaWin > 1 && k_ < pn) pa_read(p, pobj, k_, we0[k_], wv0[k_], wv1[k_]); \
   int f = 0;                                                             \
@@ -73,17 +73,20 @@ constexpr int kPaWin = SM_NFA_PA_WIN;
 #define SM_PA_NEXT(s)                                                    \
   in = pi < pn;                                                          \
   if (in) {                                                              \
-    if (kPaWin == 1) pa_read(p, pobj, pi, we0[0], wv0[0], wv1[0]);       \
-    e0 = we0[0];                                                         \
-    v0 = wv0[0];                                                         \
-    v1 = wv1[0];                                                         \
-    _Pragma("unroll") for (int k_ = 0; k_ + 1 < kPaWin; ++k_) {          \
-      we0[k_] = we0[k_ + 1];                                             \
-      wv0[k_] = wv0[k_ + 1];                                             \
-      wv1[k_] = wv1[k_ + 1];                                             \
+    if (kPaWin == 1) {                                                   \
+      pa_read(p, pobj, pi, e0, v0, v1);                                  \
+    } else {                                                             \
+      e0 = we0[0];                                                       \
+      v0 = wv0[0];                                                       \
+      v1 = wv1[0];                                                       \
+      _Pragma("unroll") for (int k_ = 0; k_ + 1 < kPaWin; ++k_) {        \
+        we0[k_] = we0[k_ + 1];                                           \
+        wv0[k_] = wv0[k_ + 1];                                           \
+        wv1[k_] = wv1[k_ + 1];                                           \
+      }                                                                  \
+      if (pi + kPaWin < pn)                                              \
+        pa_read(p, pobj, pi + kPaWin, we0[kPaWin - 1], wv0[kPaWin - 1], wv1[kPaWin - 1]); \
     }                                                                    \
-    if (kPaWin > 1 && pi + kPaWin < pn)                                  \
-      pa_read(p, pobj, pi + kPaWin, we0[kPaWin - 1], wv0[kPaWin - 1], wv1[kPaWin - 1]); \
     s = (int32_t)e0;                                                     \
     f = (int)(e0 >> 32);                                                 \
   } else {                                                               \
@@ -534,6 +537,19 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ pending arrays (K_PARR, kPaCap)
+  // whether pre p's entries carry a second operand (plan-constant dispatch in the query-specialised build: false
+  // without a load when no pre caches two operands)
+  __device__ bool pa_two(int p) const {
+#ifdef SM_NFA_JIT
+    bool two = false;
+#pragma unroll
+    for (int q = 0; q < PQ->npre; ++q)
+      if (q == p) two = PPRE[q].ncache > 1;
+    return two;
+#else
+    return PPRE[p].ncache > 1;
+#endif
+  }
 #ifdef SM_NFA_JIT
   __device__ bool pa_on(int p) const {  // plan-constant dispatch: false without a load when no pre has a cache
     bool on = false;
@@ -562,7 +578,7 @@ struct Lane {
 #endif
   // entry i of pre p's pending array (HBM object obj): the LDS head (SM_NFA_PA) or the object
   SM_JIT_INL __device__ void pa_read(int p, int32_t obj, int i, int64_t& e0, int64_t& v0, int64_t& v1) const {
-    const int E = 1 + PPRE[p].ncache;
+    const int E = pa_two(p) ? 3 : 2;
 #ifdef SM_NFA_PA
     if (i < kPaCap) {
       const int b = pa_base_of(p) + i * E;
@@ -582,7 +598,7 @@ struct Lane {
     v1 = E > 2 ? heap[b + 2] : 0;
   }
   SM_JIT_INL __device__ void pa_write(int p, int32_t obj, int i, int64_t e0, int64_t v0, int64_t v1) const {
-    const int E = 1 + PPRE[p].ncache;
+    const int E = pa_two(p) ? 3 : 2;
 #ifdef SM_NFA_PA
     if (i < kPaCap) {
       const int b = pa_base_of(p) + i * E;

@@ -148,13 +148,16 @@ int64_t staged_bytes(const DQuery* q) { return (int64_t)(q->ks_sched + 3) * 64 *
 }  // namespace
 
 int nfa_jit_pa_cap(const std::vector<char>& blob) {
-  // LDS heads of the pending arrays (nfa_impl.h SM_NFA_PA): as many entries per pre with an operand cache as fit a
-  // workgroup LDS budget beside the staged key state (SM_NFA_PA_KB, default 20 KiB per 64-lane workgroup: eight
-  // workgroups, two waves per SIMD, per CU, the occupancy the kernel's registers allow); none below 2 entries.
-  // SM_NFA_PA=0 keeps the arrays in HBM only (A/B), SM_NFA_PA=<n> fixes the capacity.
-  static const char* env = getenv("SM_NFA_PA");
-  static const char* kb = getenv("SM_NFA_PA_KB");
+  // LDS heads of the pending arrays (nfa_impl.h SM_NFA_PA): opt-in. SM_NFA_PA_KB=<k> sizes them to as many entries
+  // per pre with an operand cache as fit a k KiB workgroup LDS budget beside the staged key state (20 KiB per 64-lane
+  // workgroup keeps eight workgroups, two waves per SIMD, per CU, the occupancy the kernel's registers allow; none
+  // below 2 entries); SM_NFA_PA=<n> fixes the capacity. Off by default: on the config-5 emitting variant (pending
+  // arrays of at most ~20 partials) the 7-entry head at 20 KiB measured 148.5-149.2 ms against 144.6 ms for the
+  // arrays in HBM only (same box, round 6). Read per compile (tests switch it per app).
+  const char* env = getenv("SM_NFA_PA");
+  const char* kb = getenv("SM_NFA_PA_KB");
   if (env && atoi(env) == 0) return 0;
+  if (!env && !kb) return 0;
   const DQuery* q = (const DQuery*)blob.data();
   const DPre* pres = (const DPre*)(blob.data() + q->off_pre);
   if (nfa_pa_words(pres, q->npre, 1) == 0) return 0;

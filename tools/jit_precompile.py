@@ -22,7 +22,15 @@ def plans():
         apps[f"device_events_{k}"] = synth.app5(v)
     for k, v in bench.VARIANTS5.items():
         apps[f"bench_{k}"] = bench.app5_variant(v)
+    # test_device_events.test_config5_pending_array_lds_head: the pending arrays' LDS head switched on
+    for cap in ("2", "7"):
+        for k in ("pattern_count_not5s", "pattern_count_and_within"):
+            apps[f"pa{cap}_device_events_{k}"] = synth.app5(VARIANTS[k])
     return apps
+
+
+def plan_env(name):
+    return {"SM_NFA_PA": name[2:name.index("_")]} if name.startswith("pa") else {}
 
 
 def one(name):
@@ -41,15 +49,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=4)
     ap.add_argument("--one")
+    ap.add_argument("--only", help="comma-separated plan names")
     a = ap.parse_args()
     if a.one:
         sys.exit(one(a.one))
     env = dict(os.environ, SM_NFA_JIT_COMPACT="1")
-    names = list(plans())
+    names = a.only.split(",") if a.only else list(plans())
     procs, rc = [], 0
     while names or procs:
         while names and len(procs) < a.j:
-            procs.append(subprocess.Popen([sys.executable, __file__, "--one", names.pop(0)], env=env))
+            name = names.pop(0)
+            procs.append(subprocess.Popen([sys.executable, __file__, "--one", name], env=dict(env, **plan_env(name))))
         p = procs.pop(0)
         rc |= p.wait()
     sys.exit(rc)
