@@ -18,90 +18,11 @@
 namespace sm {
 namespace {
 
-constexpr int K_REC = 1, K_NODE = 2, K_LNODE = 3, K_LNODE4 = 4, K_PARR = 5, K_FWD = 0xFF;
-// A pending array (K_PARR, round 6): the pending list of a pre with an operand cache as one contiguous heap object,
-// header kind | E << 8 | cap << 12 | n << 32 (E words per entry, room for cap entries, n valid ones: kept up to date
-// at collections and at the end of a lane's run; between them the count lives in the pre's list word), then the
-// entries. Entry word 0 = run record | flags << 32 (PA_NULL0 / PA_NULL1: cached operand k is null; PA_OWN: the record
-// may hold the pre's own slot), words 1.. = the cached operands (DPre.ncache).
-constexpr int PA_NULL0 = 1, PA_OWN = 4;
-constexpr int kParrMaxCap = (1 << 20) - 1;
-// K_LNODE4: a list node with an operand cache (round 5; no longer made, kept readable)
+constexpr int K_REC = 1, K_NODE = 2, K_LNODE = 3, K_LNODE4 = 4, K_FWD = 0xFF;
+// words of a heap object of kind k (K_LNODE4: a list node with its operand cache, DPre.ncache)
+#define SM_OBJ_WORDS(k) ((k) == K_REC ? PQ->rec_words : (k) == K_NODE ? PQ->node_words : (k) == K_LNODE4 ? 4 : 2)
 
 struct Lane;
-
-// processAndReturn's walk over a pending list: for a pre with an operand cache its pending array (the LDS head first
-// under SM_NFA_PA, then the HBM object), read kPaWin entries ahead of the partial being processed so the loads of a
-// walk overlap instead of forming a chain; otherwise the HBM linked list. SM_PA_KEEP() / SM_PA_DROP() advance past the current
-// partial keeping / removing it (a kept array entry is written back at the write cursor, so the array compacts in
-// place as the walk goes; a list node is unlinked).
-#ifndef SM_NFA_PA_WIN
-#define SM_NFA_PA_WIN 1  // A/B build flag: entries read ahead of the one being processed
-#endif
-constexpr int kPaWin = SM_NFA_PA_WIN;
-#define SM_PA_CURSOR()                                                   \
-  const bool pa = pa_on(p);                                              \
-  int32_t pobj = pa ? pa_obj(p) : -1;                                    \
-  const int pn = pa ? pa_n(p) : 0;                                       \
-  int pi = 0, pw = 0;                                                    \
-  int64_t e0 = 0, v0 = 0, v1 = 0;                                        \
-  int64_t we0[kPaWin > 1 ? kPaWin : 1], wv0[kPaWin > 1 ? kPaWin : 1], wv1[kPaWin > 1 ? kPaWin : 1]; \
-  _Pragma("unroll") for (int k_ = 0; k_ < kPaWin; ++k_)                  \
-    if (kPaWin > 1 && k_ < pn) pa_read(p, pobj, k_, we0[k_], wv0[k_], wv1[k_]); \
-  int f = 0;                                                             \
-  bool in = false;                                                       \
-  int32_t ln = pa ? -1 : lhead(p, 0)
-// (macros, not lambdas: a lambda the compiler leaves out of line takes the Lane's address, and the Lane then lives in
-// scratch)
-#define SM_PA_KEEP()                                                           \
-  do {                                                                   \
-    if (in) { /* unmoved and unchanged entries are not written again */ \
-      if (pw != pi || f != (int)(e0 >> 32))                              \
-        pa_write(p, pobj, pw, (int64_t)(uint32_t)(int32_t)e0 | ((int64_t)f << 32), v0, v1); \
-      ++pw;                                                              \
-      ++pi;                                                              \
-    } else {                                                             \
-      prev = ln;                                                         \
-      ln = ln_next(ln);                                                  \
-    }                                                                    \
-  } while (0)
-#define SM_PA_DROP()                                                           \
-  do {                                                                   \
-    if (in) ++pi;                                                        \
-    else ln = lerase(p, 0, prev, ln);                                    \
-  } while (0)
-#define SM_PA_NEXT(s)                                                    \
-  in = pi < pn;                                                          \
-  if (in) {                                                              \
-    if (kPaWin == 1) {                                                   \
-      pa_read(p, pobj, pi, e0, v0, v1);                                  \
-    } else {                                                             \
-      e0 = we0[0];                                                       \
-      v0 = wv0[0];                                                       \
-      v1 = wv1[0];                                                       \
-      _Pragma("unroll") for (int k_ = 0; k_ + 1 < kPaWin; ++k_) {        \
-        we0[k_] = we0[k_ + 1];                                           \
-        wv0[k_] = wv0[k_ + 1];                                           \
-        wv1[k_] = wv1[k_ + 1];                                           \
-      }                                                                  \
-      if (pi + kPaWin < pn)                                              \
-        pa_read(p, pobj, pi + kPaWin, we0[kPaWin - 1], wv0[kPaWin - 1], wv1[kPaWin - 1]); \
-    }                                                                    \
-    s = (int32_t)e0;                                                     \
-    f = (int)(e0 >> 32);                                                 \
-  } else {                                                               \
-    if (ln < 0) break;                                                   \
-    s = ln_rec(ln);                                                      \
-  }
-#define SM_PA_END()                                                      \
-  if (pa) {                                                              \
-    for (; pi < pn; ++pi) { /* left by an error */                       \
-      int64_t x0, x1, x2;                                                \
-      pa_read(p, pobj, pi, x0, x1, x2);                                  \
-      pa_write(p, pobj, pw++, x0, x1, x2);                               \
-    }                                                                    \
-    pa_set(p, pobj, pw);                                                 \
-  }
 
 // Inlining of the interpreter's large member functions. Each non-inlined call saves the callee's registers to
 // per-lane scratch around the call, and at 4 waves per SIMD that scratch outgrows L2 and MALL. deliver and
@@ -171,34 +92,6 @@ constexpr int kPaWin = SM_NFA_PA_WIN;
 constexpr int kNfaLdsMisc = 3;  // misc words staged: 1..3 (bump, space, id counter); create (0, read per output) and
                                 // initialised (4, read once) stay in HBM
 
-// Pending arrays (round 6; north_star: "per-partition-key partial-match state in HBM, with LDS staging of active
-// partial matches per workgroup"). For every pre processor with an operand cache (DPre.ncache > 0:
-// a pattern's stream / count state whose filter compares the incoming event with earlier states' values, e.g.
-// `e2=B[price > e1.price]<2:5>`) the pending list is an ARRAY of {run record | flags, cached operands} entries
-// instead of a linked list of nodes: a K_PARR object in the key's HBM heap, grown by doubling, its count in the
-// pre's list word. A trial of a pending partial against an arriving event (StreamPreStateProcessor.processAndReturn
-// :274-327, CountPreStateProcessor.processAndReturn :58-93) reads one entry; the run record is read only for a
-// partial the filter accepts, and the walk reads kPaWin entries ahead, so a walk over n partials costs about
-// n / kPaWin dependent reads instead of a chain of n list-node reads. Every walk compacts the array in place
-// (partials that expired, completed or left are squeezed out by the write cursor, the survivors keep their order,
-// which is the reference's pending-list order).
-// SM_NFA_PA (the query-specialised kernel and the CPU harness): the first kPaCap entries of each array live in the
-// workgroup's LDS for the lane's whole event run (lane-interleaved, word w of lane t at [w * 64 + t]), the HBM object
-// holding the rest (entry i >= kPaCap at i - kPaCap): the oldest partials, which every walk reads, cost an LDS read;
-// the HBM object is the overflow for keys whose lists outgrow the head. The head moves back into the object at the
-// end of the run (which snapshots and the next batch see).
-#ifdef SM_NFA_PA
-#ifndef SM_NFA_PA_CAP
-#define SM_NFA_PA_CAP 8
-#endif
-constexpr int kPaCap = SM_NFA_PA_CAP;
-#ifndef SM_NFA_LDS
-constexpr int kPaHostWords = 2 * kMaxProcs * nfa_pa_pre_words(2, kPaCap);  // CPU harness: one lane at a time
-#endif
-#else
-constexpr int kPaCap = 0;
-#endif
-
 struct StateLoader {  // OP_VAR loads for a run record
   const Lane* L;
   int rec;
@@ -213,23 +106,14 @@ struct TrialLoader {
   const int64_t* evr;
   __device__ StackVal var(const Instr& in) const;
 };
-// which of pre P's cached operands (DPre.cacheIns) the load `in` is; -1 if none
-__device__ __forceinline__ int cache_index(const Instr* code, const DPre& P, const Instr& in) {
-  for (int k = 0; k < P.ncache && k < 2; ++k) {
-    const Instr& c = code[P.cacheIns[k]];
-    if (c.op == in.op && c.a == in.a && c.b == in.b && c.c == in.c) return k;
-  }
-  return -1;
-}
-// A trial with the other states' operands from a pending-array entry (DPre.ncache): the partial's run record and chain
-// nodes are not read at all
-struct PaTrialLoader {
-  Lane* L;
+// A trial whose other-state operands come from the list node's cache (DPre.ncache, K_LNODE4): the partial's run record
+// and chain nodes are not read at all (one read of the node per rejected partial)
+struct CachedTrialLoader {
+  const Lane* L;
+  int32_t ln;
   int sid;
   int pre;
   const int64_t* evr;
-  int64_t v0, v1;
-  int nb;  // null bits of the operands
   __device__ StackVal var(const Instr& in) const;
 };
 
@@ -287,9 +171,6 @@ struct Lane {
   LaneWords ks;   // per-key state words: list heads, flags, post words, misc (LDS-staged under SM_NFA_LDS)
   LaneWords ksh;  // the same key's words in HBM (timer queues always live there)
   LaneWords heap;
-#ifdef SM_NFA_PA
-  LaneWords pa;   // pending arrays (LDS)
-#endif
   int32_t half;  // words per semispace
   // batch
   const NfaBatch* b;
@@ -298,7 +179,7 @@ struct Lane {
   int64_t pos, time;
   int32_t phase, sched;
   int32_t seq;
-  int32_t err;
+  mutable int32_t err;  // (mutable: the const loaders of a filter report a broken plan invariant too)
   int64_t clock;  // EventTimeBasedMillisTimestampGenerator.currentTime() as seen by this lane
   // the earliest head of the lane's timer queues (min_head), INT64_MAX when all are empty: kept in a register, so the
   // per-event "is a timer due" check reads no timer-queue word (they live in HBM); set at lane start, lowered by
@@ -453,15 +334,27 @@ struct Lane {
   __device__ int32_t ln_rec(int32_t ln) const { return hi(ln); }
   __device__ int32_t ln_next(int32_t ln) const { return (int32_t)heap[ln + 1]; }
   __device__ void ln_set_next(int32_t ln, int32_t v) const { heap[ln + 1] = v; }
-  // list 0 of a pre with an operand cache is its pending array (patterns only: they never ask whether it is empty or
-  // clear it; kept exact all the same)
-  __device__ bool lempty(int p, int w) const {
-    if (w == 0 && pa_on(p)) return pa_n(p) == 0;
-    return lhead(p, w) < 0;
+  __device__ bool lempty(int p, int w) const { return lhead(p, w) < 0; }
+  // the trial operands of pre q's filter for run record `rec`, read once when the partial joins q's list (DPre.ncache)
+  // into the K_LNODE4 node ln {hdr | nulls << 8, next, v0, v1}; returns the null bits for the header
+  __device__ int64_t cache_fill(int q, int32_t ln, int32_t rec) {
+    int64_t nb = 0;
+    StateLoader ld{this, rec};
+    for (int k = 0; k < PPRE[q].ncache; ++k) {
+      const StackVal v = ld.var(PCODE[PPRE[q].cacheIns[k]]);
+      heap[ln + 2 + k] = v.null ? 0 : v.i;
+      if (v.null) nb |= (int64_t)1 << (8 + k);
+    }
+    return nb;
   }
+  // A node of a pre with a cache is K_LNODE4 from the start; its cache is filled when the node moves from the
+  // newAndEvery list to the pending list (lsplice, the only way a node reaches the list processAndReturn walks), so
+  // the fill has one call site instead of one per inlined append. Between the append and the splice nothing changes
+  // the cached states' chains (DPre.ncache).
   SM_INL_SMALL __device__ void lappend(int p, int w, int32_t rec) {
-    int32_t ln = alloc(2);
-    heap[ln] = K_LNODE | ((int64_t)(uint32_t)rec << 32);
+    const bool c4 = w < 2 && PPRE[p].ncache > 0;
+    int32_t ln = alloc(c4 ? 4 : 2);
+    heap[ln] = (c4 ? K_LNODE4 : K_LNODE) | ((int64_t)(uint32_t)rec << 32);
     heap[ln + 1] = -1;
     int32_t t = ltail(p, w);
     if (t < 0) lset(p, w, ln, ln);
@@ -470,12 +363,8 @@ struct Lane {
       lset(p, w, lhead(p, w), ln);
     }
   }
-  __device__ void lclear(int p, int w) const {
-    if (w == 0 && pa_on(p)) pa_set(p, pa_obj(p), 0);  // the array object stays for reuse
-    else lset(p, w, -1, -1);
-  }
+  __device__ void lclear(int p, int w) const { lset(p, w, -1, -1); }
   __device__ int lsize(int p, int w) const {
-    if (w == 0 && pa_on(p)) return pa_n(p);
     int n = 0;
     for (int32_t x = lhead(p, w); x >= 0; x = ln_next(x)) ++n;
     return n;
@@ -483,21 +372,15 @@ struct Lane {
   __device__ void lsplice(int p, int dst, int src) {  // dst.addAll(src); src.clear()
     int32_t sh = lhead(p, src);
     if (sh < 0) return;
-    if (dst == 0) {  // newAndEvery -> pending of a pre with a pending array: entries at its end
+    if (dst == 0) {  // newAndEvery -> pending: fill the operand caches of the arriving nodes (lappend)
 #ifdef SM_NFA_JIT_INLINE_ALL
-      bool done = false;
 #pragma unroll
       for (int q = 0; q < PQ->npre; ++q)
-        if (q == p && pa_on(q)) {
-          pa_splice(q);
-          done = true;
-        }
-      if (done) return;
+        if (q == p && PPRE[q].ncache > 0)
+          for (int32_t x = sh; x >= 0; x = ln_next(x)) heap[x] |= cache_fill(q, x, ln_rec(x));
 #else
-      if (pa_on(p)) {
-        pa_splice(p);
-        return;
-      }
+      if (PPRE[p].ncache > 0)
+        for (int32_t x = sh; x >= 0; x = ln_next(x)) heap[x] |= cache_fill(p, x, ln_rec(x));
 #endif
     }
     int32_t dt = ltail(p, dst);
@@ -525,216 +408,6 @@ struct Lane {
         lerase(p, w, prev, x);
         return;
       }
-  }
-
-  // CountPreStateProcessor.removeIfNextStateProcessed :95-101: the partial's next state already holds an event
-  __device__ bool next_filled(int sid, int32_t s) const {
-    return (PQ->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (PQ->nslots > sid + 2 && slot(s, sid + 2) >= 0);
-  }
-  // A count pre whose partials are tried before their record is read (the lazy path of processAndReturn below)
-  __device__ bool lazy_count(int p) const {
-    return PPRE[p].kind == PK_COUNT && PPRE[p].progLen != 0 && PPRE[p].trialCur && PPRE[p].ncache > 0;
-  }
-
-  // ------------------------------------------------------------ pending arrays (K_PARR, kPaCap)
-  // whether pre p's entries carry a second operand (plan-constant dispatch in the query-specialised build: false
-  // without a load when no pre caches two operands)
-  __device__ bool pa_two(int p) const {
-#ifdef SM_NFA_JIT
-    bool two = false;
-#pragma unroll
-    for (int q = 0; q < PQ->npre; ++q)
-      if (q == p) two = PPRE[q].ncache > 1;
-    return two;
-#else
-    return PPRE[p].ncache > 1;
-#endif
-  }
-#ifdef SM_NFA_JIT
-  __device__ bool pa_on(int p) const {  // plan-constant dispatch: false without a load when no pre has a cache
-    bool on = false;
-#pragma unroll
-    for (int q = 0; q < PQ->npre; ++q)
-      if (q == p) on = PPRE[q].ncache > 0;
-    return on;
-  }
-#else
-  __device__ bool pa_on(int p) const { return PPRE[p].ncache > 0; }
-#endif
-  __device__ int32_t pa_obj(int p) const { return (int32_t)lw(p, 0); }
-  __device__ int pa_n(int p) const {  // entries (a new lane's list word is all ones: none)
-    const int32_t n = (int32_t)(lw(p, 0) >> 32);
-    return n < 0 ? 0 : n;
-  }
-  __device__ void pa_set(int p, int32_t obj, int n) const { lw(p, 0) = (int64_t)(uint32_t)obj | ((int64_t)n << 32); }
-  __device__ int pa_cap_of(int32_t obj) const { return obj < 0 ? 0 : (int)((heap[obj] >> 12) & 0xFFFFF); }
-#ifdef SM_NFA_PA
-  __device__ int pa_base_of(int p) const {  // a plan constant in the query-specialised build
-    int o = 0;
-    for (int q = 0; q < p; ++q)
-      if (PPRE[q].ncache > 0) o += nfa_pa_pre_words(PPRE[q].ncache, kPaCap);
-    return o;
-  }
-#endif
-  // entry i of pre p's pending array (HBM object obj): the LDS head (SM_NFA_PA) or the object
-  SM_JIT_INL __device__ void pa_read(int p, int32_t obj, int i, int64_t& e0, int64_t& v0, int64_t& v1) const {
-    const int E = pa_two(p) ? 3 : 2;
-#ifdef SM_NFA_PA
-    if (i < kPaCap) {
-      const int b = pa_base_of(p) + i * E;
-      e0 = pa[b];
-      v0 = pa[b + 1];
-      v1 = E > 2 ? pa[b + 2] : 0;
-      return;
-    }
-#endif
-    if (obj < 0) {  // after a failed allocation (the lane is aborting)
-      e0 = v0 = v1 = 0;
-      return;
-    }
-    const int64_t b = (int64_t)obj + 1 + (int64_t)(i - kPaCap) * E;
-    e0 = heap[b];
-    v0 = heap[b + 1];
-    v1 = E > 2 ? heap[b + 2] : 0;
-  }
-  SM_JIT_INL __device__ void pa_write(int p, int32_t obj, int i, int64_t e0, int64_t v0, int64_t v1) const {
-    const int E = pa_two(p) ? 3 : 2;
-#ifdef SM_NFA_PA
-    if (i < kPaCap) {
-      const int b = pa_base_of(p) + i * E;
-      pa[b] = e0;
-      pa[b + 1] = v0;
-      if (E > 2) pa[b + 2] = v1;
-      return;
-    }
-#endif
-    if (obj < 0) return;
-    const int64_t b = (int64_t)obj + 1 + (int64_t)(i - kPaCap) * E;
-    heap[b] = e0;
-    heap[b + 1] = v0;
-    if (E > 2) heap[b + 2] = v1;
-  }
-  // room in pre p's HBM object for `need` entries, `have` of them in use: the object covers every entry, the LDS
-  // head's too (the end of the lane's run moves them there without allocating). Doubling growth; the old object is
-  // garbage. Returns the object (-1 after a failed allocation).
-  SM_JIT_INL __device__ int32_t pa_reserve(int p, int32_t obj, int have, int need) {
-    const int cap = pa_cap_of(obj);
-    if (need <= cap) return obj;
-    int nc = cap * 2 > 8 ? cap * 2 : 8;
-    if (nc < need) nc = need;
-    if (nc > kParrMaxCap) {
-      err |= NFA_ERR_ARENA;
-      return -1;
-    }
-    const int E = 1 + PPRE[p].ncache;
-    const int32_t o2 = alloc(1 + nc * E);
-    if (err) return -1;
-    heap[o2] = K_PARR | ((int64_t)E << 8) | ((int64_t)nc << 12);
-    const int64_t hw = (int64_t)(have > kPaCap ? have - kPaCap : 0) * E;
-    for (int64_t w = 0; w < hw; ++w) heap[o2 + 1 + w] = heap[obj + 1 + w];
-    return o2;
-  }
-  // newAndEvery -> pending (updateState): every node of list 1 becomes an entry at the end of the array, its
-  // operands read here, once (DPre.ncache: nothing changes the cached states' chains afterwards); the flag PA_OWN
-  // says the record arrived with the pre's own slot set (an every-copy), which the first rejection clears
-  SM_JIT_INL __device__ void pa_splice(int p) {
-    const int sid = PPRE[p].stateId;
-    int n = pa_n(p);
-    int32_t obj = pa_obj(p);
-    for (int32_t x = lhead(p, 1); x >= 0 && !err; x = ln_next(x)) {
-      const int32_t rec = ln_rec(x);
-      obj = pa_reserve(p, obj, n, n + 1);
-      StateLoader ld{this, rec};
-      int64_t v[2] = {0, 0};
-      int f = slot(rec, sid) >= 0 ? PA_OWN : 0;
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-        if (k < PPRE[p].ncache) {
-          const StackVal sv = ld.var(PCODE[PPRE[p].cacheIns[k]]);
-          v[k] = sv.null ? 0 : sv.i;
-          if (sv.null) f |= PA_NULL0 << k;
-        }
-      pa_write(p, obj, n, (int64_t)(uint32_t)rec | ((int64_t)f << 32), v[0], v[1]);
-      ++n;
-    }
-    pa_set(p, obj, n);
-    lset(p, 1, -1, -1);
-  }
-  // the filter of pre p tried with an entry's operands (plan-constant dispatch: a constant-length program)
-  SM_JIT_INL __device__ bool pa_trial(int p, const int64_t* evr, int64_t v0, int64_t v1, int f) {
-    bool pass = true;
-#pragma unroll
-    for (int q = 0; q < PQ->npre; ++q)
-      if (q == p && PPRE[q].progLen != 0 && PPRE[q].ncache > 0) {
-        PaTrialLoader ld{this, PPRE[q].stateId, q, evr, v0, v1, f & 3};
-        pass = truthy(eval_prog(PCODE + PPRE[q].progOff, PPRE[q].progLen, PCONSTS, ld));
-      }
-    return pass;
-  }
-#ifdef SM_NFA_PA
-  // lane start: the array's head into LDS, the rest of the object down by kPaCap entries (entry i >= kPaCap lives at
-  // object index i - kPaCap during the run)
-  SM_JIT_INL __device__ void pa_load(int p) {
-    const int n = pa_n(p);
-    const int32_t obj = pa_obj(p);
-    if (n == 0 || obj < 0) return;
-    const int E = 1 + PPRE[p].ncache;
-    const int nl = n < kPaCap ? n : kPaCap;
-    const int b = pa_base_of(p);
-    for (int w = 0; w < nl * E; ++w) pa[b + w] = heap[obj + 1 + w];
-    for (int64_t w = 0; w < (int64_t)(n - nl) * E; ++w) heap[obj + 1 + w] = heap[obj + 1 + (int64_t)kPaCap * E + w];
-  }
-#endif
-  // lane end: every entry back in the object (its capacity covers them, pa_reserve) and the object's header count,
-  // which collections between batches (pool compaction) and snapshots see
-  SM_JIT_INL __device__ void pa_finish(int p) {
-    const int n = pa_n(p);
-    const int32_t obj = pa_obj(p);
-    if (obj < 0) return;
-#ifdef SM_NFA_PA
-    const int E = 1 + PPRE[p].ncache;
-    const int nl = n < kPaCap ? n : kPaCap;
-    for (int64_t w = (int64_t)(n - nl) * E - 1; w >= 0; --w) heap[obj + 1 + (int64_t)kPaCap * E + w] = heap[obj + 1 + w];
-    const int b = pa_base_of(p);
-    for (int w = 0; w < nl * E; ++w) heap[obj + 1 + w] = pa[b + w];
-#endif
-    heap[obj] = (heap[obj] & 0xFFFFFFFFll) | ((int64_t)n << 32);
-  }
-  // collector roots: each array's object (its header count set to the entries it holds, whose records the scan
-  // forwards) and the LDS head's records (forwarded here). ADVICE r05: on the lazy count path a partial whose next
-  // state is filled stays pending until a trial passes (the reference drops it at the pre's next event), so with
-  // falling prices it could stay for good with its record and chain; nothing reads such a partial before it goes
-  // (patterns only: no lempty / lsize of the list), so every collection drops them first.
-  template <typename F>
-  SM_JIT_INL __device__ void pa_roots(F&& fwd_one) {
-    for (int p = 0; p < PQ->npre; ++p) {
-      if (!pa_on(p)) continue;
-      int n = pa_n(p);
-      int32_t obj = pa_obj(p);
-      if (lazy_count(p)) {
-        int w = 0;
-        for (int i = 0; i < n; ++i) {
-          int64_t e0, v0, v1;
-          pa_read(p, obj, i, e0, v0, v1);
-          if (next_filled(PPRE[p].stateId, (int32_t)e0)) continue;
-          if (w != i) pa_write(p, obj, w, e0, v0, v1);
-          ++w;
-        }
-        n = w;
-      }
-#ifdef SM_NFA_PA
-      for (int i = 0; i < n && i < kPaCap; ++i) {
-        int64_t e0, v0, v1;
-        pa_read(p, obj, i, e0, v0, v1);
-        pa_write(p, obj, i, (e0 & ~0xFFFFFFFFll) | (int64_t)(uint32_t)fwd_one((int32_t)e0), v0, v1);
-      }
-#endif
-      if (obj >= 0) {
-        heap[obj] = (heap[obj] & 0xFFFFFFFFll) | ((int64_t)(n > kPaCap ? n - kPaCap : 0) << 32);
-        obj = fwd_one(obj);
-      }
-      pa_set(p, obj, n);
-    }
   }
 
   // ------------------------------------------------------------ flags
@@ -796,6 +469,24 @@ struct Lane {
     return truthy(eval_prog(PCODE + P.progOff, P.progLen, PCONSTS, ld));
 #endif
   }
+  // trial_pass with the other states' operands from the list node's cache (DPre.ncache > 0)
+  SM_JIT_INL __device__ bool trial_cached(int p, int32_t ln, const int64_t* evr) const {
+#ifdef SM_NFA_JIT_INLINE_ALL
+    bool pass = true;
+#pragma unroll
+    for (int q = 0; q < PQ->npre; ++q)
+      if (q == p && PPRE[q].progLen != 0 && PPRE[q].ncache > 0) {  // the only pres that call it
+        CachedTrialLoader ld{this, ln, PPRE[q].stateId, q, evr};
+        pass = truthy(eval_prog(PCODE + PPRE[q].progOff, PPRE[q].progLen, PCONSTS, ld));
+      }
+    return pass;
+#else
+    const DPre& P = PPRE[p];
+    if (P.progLen == 0) return true;
+    CachedTrialLoader ld{this, ln, P.stateId, p, evr};
+    return truthy(eval_prog(PCODE + P.progOff, P.progLen, PCONSTS, ld));
+#endif
+  }
   // filter_pass for a trialCur state with the incoming event in place of its own slot's CURRENT: nothing is added to
   // the partial, so a partial that fails costs only the loads of the other slots' values
   SM_JIT_INL __device__ bool trial_pass(int p, int32_t rec, const int64_t* evr) const {
@@ -803,7 +494,7 @@ struct Lane {
     bool pass = true;
 #pragma unroll
     for (int q = 0; q < PQ->npre; ++q)
-      if (q == p && PPRE[q].progLen != 0 && PPRE[q].ncache == 0) {  // pres with a cache use pa_trial
+      if (q == p && PPRE[q].progLen != 0 && PPRE[q].ncache == 0) {  // pres with a cache use trial_cached
         TrialLoader ld{this, rec, PPRE[q].stateId, evr};
         pass = truthy(eval_prog(PCODE + PPRE[q].progOff, PPRE[q].progLen, PCONSTS, ld));
       }
@@ -1098,22 +789,20 @@ struct Lane {
         // fresh one.
         const bool trial = P.kind == PK_STREAM && P.progLen != 0;
         int32_t shared = -1;
-        SM_PA_CURSOR();
-        for (;;) {
-          int32_t s;
-          SM_PA_NEXT(s);
-          if (err) break;
+        for (int32_t ln = lhead(p, 0); ln >= 0;) {
+          if (err) return;
+          int32_t s = ln_rec(ln);
           if (P.withinCnt > 0 && expired(p, s, now)) {
-            SM_PA_DROP();
+            ln = lerase(p, 0, prev, ln);
             continue;
           }
           if (trial) {
             bool pass;
             if (P.trialCur) {
-              pass = in ? pa_trial(p, evr, v0, v1, f) : trial_pass(p, s, evr);
+              pass = P.ncache > 0 ? trial_cached(p, ln, evr) : trial_pass(p, s, evr);
               // the reference sets the slot to the event and back to null on a rejection: an every-copy that
-              // arrived with the slot filled leaves it null (an array entry knows whether one did, PA_OWN)
-              if (!pass && (!in || (f & PA_OWN))) set_slot(s, sid, -1);
+              // arrived with the slot filled leaves it null
+              if (!pass) set_slot(s, sid, -1);
             } else {
               if (shared < 0) shared = copy_event(evr);
               set_slot(s, sid, shared);
@@ -1123,10 +812,10 @@ struct Lane {
             setfl(p, F_STATE_CHANGED, false);
             if (!pass) {  // what the loop below does for a partial the filter rejects
               if (!P.sequence) {
-                f &= ~PA_OWN;
-                SM_PA_KEEP();
+                prev = ln;
+                ln = ln_next(ln);
               } else {
-                SM_PA_DROP();
+                ln = lerase(p, 0, prev, ln);
                 int cb = PPOST[P.post].callbackPre;
                 if (cb >= 0) count_startStateReset(cb);
               }
@@ -1146,20 +835,19 @@ struct Lane {
             lappend(p, 3, s);
           }
           if (fl(p, F_STATE_CHANGED)) {
-            SM_PA_DROP();
+            ln = lerase(p, 0, prev, ln);
           } else if (!P.sequence) {
             set_slot(s, sid, -1);
-            f &= ~PA_OWN;
-            SM_PA_KEEP();
+            prev = ln;
+            ln = ln_next(ln);
           } else {
             set_slot(s, sid, -1);
-            SM_PA_DROP();
+            ln = lerase(p, 0, prev, ln);
             int cb = PPOST[P.post].callbackPre;
             if (cb >= 0) count_startStateReset(cb);
           }
         }
         if (P.kind == PK_ABSENT_STREAM) lclear(p, 3);  // AbsentStreamPreStateProcessor.processAndReturn :218-231
-        SM_PA_END();
         return;
       }
       case PK_COUNT: {  // CountPreStateProcessor.processAndReturn :58-93
@@ -1169,22 +857,23 @@ struct Lane {
         // with an operand cache the trial comes first and the run record is read only for a partial that passes
         // (lazy removal): a partial whose next state is already filled is removed by the first event that would
         // otherwise act on it, and until then nothing reads it, so every output and list order is the reference's
-        const bool lazy = trial && P.trialCur && P.ncache > 0;
-        SM_PA_CURSOR();
-        for (;;) {
-          int32_t s;
-          SM_PA_NEXT(s);
-          if (err) break;
-          if (!lazy && next_filled(sid, s)) {
-            SM_PA_DROP();
+        const bool lazy = lazy_count(P);  // trial && P.trialCur && P.ncache > 0
+        for (int32_t ln = lhead(p, 0); ln >= 0;) {
+          if (err) return;
+          int32_t s = ln_rec(ln);
+          auto next_filled = [&]() {
+            return (PQ->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (PQ->nslots > sid + 2 && slot(s, sid + 2) >= 0);
+          };
+          if (!lazy && next_filled()) {
+            ln = lerase(p, 0, prev, ln);
             continue;
           }
           if (trial) {
             bool pass;
             if (lazy) {
-              pass = pa_trial(p, evr, v0, v1, f);  // a lazy pre has an operand cache: its entries are array entries
-              if (pass && next_filled(sid, s)) {
-                SM_PA_DROP();
+              pass = trial_cached(p, ln, evr);
+              if (pass && next_filled()) {
+                ln = lerase(p, 0, prev, ln);
                 continue;
               }
             } else if (P.trialCur) {
@@ -1198,8 +887,12 @@ struct Lane {
             setfl(p, F_SUCCESS, false);
             setfl(p, F_STATE_CHANGED, false);
             if (!pass) {  // what the loop below does for a partial the filter rejects
-              if (!P.sequence) SM_PA_KEEP();
-              else SM_PA_DROP();
+              if (!P.sequence) {
+                prev = ln;
+                ln = ln_next(ln);
+              } else {
+                ln = lerase(p, 0, prev, ln);
+              }
               continue;
             }
             int cn = 0;
@@ -1224,7 +917,7 @@ struct Lane {
           }
           bool removed = false;
           if (fl(p, F_STATE_CHANGED)) {
-            SM_PA_DROP();
+            ln = lerase(p, 0, prev, ln);
             removed = true;
           }
           if (!fl(p, F_SUCCESS)) {
@@ -1232,15 +925,17 @@ struct Lane {
             if (P.sequence) {
               if (removed) {
                 err |= NFA_ERR_NPE;
-                break;
+                return;
               }
-              SM_PA_DROP();
+              ln = lerase(p, 0, prev, ln);
               removed = true;
             }
           }
-          if (!removed) SM_PA_KEEP();
+          if (!removed) {
+            prev = ln;
+            ln = ln_next(ln);
+          }
         }
-        SM_PA_END();
         return;
       }
       case PK_LOGICAL: {  // LogicalPreStateProcessor.processAndReturn :125-163
@@ -1516,19 +1211,11 @@ struct Lane {
   }
 
   // ------------------------------------------------------------ garbage collection (Cheney, safe points only)
-  // words of the heap object with header word h0
-  SM_JIT_INL __device__ int obj_words(int64_t h0) const {
-    const int k = (int)(h0 & 0xFF);
-    if (k == K_REC) return PQ->rec_words;
-    if (k == K_NODE) return PQ->node_words;
-    if (k == K_PARR) return 1 + (int)((h0 >> 12) & 0xFFFFF) * (int)((h0 >> 8) & 0xF);
-    return k == K_LNODE4 ? 4 : 2;
-  }
-  SM_JIT_INL __device__ int32_t fwd(int32_t o, int64_t& top) {
+  __device__ int32_t fwd(int32_t o, int64_t& top) {
     if (o < 0) return o;
     int k = kind_of(o);
     if (k == K_FWD) return hi(o);
-    int words = obj_words(heap[o]);
+    int words = SM_OBJ_WORDS(k);
     int32_t n = (int32_t)top;
     SM_COUNT(3, words);
     for (int w = 0; w < words; ++w) heap[n + w] = heap[o + w];
@@ -1541,12 +1228,12 @@ struct Lane {
   // (StreamPreStateProcessor :58-59), so a hot key keeps growing while the other keys keep their small arenas.
   // After a collection that leaves a semispace more than a quarter full, the live objects are copied (the same
   // Cheney copy as gc, into a region of the pool) to a region with >= 8x their size per semispace.
-  SM_JIT_INL __device__ int32_t fwd_to(int32_t o, int64_t& top, const LaneWords& dst) {
+  __device__ int32_t fwd_to(int32_t o, int64_t& top, const LaneWords& dst) {
     if (o < 0) return o;
     const int64_t h0 = heap[o];
     const int k = (int)(h0 & 0xFF);
     if (k == K_FWD) return (int32_t)(h0 >> 32);
-    const int words = obj_words(h0);
+    const int words = SM_OBJ_WORDS(k);
     const int32_t n = (int32_t)top;
     SM_COUNT(3, words);
     for (int w = 0; w < words; ++w) dst[n + w] = heap[o + w];
@@ -1556,17 +1243,17 @@ struct Lane {
   }
   // Cheney copy of the live objects (reachable from the pending / newAndEvery lists, the collector's roots) into
   // semispace 0 of dst; returns the words copied. The source is left holding forwarding words.
-  SM_JIT_INL __device__ int64_t copy_live(const LaneWords& dst) {
+  __device__ int64_t copy_live(const LaneWords& dst) {
     auto hi_of = [&](int64_t w) { return (int32_t)(w >> 32); };
     auto with_hi = [&](int64_t w, int32_t v) { return (w & 0xFFFFFFFFll) | ((int64_t)(uint32_t)v << 32); };
     int64_t top = 0, scan = 0;
+    prune_stale();
     for (int p = 0; p < PQ->npre; ++p)
-      for (int w = pa_on(p) ? 1 : 0; w < 2; ++w) {  // (a pending array is forwarded by pa_roots)
+      for (int w = 0; w < 2; ++w) {
         const int32_t h = fwd_to(lhead(p, w), top, dst);
         const int32_t t = ltail(p, w) >= 0 ? fwd_to(ltail(p, w), top, dst) : -1;
         lset(p, w, h, t);
       }
-    pa_roots([&](int32_t o) { return fwd_to(o, top, dst); });
     while (scan < top) {
       const int32_t o = (int32_t)scan;
       const int64_t h0 = dst[o];
@@ -1575,13 +1262,6 @@ struct Lane {
         dst[o] = with_hi(h0, fwd_to(hi_of(h0), top, dst));
         dst[o + 1] = fwd_to((int32_t)dst[o + 1], top, dst);
         scan += k == K_LNODE4 ? 4 : 2;
-      } else if (k == K_PARR) {  // the entries' records (the header count: the entries the object holds)
-        const int E = (int)((h0 >> 8) & 0xF), nh = (int)(h0 >> 32);
-        for (int e = 0; e < nh; ++e) {
-          int64_t& w = dst[o + 1 + (int64_t)e * E];
-          w = (w & ~0xFFFFFFFFll) | (int64_t)(uint32_t)fwd_to((int32_t)w, top, dst);
-        }
-        scan += obj_words(h0);
       } else if (k == K_REC) {
         for (int s = 0; s < PQ->nslots; ++s) {
           int64_t& w = dst[o + 2 + (s >> 1)];
@@ -1617,7 +1297,7 @@ struct Lane {
       cur = prev;
     }
   }
-  SM_JIT_INL __device__ void promote(int64_t live) {
+  __device__ void promote(int64_t live) {
     const int64_t nh = pool_half(live, half);
     if (nh > ((int64_t)1 << 30)) return;  // heap offsets are 32-bit: stay (alloc reports an arena overflow)
     const int64_t words = 2 * nh + 64;
@@ -1633,18 +1313,43 @@ struct Lane {
     misc(5) = off + 1;
     misc(6) = nh;
   }
-  SM_JIT_INL __device__ void gc() {
+  // Stale partials of a lazily removed count state: with an operand cache a count partial is tried before
+  // its run record is read, so one whose next state is already filled stays in the pending list until an event passes
+  // its trial (processAndReturn, PK_COUNT). The reference drops it at the next event whatever the filter says
+  // (CountPreStateProcessor.processAndReturn :58-93, removeIfNextStateProcessed), and until then nothing reads it, so
+  // the collector may drop it first: the lists are pruned before they are forwarded, and a key whose count partials
+  // keep failing their trials holds only its live partials (outputs and list order are unchanged).
+  __device__ static bool lazy_count(const DPre& P) {
+    return P.kind == PK_COUNT && P.progLen != 0 && P.trialCur && P.ncache > 0;
+  }
+  __device__ void prune_stale() {
+    for (int p = 0; p < PQ->npre; ++p) {
+      if (!lazy_count(PPRE[p])) continue;
+      const int sid = PPRE[p].stateId;
+      int32_t prev = -1;
+      for (int32_t ln = lhead(p, 0); ln >= 0;) {
+        const int32_t s = ln_rec(ln);
+        if ((PQ->nslots > sid + 1 && slot(s, sid + 1) >= 0) || (PQ->nslots > sid + 2 && slot(s, sid + 2) >= 0)) {
+          ln = lerase(p, 0, prev, ln);
+        } else {
+          prev = ln;
+          ln = ln_next(ln);
+        }
+      }
+    }
+  }
+  __device__ void gc() {
     int64_t space = misc(2);
     SM_COUNT(4, 1);
+    prune_stale();
     int64_t to = (1 - space) * half;
     int64_t top = to, scan = to;
     for (int p = 0; p < PQ->npre; ++p)
-      for (int w = pa_on(p) ? 1 : 0; w < 2; ++w) {  // (a pending array is forwarded by pa_roots)
+      for (int w = 0; w < 2; ++w) {
         int32_t h = fwd(lhead(p, w), top);
         int32_t t = ltail(p, w) >= 0 ? fwd(ltail(p, w), top) : -1;
         lset(p, w, h, t);
       }
-    pa_roots([&](int32_t o) { return fwd(o, top); });
     while (scan < top) {
       int32_t o = (int32_t)scan;
       int k = kind_of(o);
@@ -1653,15 +1358,6 @@ struct Lane {
         int32_t nx = (int32_t)heap[o + 1];
         heap[o + 1] = fwd(nx, top);
         scan += k == K_LNODE4 ? 4 : 2;
-      } else if (k == K_PARR) {
-        const int64_t h0 = heap[o];
-        const int E = (int)((h0 >> 8) & 0xF), nh = (int)(h0 >> 32);
-        for (int e = 0; e < nh; ++e) {
-          const int64_t w = heap[o + 1 + (int64_t)e * E];
-          const int32_t r = fwd((int32_t)w, top);
-          heap[o + 1 + (int64_t)e * E] = (w & ~0xFFFFFFFFll) | (int64_t)(uint32_t)r;
-        }
-        scan += obj_words(h0);
       } else if (k == K_REC) {
         for (int s = 0; s < PQ->nslots; ++s) set_slot(o, s, fwd(slot(o, s), top));
         scan += PQ->rec_words;
@@ -1787,22 +1483,33 @@ __device__ StackVal TrialLoader::var(const Instr& in) const {
   return v;
 }
 
-__device__ StackVal PaTrialLoader::var(const Instr& in) const {
+__device__ StackVal CachedTrialLoader::var(const Instr& in) const {
   if (in.a == sid) return TrialLoader{L, -1, sid, evr}.var(in);
 #ifdef SM_NFA_JIT
-  const int k = cache_index(PCODE, PPRE[pre], in);
+  const DPre* PP = PPRE;
+  const Instr* PC = PCODE;
 #else
-  const int k = cache_index(L->PCODE, L->PPRE[pre], in);
+  const DPre* PP = L->PPRE;
+  const Instr* PC = L->PCODE;
 #endif
+  // operand k of this pre's cache (DPre.cacheIns; plan constants in the query-specialised build). A load that is none
+  // of them breaks the compiler's invariant (every other-state load of a cached filter is a cached operand): error,
+  // never a silent read of the other slot
+  const DPre& P = PP[pre];
+  int k = -1;
+  for (int c = 0; c < P.ncache && c < 2; ++c) {
+    const Instr& ci = PC[P.cacheIns[c]];
+    if (k < 0 && ci.op == in.op && ci.a == in.a && ci.b == in.b && ci.c == in.c) k = c;
+  }
   StackVal v;
-  v.i = 0;
-  v.null = 1;
   if (k < 0) {
     L->err |= NFA_ERR_NPE;
+    v.i = 0;
+    v.null = 1;
     return v;
   }
-  v.i = k == 0 ? v0 : v1;
-  v.null = (nb >> k) & 1;
+  v.i = L->heap[ln + 2 + k];
+  v.null = (int)((L->heap[ln] >> (8 + k)) & 1);
   return v;
 }
 
@@ -2019,18 +1726,6 @@ SM_JIT_INL __device__ void nfa_lane(const NfaBatch& b, const char* __restrict__ 
   for (int k = 0; k < kNfaLdsMisc; ++k) st[nst + k] = L.ksh[PQ->ks_misc + 1 + k];
   L.ks = st;
 #endif
-#ifdef SM_NFA_PA
-#ifdef SM_NFA_LDS
-  L.pa = LaneWords{sm_nfa_lds + (int64_t)(nst + kNfaLdsMisc) * 64 + threadIdx.x, 64};
-#else  // the CPU harness (lanes run one at a time)
-  static int64_t pa_host[kPaHostWords];
-  L.pa = LaneWords{pa_host, 1};
-  if (nfa_pa_words(PPRE, PQ->npre, kPaCap) > kPaHostWords) {
-    atomicOr(err_out, NFA_ERR_NPE);
-    return;
-  }
-#endif
-#endif
   nfa_lane_run(L, b, key, err_out);
 #ifdef SM_NFA_LDS
   for (int w = 0; w < nst; ++w) L.ksh[w] = st[w];
@@ -2076,11 +1771,6 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
   if (ebeg == eend && !has_timers) {
     return;
   }
-#ifdef SM_NFA_PA
-#pragma unroll
-  for (int p = 0; p < PQ->npre; ++p)
-    if (L.pa_on(p)) L.pa_load(p);  // the pending arrays' heads into LDS
-#endif
   if (has_timers) {  // timers left by earlier batches (a lane created just now has only what pre_init scheduled)
     int64_t h;
     L.due = L.min_head(h) ? h : INT64_MAX;
@@ -2130,9 +1820,6 @@ SM_JIT_INL __device__ void nfa_lane_run(Lane& L, const NfaBatch& b, int32_t key,
     if (L.err) break;
     L.safe_point();
   }
-#pragma unroll
-  for (int p = 0; p < PQ->npre; ++p)
-    if (L.pa_on(p)) L.pa_finish(p);
   if (L.err) atomicOr(err_out, L.err);
 }
 

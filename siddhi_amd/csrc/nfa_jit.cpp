@@ -18,7 +18,6 @@
 
 #include <cstdio>
 #include <cstdlib>
-#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -104,10 +103,8 @@ std::string nfa_jit_source(const std::vector<char>& blob, bool lds, int compact)
   // reach HBM, and under rocprofv3 the kernel ran 27 ms against 18 ms), 2 waves = 256 VGPRs + 32 spilled (144 B),
   // 1 wave = 288 with no scratch; NFA kernel 19.1 / 18.1 / 19.2 ms, 4 waves 20.4 ms. Default 2.
   // A/B: SM_NFA_JIT_WAVES=<n> (0 = no hint).
-  // (A workgroup LDS above 20 KiB, SM_NFA_PA_KB, leaves one wave per SIMD: the hint is then 1, 512 VGPRs.)
-  const int pa = lds ? nfa_jit_pa_cap(blob) : 0;
   const char* w = getenv("SM_NFA_JIT_WAVES");
-  const int waves = w ? atoi(w) : (lds && nfa_jit_lds_bytes(blob) > 20 * 1024 ? 1 : 2);
+  const int waves = w ? atoi(w) : 2;
   if (waves > 0)
     src += "#define SM_NFA_JIT_ATTR __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))\n";
   else
@@ -116,7 +113,6 @@ std::string nfa_jit_source(const std::vector<char>& blob, bool lds, int compact)
   const char* e = getenv("SM_NFA_JIT_INLINE_ALL");
   if (!e || atoi(e)) src += "#define SM_NFA_JIT_INLINE_ALL 1\n";
   if (lds) src += "#define SM_NFA_LDS 1\n";
-  if (pa > 0) src += "#define SM_NFA_PA 1\n#define SM_NFA_PA_CAP " + std::to_string(pa) + "\n";
   if (compact >= 0) src += "#define SM_LANE_COMPACT_CONST " + std::to_string(compact ? 1 : 0) + "\n";
   src += blob_array(blob);
   src += kNfaJitBody;
@@ -143,42 +139,13 @@ int64_t device_lds_limit() {
 }
 }  // namespace
 
-namespace {
-int64_t staged_bytes(const DQuery* q) { return (int64_t)(q->ks_sched + 3) * 64 * 8; }  // pre + post + misc words x 64
-}  // namespace
-
-int nfa_jit_pa_cap(const std::vector<char>& blob) {
-  // LDS heads of the pending arrays (nfa_impl.h SM_NFA_PA): opt-in. SM_NFA_PA_KB=<k> sizes them to as many entries
-  // per pre with an operand cache as fit a k KiB workgroup LDS budget beside the staged key state (20 KiB per 64-lane
-  // workgroup keeps eight workgroups, two waves per SIMD, per CU, the occupancy the kernel's registers allow; none
-  // below 2 entries); SM_NFA_PA=<n> fixes the capacity. Off by default: on the config-5 emitting variant (pending
-  // arrays of at most ~20 partials) the 7-entry head at 20 KiB measured 148.5-149.2 ms against 144.6 ms for the
-  // arrays in HBM only (same box, round 6). Read per compile (tests switch it per app).
-  const char* env = getenv("SM_NFA_PA");
-  const char* kb = getenv("SM_NFA_PA_KB");
-  if (env && atoi(env) == 0) return 0;
-  if (!env && !kb) return 0;
-  const DQuery* q = (const DQuery*)blob.data();
-  const DPre* pres = (const DPre*)(blob.data() + q->off_pre);
-  if (nfa_pa_words(pres, q->npre, 1) == 0) return 0;
-  if (env && atoi(env) > 0) return std::min(atoi(env), 255);
-  static const int64_t limit = device_lds_limit();
-  int64_t budget = (kb ? atoi(kb) : 20) * (int64_t)1024;
-  if (limit > 0 && budget > limit) budget = limit;
-  for (int cap = 64; cap >= 2; --cap)
-    if (staged_bytes(q) + (int64_t)nfa_pa_words(pres, q->npre, cap) * 64 * 8 <= budget) return cap;
-  return 0;
-}
-
 int64_t nfa_jit_lds_bytes(const std::vector<char>& blob) {
   if (!nfa_jit_lds()) return 0;
   const DQuery* q = (const DQuery*)blob.data();
-  const int64_t need = staged_bytes(q);
+  const int64_t need = (int64_t)(q->ks_sched + 3) * 64 * 8;  // (pre words + post bits word + kNfaLdsMisc) x 64 lanes
   static const int64_t limit = device_lds_limit();
   // a plan whose staged key state exceeds the workgroup's LDS keeps it in HBM (the interpreter's layout)
-  if (limit > 0 && need > limit) return 0;
-  const DPre* pres = (const DPre*)(blob.data() + q->off_pre);
-  return need + (int64_t)nfa_pa_words(pres, q->npre, nfa_jit_pa_cap(blob)) * 64 * 8;
+  return limit > 0 && need > limit ? 0 : need;
 }
 
 bool nfa_jit_wanted(int option, int64_t records) {
@@ -205,7 +172,8 @@ namespace {
 // runs the plan (a test run, the bench, a profiler pass) would compile it again. The file name is a hash of
 // everything the code depends on (HIP version, target, options, the whole source with the plan and the knobs), so
 // a stale file is never picked up. Directory: SM_NFA_JIT_CACHE ("" = off), else jit_cache/ next to the library's
-// lib/ directory (in-tree, so code objects compiled on the build host travel with the tree like the library).
+// lib/ directory (in-tree, so code objects compiled on the build host travel with the tree like the library;
+// tools/jit_precompile.py fills it).
 uint64_t fnv1a(const std::string& s) {
   uint64_t h = 1469598103934665603ull;
   for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
@@ -235,9 +203,16 @@ std::vector<char> nfa_jit_compile(const std::vector<char>& blob, int compact) {
   const std::string dir = jit_cache_dir();
   std::string file;
   if (!dir.empty()) {
+    // the hiprtc that is loaded, not the one built against: a process that imported torch first compiles with the
+    // hiprtc and comgr torch bundles (ROCm 7.0 in this image), one without with /opt/rocm's (7.2), and the two make
+    // different code from the same source (config-5 emitting variant: 170 VGPRs and 112 B of scratch, NFA kernel 108
+    // ms, against 256 VGPRs and 192 B, 139 ms)
+    int rtc_major = 0, rtc_minor = 0;
+    hiprtcVersion(&rtc_major, &rtc_minor);
     char name[32];
     snprintf(name, sizeof name, "%016llx.co",
-             (unsigned long long)fnv1a(std::to_string(HIP_VERSION) + "|" + opts[0] + "|" + opts[1] + "|" + opts[2] +
+             (unsigned long long)fnv1a(std::to_string(HIP_VERSION) + "|" + std::to_string(rtc_major) + "." +
+                                       std::to_string(rtc_minor) + "|" + opts[0] + "|" + opts[1] + "|" + opts[2] +
                                        "|" + opts[3] + "|" + src));
     file = dir + "/" + name;
     if (FILE* f = fopen(file.c_str(), "rb")) {

@@ -25,9 +25,6 @@ void* nfa_jit_function(const std::vector<char>& blob, int compact = -1);
 // they exceed the device's LDS per workgroup, in which case the kernel is built without the staging)
 bool nfa_jit_lds();
 int64_t nfa_jit_lds_bytes(const std::vector<char>& blob);
-// entries per pending array (nfa_impl.h SM_NFA_PA) of the plan's kernel; 0 = none (no pre with an operand cache, or
-// SM_NFA_PA=0); included in nfa_jit_lds_bytes
-int nfa_jit_pa_cap(const std::vector<char>& blob);
 void launch_nfa_jit(void* fn, int64_t lds_bytes, const NfaBatch& b, int64_t* ks, int64_t* heap, int32_t heap_half,
                     int64_t lanes, int32_t nkeys, int32_t* err_dev, hipStream_t s);
 

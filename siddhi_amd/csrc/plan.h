@@ -149,16 +149,6 @@ constexpr int kSchedCap = 32;
 constexpr int kPreWords = 4;
 constexpr int kPreWordsAbsent = 5;
 
-// Pending arrays (nfa_impl.h, SM_NFA_PA): the LDS head of the pending array of every pre processor with an operand
-// cache (DPre.ncache > 0), per lane: `cap` entries of 1 + ncache words. (constexpr: host and device code alike)
-constexpr int nfa_pa_pre_words(int ncache, int cap) { return cap * (1 + ncache); }
-constexpr int nfa_pa_words(const DPre* pres, int npre, int cap) {
-  int w = 0;
-  for (int q = 0; q < npre; ++q)
-    if (pres[q].ncache > 0) w += nfa_pa_pre_words(pres[q].ncache, cap);
-  return w;
-}
-
 // pre flags (bit set in the flags word)
 enum : int64_t { F_STATE_CHANGED = 1, F_INITIALIZED = 2, F_SUCCESS = 4, F_START_RESET = 8, F_ACTIVE = 16 };
 

@@ -14,12 +14,10 @@ class HV(ctypes.Structure):
 _L = {}
 
 
-def lib(asan=False, pa=0):
-    """asan: the AddressSanitizer build; pa: the build with pending arrays of `pa` entries (`make pa=<n>`)."""
-    key = ("asan" if asan else "plain") + (f"_pa{pa}" if pa else "")
+def lib(asan=False):
+    key = "asan" if asan else "plain"
     if key not in _L:
-        name = "libnfa_host" + ("_asan" if asan else "") + (f"_pa{pa}" if pa else "") + ".so"
-        p = os.path.join(HERE, "native", "build", name)
+        p = os.path.join(HERE, "native", "build", "libnfa_host_asan.so" if asan else "libnfa_host.so")
         L = ctypes.CDLL(p)
         L.h_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_size_t]
         L.h_destroy.argtypes = [ctypes.c_void_p]
@@ -41,24 +39,23 @@ class HarnessError(Exception):
 
 class HostHarnessApp:
     asan = False
-    pa = 0
     TYPES = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3, "STRING": 4, "BOOL": 5}
 
     def __init__(self, text):
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(1024)
-        rc = lib(self.asan, self.pa).h_create(text.encode(), ctypes.byref(h), err, 1024)
+        rc = lib(self.asan).h_create(text.encode(), ctypes.byref(h), err, 1024)
         if rc:
             raise HarnessError(rc, err.value.decode())
         self.h = h
 
     def close(self):
         if self.h:
-            lib(self.asan, self.pa).h_destroy(self.h)
+            lib(self.asan).h_destroy(self.h)
             self.h = None
 
     def start(self):
-        lib(self.asan, self.pa).h_start(self.h)
+        lib(self.asan).h_start(self.h)
 
     def send(self, sid, ts, row, types):
         arr = (HV * max(len(row), 1))()
@@ -77,22 +74,22 @@ class HostHarnessApp:
                 arr[k].i = 1 if v else 0
             else:
                 arr[k].i = int(v)
-        lib(self.asan, self.pa).h_send(self.h, sid.encode(), int(ts), arr)
+        lib(self.asan).h_send(self.h, sid.encode(), int(ts), arr)
 
     def advance_time(self, ts):
-        lib(self.asan, self.pa).h_advance(self.h, int(ts), 0)
+        lib(self.asan).h_advance(self.h, int(ts), 0)
 
     def advance_wallclock(self, ts):
-        lib(self.asan, self.pa).h_advance(self.h, int(ts), 1)
+        lib(self.asan).h_advance(self.h, int(ts), 1)
 
     def flush(self):
         err = ctypes.create_string_buffer(1024)
-        rc = lib(self.asan, self.pa).h_flush(self.h, err, 1024)
+        rc = lib(self.asan).h_flush(self.h, err, 1024)
         if rc:
             raise HarnessError(rc, err.value.decode())
 
     def outputs(self):
-        n = lib(self.asan, self.pa).h_dump(self.h, None, 0)
+        n = lib(self.asan).h_dump(self.h, None, 0)
         buf = ctypes.create_string_buffer(n + 1)
-        lib(self.asan, self.pa).h_dump(self.h, buf, n + 1)
+        lib(self.asan).h_dump(self.h, buf, n + 1)
         return json.loads(buf.value.decode())

@@ -130,20 +130,6 @@ def test_config5_variants_jit_equal_oracle(name):
     assert got == exp
 
 
-@pytest.mark.parametrize("cap", ["2", "7"])
-@pytest.mark.parametrize("name", ["pattern_count_not5s", "pattern_count_and_within"])
-def test_config5_pending_array_lds_head(name, cap, monkeypatch):
-    """The pending arrays' LDS head (opt-in, SM_NFA_PA=<entries>: read per JIT compile): the first `cap` entries of
-    each array in LDS, the rest in the HBM object, moved in at lane start and back at lane end; identical outputs."""
-    monkeypatch.setenv("SM_NFA_PA", cap)
-    sid, cols, ts = synth.gen5(0, 60_000, 300, 1)
-    text = synth.app5(VARIANTS[name])
-    exp = oracle_out(text, sid, cols, ts)
-    got, _ = product_out(text, sid, cols, ts, splits=(7_777, 40_001), nfa_jit=1)
-    assert len(exp["streams"].get("Out", [])) > 50
-    assert got == exp
-
-
 def _key_subsample(sid, cols, ts, keep_key):
     """The events of the keys `keep_key` selects, plus every other event that advances the playback clock as a
     heartbeat (stream -1): the clock is global (StreamJunction.sendData :232-237), so a key's timers must see the

@@ -13,19 +13,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 KATS = [k for k in load_kats() if "skip" not in k]
 
 
-@pytest.fixture(scope="module", params=[0, 2], ids=["lists", "pending_arrays2"])
-def harness(request):
-    """pending_arrays2: the build with the query-specialised kernel's LDS pending arrays (nfa_impl.h SM_NFA_PA) of 2
-    entries, so that most partials of a longer list go through the HBM part, the refills and the relink"""
-    pa = request.param
-    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")] + ([f"pa={pa}"] if pa else []))
+@pytest.fixture(scope="module")
+def harness():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
     from host_harness_lib import HostHarnessApp
-
-    class H(HostHarnessApp):
-        pass
-
-    H.pa = pa
-    return H
+    return HostHarnessApp
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])

@@ -27,19 +27,11 @@ EXTRA = {
 }
 
 
-@pytest.fixture(scope="module", params=[0, 3], ids=["lists", "pending_arrays3"])
-def harness(request):
-    """pending_arrays3: the build with the query-specialised kernel's LDS pending arrays (nfa_impl.h SM_NFA_PA) of 3
-    entries (most partials go through the HBM part, the refills and the relink at each flush)"""
-    pa = request.param
-    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")] + ([f"pa={pa}"] if pa else []))
+@pytest.fixture(scope="module")
+def harness():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
     from host_harness_lib import HostHarnessApp
-
-    class H(HostHarnessApp):
-        pass
-
-    H.pa = pa
-    return H
+    return HostHarnessApp
 
 
 def harness_out(H, text, sid, cols, ts, flush_every=0):
@@ -74,7 +66,7 @@ def test_variant_host_nfa_equals_oracle(harness, name):
     if name not in ("config5",):
         assert len(exp["streams"].get("Out", [])) > 20
     assert got["streams"].get("Out", []) == exp["streams"].get("Out", [])
-    if harness.pa and name not in ("config5",):  # lane runs cut into batches: arrays loaded and relinked each flush
+    if name not in ("config5",):  # the same stream cut into batches (lane state carried across flushes)
         got = harness_out(harness, text, sid, cols, ts, flush_every=7919)
         assert got["streams"].get("Out", []) == exp["streams"].get("Out", [])
 
