@@ -1372,7 +1372,9 @@ void run_pattern_query(sm_app* a, int qi, const EvArrays& ev, int64_t N, std::ve
   b.clock_in = ev.clock_in;
   if (h.nsched > 0 && ev.nadv > 0 && ev.nadv < INT32_MAX) {
     // timers: the clock index of the advance points (timer_fire finds a timer's due point with one load instead of a
-    // gallop), for a clock span of at most 2^26 values (256 MB of int32); wider spans keep the gallop
+    // gallop), for a clock span of at most 2^26 values (256 MB of int32); wider spans keep the gallop. The span's two
+    // ends are read back here: that waits for the work queued before it on the stream, which the NFA
+    // launch below waits for anyway, so the host loses one launch latency per batch, not device time
     int64_t ends[2];
     SM_HIP(hipMemcpyAsync(&ends[0], ev.adv_clock, 8, hipMemcpyDeviceToHost, hs));
     SM_HIP(hipMemcpyAsync(&ends[1], ev.adv_clock + ev.nadv - 1, 8, hipMemcpyDeviceToHost, hs));
