@@ -811,7 +811,8 @@ def main():
 # Kernels of the device pipelines (labels recorded by kernels/fastpath3.hip and kernels/filter.hip) and their
 # ALGORITHMIC bytes per launch for a batch of n events with m matches: what each launch must read
 # and write at minimum.
-KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_up", "j_pass", "j_pass_last",
+KERNELS = ["prep", "key_up", "scan", "key_pass0", "key_pass", "walk", "j_count", "j_tile", "j_up", "j_pass",
+           "j_pass_last",
            "stack_prep", "stack", "order", "carry_merge", "carry_out",
            "filter_count", "filter_scan", "filter_write",
            "event_index", "nfa_select", "nfa_group", "nfa_setup", "nfa"]
@@ -833,6 +834,8 @@ def alg_bytes(label, n, m, config):
             "order": 8 * m + 8 * m,         # staged pairs in, output pairs out (reference order)
             "carry_merge": 16 * m,
             "carry_out": 0,                 # open partials at the end of the batch (O(keys))
+            "j_count": 8 * m,               # (j, i) pairs in: pairs per output j-tile
+            "j_tile": 16 * m,               # (j, i) in (in i order) and out (in j order), once each
             "j_up": 4 * m,
             "j_pass": 16 * m,               # (j, i) in and out
             "j_pass_last": 16 * m,

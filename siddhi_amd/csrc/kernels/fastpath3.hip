@@ -1285,6 +1285,235 @@ void launch_walk(int spec, int G, hipStream_t s, const WalkArgs& wa, int64_t per
 #undef SM_WALK
 }
 
+// ---------------------------------------------------------------- j order by output tiles (round 6)
+// The unkeyed walk leaves its (j << 32) | i pairs chunk by chunk in i order; the output wants (j, i) order (the
+// reference emits at e2's arrival, the partials it completes oldest first). A match's j is at most D ordinals after
+// its i, and in the config-3 shape D is small (`within 1 sec` over one event per ms: D <= 1000). Then the pairs whose
+// j falls in an output tile of kJtTile ordinals all have i in [tile start - D, tile end): one workgroup per tile reads
+// that i range (binary search in the walk chunks that cover it), keeps the pairs whose j is in the tile, and places
+// them by a stable counting sort on j in LDS, i order kept within a j. That replaces the LSD j passes (an up-sweep and
+// a scatter of every pair per 10 bits of j) with one count pass and one read of about (kJtTile + D) / kJtTile of the
+// pairs. Batches with D > kJtDMax, or a tile with more than kJtCap pairs, keep the LSD passes.
+constexpr int kJtB = 11;
+constexpr uint32_t kJtTile = 1u << kJtB;  // output ordinals per tile
+constexpr uint32_t kJtCap = 4096;         // pairs a tile's workgroup holds in LDS
+constexpr uint32_t kJtDMax = 4 * kJtTile;
+constexpr int kJtThreads = 256;
+
+// Pairs per output tile (cnt[t], t = j >> kJtB, runs of equal tiles within a wave counted once), the largest j - i,
+// and where each i-tile's pairs start: P[u] = the staging index of the first pair with i >= u * kJtTile, for the
+// tiles whose first ordinal falls in this chunk's ordinal range [ord of its first event, ord of the next chunk's)
+// (ordinals rise with the batch position, so the chunks' ranges partition the ordinals; a tile with no pair in its
+// chunk points at the chunk's end). A tile's workgroup then finds its input with two loads instead of searches.
+__global__ void __launch_bounds__(256) jt_count_kernel(const uint64_t* __restrict__ stq,
+                                                       const uint32_t* __restrict__ mcount, int64_t perw, int Gw,
+                                                       const int64_t* __restrict__ ord, int64_t obase, int64_t n,
+                                                       uint32_t T, uint32_t* __restrict__ cnt,
+                                                       uint32_t* __restrict__ dmax, uint32_t* __restrict__ P) {
+  const int g = blockIdx.x, lane = threadIdx.x & 63;
+  const int64_t p0 = (int64_t)g * perw, p1 = p0 + perw;
+  if (p0 >= n) return;
+  auto ord_at = [&](int64_t p) { return ord ? (uint32_t)(ord[p] - obase) : (uint32_t)p; };
+  const uint32_t c0 = ord_at(p0);
+  const uint32_t u_first = (c0 + kJtTile - 1) >> kJtB;  // tiles whose first ordinal is in this chunk's range
+  const uint32_t u_end = p1 < n ? (ord_at(p1) + kJtTile - 1) >> kJtB : T;
+  const uint64_t* q = stq + p0;
+  const uint32_t m = mcount[g];
+  const uint32_t xbase = (uint32_t)p0;
+  if (g == 0 && threadIdx.x == 0) P[T] = (uint32_t)((int64_t)Gw * perw < 0xffffffffll ? Gw * perw : 0xffffffffll);
+  if (m == 0) {
+    for (uint32_t u = u_first + threadIdx.x; u < u_end; u += blockDim.x) P[u] = xbase;
+    return;
+  }
+  uint32_t dm = 0;
+  constexpr int kLd = 8;  // pairs per thread whose loads are in flight together
+  for (uint32_t b0 = (threadIdx.x >> 6) * 64u; b0 < m; b0 += blockDim.x * kLd) {
+    uint64_t vv[kLd];
+#pragma unroll
+    for (int r = 0; r < kLd; ++r) {
+      const uint32_t k = b0 + r * blockDim.x + lane;
+      vv[r] = k < m ? q[k] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kLd; ++r) {
+    const uint32_t b = b0 + r * blockDim.x;
+    const uint32_t k = b + lane;
+    const bool valid = k < m;
+    const uint64_t v = vv[r];
+    const uint32_t j = (uint32_t)(v >> 32), i = (uint32_t)v;
+    if (valid && j - i > dm) dm = j - i;
+    const uint32_t t = valid ? j >> kJtB : 0xffffffffu;
+    const uint32_t tp = __shfl_up(t, 1, 64);
+    const bool head = valid && (lane == 0 || t != tp);
+    const uint64_t hm = __ballot(head);
+    const uint32_t nv = (uint32_t)__popcll(__ballot(valid));
+    const uint64_t after = lane == 63 ? 0ull : hm >> (lane + 1);
+    const uint32_t next = after ? (uint32_t)lane + 1u + (uint32_t)__builtin_ctzll(after) : nv;
+    if (head) atomicAdd(&cnt[t], next - (uint32_t)lane);
+    const uint32_t ip = __shfl_up(i, 1, 64);  // the previous pair's i (lane 0: from memory)
+    if (valid) {  // i-tiles that start after the previous pair's i and at or before this one's: they start here
+      const uint32_t ui = i >> kJtB;
+      const uint32_t up = k == 0 ? u_first : (((lane == 0 ? (uint32_t)q[k - 1] : ip)) >> kJtB) + 1u;
+      for (uint32_t u = up > u_first ? up : u_first; u <= ui && u < u_end; ++u) P[u] = xbase + k;
+      if (k == m - 1)
+        for (uint32_t u = (ui + 1 > u_first ? ui + 1 : u_first); u < u_end; ++u) P[u] = xbase + m;
+    }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t x = __shfl_xor(dm, o, 64);
+    dm = x > dm ? x : dm;
+  }
+  if (lane == 0) atomicMax(dmax, dm);
+}
+
+// output tile blockIdx.x: off[t] = pairs before the tile (exclusive scan of the counts over T + 1 entries); its input
+// is the staging range [P[i-tile of t0 - D], P[t + 1]), walk chunk by chunk (pairs at [g perw, g perw + mcount[g]))
+constexpr int kJtLd = 8;  // staged pairs per thread and load round (their loads are in flight together)
+__global__ void __launch_bounds__(kJtThreads) jt_place_kernel(const uint64_t* __restrict__ stq,
+                                                              const uint32_t* __restrict__ mcount, int64_t perw,
+                                                              const uint32_t* __restrict__ P,
+                                                              const uint32_t* __restrict__ off, uint32_t D,
+                                                              uint64_t* __restrict__ out, uint32_t* __restrict__ err) {
+  constexpr int kJtW = kJtThreads / 64;
+  __shared__ uint64_t a[kJtCap];
+  __shared__ __attribute__((aligned(4))) uint16_t cw[kJtW][kJtTile];  // per (wave, j): count, then cursor
+  __shared__ uint32_t wsum[kJtThreads / 64];
+  __shared__ uint32_t wrc[kJtLd][kJtThreads / 64];
+  __shared__ uint32_t s_n;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t K = off[t + 1] - off[t];
+  if (K == 0) return;
+  if (K > kJtCap) {  // the whole batch takes the LSD passes
+    if (tid == 0) atomicOr(err, 1u);
+    return;
+  }
+  const uint32_t t0 = (uint32_t)t << kJtB, t1 = t0 + kJtTile;
+  const uint32_t lo_i = t0 > D ? t0 - D : 0u;
+  const uint32_t x0 = P[lo_i >> kJtB], x1 = P[t + 1];
+  for (uint32_t x = tid; x < kJtW * kJtTile / 2; x += kJtThreads) ((uint32_t*)&cw[0][0])[x] = 0;
+  if (tid == 0) s_n = 0;
+  const uint64_t lt = lanemask_lt();
+  lds_barrier();
+  for (uint32_t g = x0 / (uint32_t)perw; x0 < x1 && g <= (x1 - 1) / (uint32_t)perw; ++g) {
+    const uint32_t gb = g * (uint32_t)perw;
+    const uint32_t b0 = x0 > gb ? x0 - gb : 0u;
+    const uint32_t m = mcount[g];
+    const uint32_t b1 = x1 - gb < m ? x1 - gb : m;
+    const uint64_t* q = stq + gb;
+    for (uint32_t b = b0; b < b1; b += kJtThreads * kJtLd) {  // the tile's pairs, compacted in i order
+      uint64_t v[kJtLd];
+#pragma unroll
+      for (int r = 0; r < kJtLd; ++r) {
+        const uint32_t k = b + r * kJtThreads + tid;
+        v[r] = k < b1 ? q[k] : 0ull;
+      }
+      // the round's selected pairs in (r, wave, lane) order = i order: per (r, wave) counts, then one prefix
+      uint64_t bal[kJtLd];
+#pragma unroll
+      for (int r = 0; r < kJtLd; ++r) {
+        const uint32_t k = b + r * kJtThreads + tid;
+        const uint32_t j = (uint32_t)(v[r] >> 32);
+        bal[r] = __ballot(k < b1 && j >= t0 && j < t1);
+        if (lane == 0) wrc[r][w] = (uint32_t)__popcll(bal[r]);
+      }
+      lds_barrier();
+      uint32_t run = s_n;
+#pragma unroll
+      for (int r = 0; r < kJtLd; ++r) {
+        uint32_t o = run;
+#pragma unroll
+        for (int x = 0; x < kJtThreads / 64; ++x) {
+          if (x < w) o += wrc[r][x];
+          run += wrc[r][x];
+        }
+        if ((bal[r] >> lane) & 1ull) {
+          const uint32_t idx = o + (uint32_t)__popcll(bal[r] & lt);
+          if (idx < kJtCap) a[idx] = v[r];
+        }
+      }
+      lds_barrier();  // every thread read s_n and the counts
+      if (tid == 0) s_n = run;
+      lds_barrier();
+    }
+  }
+  if (s_n != K) {  // the counts and the tile's pairs disagree: never expected; the LSD passes take the batch
+    if (tid == 0) atomicOr(err, 2u);
+    return;
+  }
+  // stable placement by all waves: wave w takes the quarter [q0, q1) of the tile's pairs; per (wave, j) counts, then
+  // per (wave, j) cursors = j's start + the counts of the earlier quarters, so each wave places its pairs after every
+  // earlier pair of the same j
+  const uint32_t q0 = (uint32_t)(((uint64_t)K * (uint32_t)w) / kJtW);
+  const uint32_t q1 = (uint32_t)(((uint64_t)K * (uint32_t)(w + 1)) / kJtW);
+  uint32_t* cw32 = (uint32_t*)&cw[0][0];
+  for (uint32_t x = q0 + lane; x < q1; x += 64) {
+    const uint32_t jo = (uint32_t)(a[x] >> 32) - t0;
+    atomicAdd(&cw32[w * (kJtTile / 2) + (jo >> 1)], 1u << (16 * (jo & 1)));
+  }
+  lds_barrier();
+  {  // thread tid owns kPer consecutive j's: totals, block scan, per-wave cursors
+    constexpr int kPer = kJtTile / kJtThreads;
+    uint32_t tot[kPer], s = 0;
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      const uint32_t jo = tid * kPer + x;
+      tot[x] = 0;
+#pragma unroll
+      for (int v = 0; v < kJtW; ++v) tot[x] += cw[v][jo];
+      s += tot[x];
+    }
+    uint32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    lds_barrier();
+    uint32_t base = inc - s;
+    for (int x = 0; x < w; ++x) base += wsum[x];
+#pragma unroll
+    for (int x = 0; x < kPer; ++x) {
+      const uint32_t jo = tid * kPer + x;
+      uint32_t st = base;
+#pragma unroll
+      for (int v = 0; v < kJtW; ++v) {
+        const uint32_t c = cw[v][jo];
+        cw[v][jo] = (uint16_t)st;
+        st += c;
+      }
+      base += tot[x];
+    }
+  }
+  lds_barrier();
+  uint64_t* o = out + off[t];
+  for (uint32_t b = q0; b < q1; b += 64) {
+    const uint32_t k = b + lane;
+    const bool valid = k < q1;
+    const uint64_t v = valid ? a[k] : 0ull;
+    const uint32_t jo = valid ? (uint32_t)(v >> 32) - t0 : 0u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bb = 0; bb < kJtB; ++bb) {
+      const uint64_t bl = __ballot((jo >> bb) & 1u);
+      peers &= ((jo >> bb) & 1u) ? bl : ~bl;
+    }
+    const uint32_t below = (uint32_t)__popcll(peers & lt);
+    const uint32_t c = valid ? (uint32_t)cw[w][jo] : 0u;
+    wave_lockstep();
+    if (valid && below == 0) cw[w][jo] = (uint16_t)(c + (uint32_t)__popcll(peers));
+    wave_lockstep();
+    if (valid) o[c + below] = v;
+  }
+}
+
+// j order by tiles: on by default; SM_JTILE=0 keeps the LSD passes (A/B and tests; read per batch)
+bool jtile_on() {
+  const char* e = getenv("SM_JTILE");
+  return !(e && e[0] == '0');
+}
+
 // record passes with the write-combining down-sweep (SM_SORT_WC=0 selects the plain one, for comparison)
 bool sort_wc() {
   static const bool on = [] {
@@ -1795,6 +2024,23 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   }
   fs.last_path = 2;
   tmark("walk");
+  // j order by output tiles (unkeyed walk, jt_place_kernel): pairs per tile and the largest j - i, read back with the
+  // match counts below
+  const int64_t jt_T = keyed ? 0 : (int64_t)(hc.omax >> kJtB) + 1;
+  const bool jt_try = !keyed && jtile_on() && jt_T <= ((int64_t)1 << 22) && (int64_t)Gw * perw < 0xffffffffll;
+  uint32_t* jt_cnt = nullptr;
+  uint32_t* jt_misc = nullptr;  // [0] largest j - i, [1] placement error
+  uint32_t* jt_P = nullptr;      // staging index where each i-tile's pairs start (T + 1 entries)
+  if (jt_try) {
+    jt_cnt = (uint32_t*)sc.take((size_t)(jt_T + 1) * 4);
+    jt_misc = (uint32_t*)sc.take(8);
+    jt_P = (uint32_t*)sc.take((size_t)(jt_T + 1) * 4);
+    SM_HIP(hipMemsetAsync(jt_cnt, 0, (size_t)(jt_T + 1) * 4, s));
+    SM_HIP(hipMemsetAsync(jt_misc, 0, 8, s));
+    hipLaunchKernelGGL(jt_count_kernel, dim3(Gw), dim3(256), 0, s, stq, mcount, perw, Gw, a.ordinals, a.ordinal_base,
+                       n, (uint32_t)jt_T, jt_cnt, jt_misc, jt_P);
+    tmark("j_count");
+  }
   if (tm) SM_HIP(hipEventRecord(tm->ev[2], s));
 
   // carried partials against this batch (before the walk's records are overwritten by the j passes)
@@ -1850,6 +2096,8 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
   scan_counts(Gw);
   uint32_t hcf[2];
   SM_HIP(hipMemcpyAsync(hcf, cflags, 8, hipMemcpyDeviceToHost, s));
+  uint32_t hjd = 0xffffffffu;
+  if (jt_try) SM_HIP(hipMemcpyAsync(&hjd, jt_misc, 4, hipMemcpyDeviceToHost, s));
   SM_HIP(hipStreamSynchronize(s));
   if (hcf[1]) {
     sc.used = mark;
@@ -1865,7 +2113,22 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     throw std::runtime_error("match buffer too small");
   }
   uint64_t* mainq = (uint64_t*)pairs_out;
-  if (M > 0) {
+  bool jt_done = false;
+  if (M > 0 && jt_try && hjd <= kJtDMax) {
+    uint64_t* tgt = Mc == 0 ? (uint64_t*)pairs_out : pq;
+    exclusive_scan_u32(jt_cnt, (size_t)jt_T + 1, sc, s);
+    hipLaunchKernelGGL(jt_place_kernel, dim3((unsigned)jt_T), dim3(kJtThreads), 0, s, stq, mcount, perw, jt_P, jt_cnt,
+                       hjd, tgt, jt_misc + 1);
+    tmark("j_tile");
+    uint32_t herr = 0;
+    SM_HIP(hipMemcpyAsync(&herr, jt_misc + 1, 4, hipMemcpyDeviceToHost, s));
+    SM_HIP(hipStreamSynchronize(s));
+    if (herr == 0) {
+      jt_done = true;
+      mainq = tgt;
+    }
+  }
+  if (M > 0 && !jt_done) {
     const int64_t perM = round_up((M + G - 1) / G, kTile);
     const uint64_t* cq = stq;
     uint64_t* outs[2] = {pq, qq};

@@ -510,3 +510,68 @@ def test_spilled_stacks_carried_into_key_range(stack):
     got, paths = _paths_and_pairs(text, cols, ts, list(zip(bounds[:-1], bounds[1:])), stack=stack)
     assert paths == [3 if stack == 1 else 2] * 3, paths
     np.testing.assert_array_equal(got, exp)
+
+
+def _run_unkeyed(text, cols, ts, ranges, ordinals=None):
+    """run_stream for the unkeyed walk with phase timing on: the pairs, and whether the j-tile kernel ran."""
+    import torch
+    from siddhi_amd.testing import ProductApp
+    app = ProductApp(text, fast_stack=2, fast_timing=1)
+    dev = torch.device("cuda", 0)
+    got, tiled = [], 0
+    for lo, hi in ranges:
+        tcols = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
+        tts = torch.from_numpy(np.ascontiguousarray(ts[lo:hi], dtype=np.int64)).to(dev)
+        tord = None if ordinals is None else torch.from_numpy(np.ascontiguousarray(ordinals[lo:hi])).to(dev)
+        base = lo if ordinals is None else 0
+        torch.cuda.synchronize()
+        app.process_device_batch("StockStream", tts, tcols, ordinals=tord, ordinal_base=base)
+        tiled += int(app.get_stat("kernel_calls:j_tile"))
+        got.append(app.device_matches_host("q").view(np.int32).astype(np.int64) + base)
+    app.close()
+    return np.concatenate(got), tiled
+
+
+@pytest.mark.parametrize("case", ["spikes", "sharded", "window_8s_spikes", "long_wait", "no_within"])
+def test_unpartitioned_j_tile_order(case, monkeypatch):
+    """Round 6: the unkeyed walk's (e1, e2) pairs put in e2 order by output tiles of 2048 ordinals (fastpath3.hip
+    jt_place_kernel) when no match lies more than 8192 ordinals after its e1; otherwise, or when a tile holds more
+    than 4096 pairs, by the LSD j passes. Both equal the oracle: price spikes that complete hundreds to thousands of
+    partials at one e2 (ties of j, i ascending), sharded ordinals with gaps, ragged batches with carried partials, and
+    windows past the tile path's reach."""
+    n = 60000
+    rng = np.random.default_rng(11)
+    price = rng.uniform(21.0, 60.0, n)
+    within = " within 1 sec"
+    if case in ("spikes", "sharded"):
+        price[rng.integers(0, n, n // 300)] = 1000.0  # each spike completes every pending partial of the last second
+    if case == "window_8s_spikes":
+        within = " within 8 sec"
+        price[np.arange(7000, n, 7000)] = 1000.0  # ~7000 partials per spike: more than a tile's workgroup holds
+    if case == "long_wait":  # a falling run of 10000 events, then a spike: a match 10000 ordinals after its e1
+        within = " within 30 sec"
+        price[20000:30000] = np.linspace(59.0, 21.5, 10000)
+        price[30000] = 1000.0
+    if case == "no_within":
+        within = ""
+    sym = rng.integers(0, 10, n).astype(np.int32)
+    vol = rng.integers(0, 2000, n).astype(np.int64)
+    tsa = np.arange(n, dtype=np.int64)
+    cols = [sym, price, vol, tsa]
+    text = app_text(partitioned=False, within=within)
+    exp = oracle_pairs(text, cols, tsa)
+    ordinals = None
+    if case == "sharded":  # this rank's events carry global ordinals 3 k + 1 (gaps of two)
+        ordinals = 3 * np.arange(n, dtype=np.int64) + 1
+        exp = 3 * exp + 1
+    ranges = [(0, n)] if case == "long_wait" else pieces(n, [1, 8191, 20000])
+    got, tiled = _run_unkeyed(text, cols, tsa, ranges, ordinals)
+    np.testing.assert_array_equal(got, exp)
+    if case in ("spikes", "sharded"):
+        assert tiled > 0
+    if case == "long_wait":
+        assert tiled == 0
+    monkeypatch.setenv("SM_JTILE", "0")
+    lsd, tiled0 = _run_unkeyed(text, cols, tsa, ranges, ordinals)
+    assert tiled0 == 0
+    np.testing.assert_array_equal(lsd, exp)

@@ -21,7 +21,7 @@ from bench import alg_bytes  # noqa: E402
 
 OUT = os.path.join(ROOT, "gpurun_out", os.environ.get("PROF_DIR", "."))
 # kernel-name fragment -> bench label (first match wins)
-FAMILIES = [("walk_kernel<", "walk"), ("pass0_kernel", "key_pass0"), ("downsweep_wc_kernel<0", "key_pass0"), ("downsweep_kernel<0", "key_pass0"),
+FAMILIES = [("walk_kernel<", "walk"), ("jt_count_kernel", "j_count"), ("jt_place_kernel", "j_tile"), ("pass0_kernel", "key_pass0"), ("downsweep_wc_kernel<0", "key_pass0"), ("downsweep_kernel<0", "key_pass0"),
             ("downsweep_wc_kernel<1", "key_pass"), ("downsweep_kernel<1", "key_pass"),
             ("downsweep_wc_kernel<2", "j_pass*"), ("downsweep_kernel<2", "j_pass*"),
             ("upsweep_kernel<sm::(anonymous namespace)::KeyColDigits", "key_up"),
