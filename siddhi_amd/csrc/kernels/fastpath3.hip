@@ -1305,16 +1305,21 @@ constexpr int kJtThreads = 256;
 // tiles whose first ordinal falls in this chunk's ordinal range [ord of its first event, ord of the next chunk's)
 // (ordinals rise with the batch position, so the chunks' ranges partition the ordinals; a tile with no pair in its
 // chunk points at the chunk's end). A tile's workgroup then finds its input with two loads instead of searches.
-__global__ void __launch_bounds__(256) jt_count_kernel(const uint64_t* __restrict__ stq,
+__global__ void __launch_bounds__(1024) jt_count_kernel(const uint64_t* __restrict__ stq,
                                                        const uint32_t* __restrict__ mcount, int64_t perw, int Gw,
                                                        const int64_t* __restrict__ ord, int64_t obase, int64_t n,
                                                        uint32_t T, uint32_t* __restrict__ cnt,
                                                        uint32_t* __restrict__ dmax, uint32_t* __restrict__ P) {
+  constexpr uint32_t kLoc = 256;  // output tiles from the chunk's first one counted in LDS, flushed once
+  __shared__ uint32_t lcnt[kLoc];
   const int g = blockIdx.x, lane = threadIdx.x & 63;
   const int64_t p0 = (int64_t)g * perw, p1 = p0 + perw;
   if (p0 >= n) return;
+  for (uint32_t x = threadIdx.x; x < kLoc; x += blockDim.x) lcnt[x] = 0;
+  __syncthreads();
   auto ord_at = [&](int64_t p) { return ord ? (uint32_t)(ord[p] - obase) : (uint32_t)p; };
   const uint32_t c0 = ord_at(p0);
+  const uint32_t tbase = c0 >> kJtB;  // a pair's e2 is after its e1: no tile below this one
   const uint32_t u_first = (c0 + kJtTile - 1) >> kJtB;  // tiles whose first ordinal is in this chunk's range
   const uint32_t u_end = p1 < n ? (ord_at(p1) + kJtTile - 1) >> kJtB : T;
   const uint64_t* q = stq + p0;
@@ -1323,7 +1328,7 @@ __global__ void __launch_bounds__(256) jt_count_kernel(const uint64_t* __restric
   if (g == 0 && threadIdx.x == 0) P[T] = (uint32_t)((int64_t)Gw * perw < 0xffffffffll ? Gw * perw : 0xffffffffll);
   if (m == 0) {
     for (uint32_t u = u_first + threadIdx.x; u < u_end; u += blockDim.x) P[u] = xbase;
-    return;
+    return;  // (uniform: nothing was counted)
   }
   uint32_t dm = 0;
   constexpr int kLd = 8;  // pairs per thread whose loads are in flight together
@@ -1349,7 +1354,10 @@ __global__ void __launch_bounds__(256) jt_count_kernel(const uint64_t* __restric
     const uint32_t nv = (uint32_t)__popcll(__ballot(valid));
     const uint64_t after = lane == 63 ? 0ull : hm >> (lane + 1);
     const uint32_t next = after ? (uint32_t)lane + 1u + (uint32_t)__builtin_ctzll(after) : nv;
-    if (head) atomicAdd(&cnt[t], next - (uint32_t)lane);
+    if (head) {
+      if (t - tbase < kLoc) atomicAdd(&lcnt[t - tbase], next - (uint32_t)lane);
+      else atomicAdd(&cnt[t], next - (uint32_t)lane);
+    }
     const uint32_t ip = __shfl_up(i, 1, 64);  // the previous pair's i (lane 0: from memory)
     if (valid) {  // i-tiles that start after the previous pair's i and at or before this one's: they start here
       const uint32_t ui = i >> kJtB;
@@ -1365,6 +1373,9 @@ __global__ void __launch_bounds__(256) jt_count_kernel(const uint64_t* __restric
     dm = x > dm ? x : dm;
   }
   if (lane == 0) atomicMax(dmax, dm);
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < kLoc; x += blockDim.x)
+    if (lcnt[x] && tbase + x < T) atomicAdd(&cnt[tbase + x], lcnt[x]);
 }
 
 // output tile blockIdx.x: off[t] = pairs before the tile (exclusive scan of the counts over T + 1 entries); its input
@@ -2037,7 +2048,7 @@ int64_t fast_every_within_v2(const FastArgs& a, const FastHostInfo& hi, FastStat
     jt_P = (uint32_t*)sc.take((size_t)(jt_T + 1) * 4);
     SM_HIP(hipMemsetAsync(jt_cnt, 0, (size_t)(jt_T + 1) * 4, s));
     SM_HIP(hipMemsetAsync(jt_misc, 0, 8, s));
-    hipLaunchKernelGGL(jt_count_kernel, dim3(Gw), dim3(256), 0, s, stq, mcount, perw, Gw, a.ordinals, a.ordinal_base,
+    hipLaunchKernelGGL(jt_count_kernel, dim3(Gw), dim3(1024), 0, s, stq, mcount, perw, Gw, a.ordinals, a.ordinal_base,
                        n, (uint32_t)jt_T, jt_cnt, jt_misc, jt_P);
     tmark("j_count");
   }
