@@ -32,6 +32,7 @@
 
 #include "fastpath.h"
 #include "stack_dev.h"
+#include "order_dev.h"
 
 namespace sm {
 
@@ -72,6 +73,9 @@ constexpr int kOCap = kOCapMax >= 12288 ? 12288 : (kOCapMax >= 8192 ? kOCapMax :
 #define SM_ORDER_GT (SM_ORDER_TB >= 15 ? 4 : SM_ORDER_TB == 14 ? 8 : 16)  // A/B build flag
 #endif
 constexpr int kGT = SM_ORDER_GT;  // consecutive tiles per order workgroup
+#ifndef SM_ORDER_V1
+#define SM_ORDER_V1 0  // A/B build flag: 1 = this round-3 order kernel instead of order2_kernel (order_dev.h)
+#endif
 #ifndef SM_ORDER_XCD
 #define SM_ORDER_XCD 0  // A/B build flag: 1 = XCD-contiguous tile groups (blocks b and b + 8 share an XCD and its L2)
 #endif
@@ -509,14 +513,6 @@ __global__ void __launch_bounds__(256) transpose_kernel(const uint32_t* __restri
     if (c < cols) dst[c * kBins + r0 + tx] = tile[tx][k];
   }
 }
-
-struct OrderArgs {
-  const uint64_t* stage;
-  const uint32_t* sbase;
-  const uint32_t* mt;  // [t][d]: matches of bucket d whose j precedes tile t
-  int64_t ntiles;
-  uint64_t* out;
-};
 
 // Tiles [blockIdx.x * kGT, +kGT) of kOT ordinals each, in order. Per tile, bucket d's staged matches with j in
 // the tile are one contiguous segment in (j, i) order (a j's matches are consecutive in it); 16 lanes read a
@@ -1055,7 +1051,24 @@ int64_t stack_pipeline(const StackPlan& p, const FastArgs& a, const FastHostInfo
       // 80 KB of LDS: exact, 8.5 against 6.75 ms; the same 16 waves per CU, more passes over longer segments; and the
       // next tile's first matches loaded during this tile's scan and placement: 7.6 ms, 18 VGPRs spilled; and
       // nontemporal stores of the output image: 6.58 against 6.48 ms)
-      hipLaunchKernelGGL(order_kernel, dim3((unsigned)((sa.ntiles + kGT - 1) / kGT)), dim3(kOB), 0, s, oa);
+      if (SM_ORDER_V1)
+        hipLaunchKernelGGL(order_kernel, dim3((unsigned)((sa.ntiles + kGT - 1) / kGT)), dim3(kOB), 0, s, oa);
+      else  // round 6: LDS images, loading and storing waves apart (order_dev.h)
+        hipLaunchKernelGGL(order2_kernel, dim3((unsigned)((sa.ntiles + kGT2 - 1) / kGT2)), dim3(kOB), 0, s, oa);
+#if SM_ORDER2_STAMPS
+      {
+        unsigned long long h[8];
+        SM_HIP(hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_o2_stamps), sizeof(h), 0, hipMemcpyDeviceToHost, s));
+        SM_HIP(hipStreamSynchronize(s));
+        double tot = 0;
+        for (unsigned long long v : h) tot += v;
+        fprintf(stderr, "[order2 phases] prologue %.3f issue %.3f count %.3f scan %.3f place %.3f land %.3f writes %.3f "
+                "desc %.3f\n", h[0] / tot, h[6] / tot, h[1] / tot, h[2] / tot, h[3] / tot, h[7] / tot, h[4] / tot,
+                h[5] / tot);
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        SM_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_o2_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+      }
+#endif
     }
   }
   tmark("order");

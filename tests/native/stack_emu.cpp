@@ -5,6 +5,7 @@
 // fault be found with AddressSanitizer instead of on the GPU.
 #define SM_HOST_EMU 1
 #include "../../siddhi_amd/csrc/kernels/stack_dev.h"
+#include "../../siddhi_amd/csrc/kernels/order_dev.h"
 
 #include "emu_fibers.h"
 
@@ -67,5 +68,19 @@ int sm_stack4_emu_consts(int* out) {  // kBins, kKeys, kTB, kQ, kSS, kR, kC
   out[5] = kR;
   out[6] = kC;
   return 0;
+}
+
+// One launch of order2_kernel (order_dev.h) over staged matches: bucket d's run at stage[sbase[d] ..), mt[t][d] =
+// matches of bucket d whose j precedes tile t (ntiles + 1 rows of kBins). Returns the kernel's image capacity.
+int sm_order2_emu(const uint64_t* stage, const uint32_t* sbase, const uint32_t* mt, int64_t ntiles, uint64_t* out) {
+  using namespace sm;
+  OrderArgs a{};
+  a.stage = stage;
+  a.sbase = sbase;
+  a.mt = mt;
+  a.ntiles = ntiles;
+  a.out = out;
+  emu_launch((int)((ntiles + kGT2 - 1) / kGT2), kOB, [&] { order2_kernel(a); });
+  return kOC2;
 }
 }
