@@ -44,7 +44,7 @@ constexpr int kLP = (kOC2 + kOB - 1) / kOB;  // image entries per thread
 constexpr int kLP1 = kLP;
 static_assert(kOT == 8 * kOB, "eight u16 counts (one 16-byte LDS word) per thread in the scan");
 static_assert(kBins == kOB && kOB == 1024, "one bucket per thread");
-static_assert(kLP <= 8, "a thread's image entries fit 8 bits of start flags");
+static_assert(kLP == 8 && kOC2 % kLP == 0 && kOC2 <= kLP * kOB, "a thread's block of the image: eight entries, whole");
 static_assert(kOC2 < 65536 && (size_t)kOT * 4 <= (size_t)kOC2 * 8, "u16 offsets; the u32 overflow counts alias the input image");
 
 __device__ __forceinline__ uint32_t o2_j(uint64_t v) { return (uint32_t)(v >> 32); }
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
   const int64_t T = a.ntiles;
   const uint32_t* inj = (const uint32_t*)inb + 1;  // j of image entry e: inj[2 e]
   unsigned long long o2_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, o2_last = SM_O2_CLOCK();
-  // phases: 0 prologue 1 count 2 scan 3 place 4 image hand-over + output writes 5 descriptor
+  // phases: 0 prologue 6 issue 1 count 2 scan 3 place 7 land 4 output writes 5 descriptor
 
   // descriptor of bucket tid's segment [lo, hi) of its run (block scan: one barrier; the writes become visible at
   // the caller's next barrier); returns the tile's total
@@ -158,34 +158,46 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
       if (more) issue(tnext);
       SM_O2_PHASE(6);
       if (!ovf) {
-        // run lengths: at the first match of each j-run (the entry before it is another j: of this bucket, or of
-        // another bucket, which never has this j); every read issued before the first use
-        uint32_t jj[kLP1], jp[kLP1], jn[kLP1];
+        // runs: thread tid takes the kLP consecutive entries [e0, e0 + kLP) (kLP1 16-byte reads); run starts, run
+        // lengths and ranks come from register compares, LDS only at the block's edges (a run crossing one: rare).
+        // The entry before a run's first is another j: of this bucket, or of another bucket, which never has it.
+        const uint32_t e0 = (uint32_t)tid * kLP;
+        uint32_t jj[kLP], rk8[kLP];
+        if (e0 < tcur) {
+          const uint4* b4 = (const uint4*)inb + e0 / 2;
 #pragma unroll
-        for (int k = 0; k < kLP1; ++k) {
-          const uint32_t e = (uint32_t)(tid + k * kOB);
-          const uint32_t ec = e < (uint32_t)kOC2 ? e : (uint32_t)kOC2 - 1u;
-          jj[k] = inj[2 * ec];
-          jp[k] = inj[2 * (ec ? ec - 1u : 0u)];
-          jn[k] = inj[2 * (ec + 1u < (uint32_t)kOC2 ? ec + 1u : ec)];
-        }
-        uint32_t stf = 0;  // bit k: entry k starts its run
-#pragma unroll
-        for (int k = 0; k < kLP1; ++k) {
-          const uint32_t e = (uint32_t)(tid + k * kOB);
-          const bool valid = e < tcur;
-          const bool st = valid && (e == 0 || jp[k] != jj[k]);
-          stf |= st ? 1u << k : 0u;
-          if (st) {
-            uint32_t n = 1;
-            if (e + 1 < tcur && jn[k] == jj[k]) {  // a longer run (rare): walk it
-              n = 2;
-              const uint32_t eo = o2_opaque(e);  // no hoisted per-k addresses (they spill; a scratch reload would
-                                                 // wait for the next tile's loads in flight)
-              while (eo + n < tcur && inj[2 * (eo + n)] == jj[k]) ++n;
-            }
-            c16[jj[k] - j0] = (uint16_t)n;
+          for (int q = 0; q < kLP / 2; ++q) {
+            const uint4 x = b4[q];
+            jj[2 * q] = x.y;
+            jj[2 * q + 1] = x.w;
           }
+          const uint32_t nv = tcur - e0 < (uint32_t)kLP ? tcur - e0 : (uint32_t)kLP;  // valid entries of the block
+          // rank of each entry in its run (the first one's run may come from the block before)
+          uint32_t r0 = 0;
+          if (e0 > 0 && inj[2 * (e0 - 1)] == jj[0]) {
+            const uint32_t eo = o2_opaque(e0);  // no hoisted (spilled) addresses: a scratch reload would wait for
+            r0 = 1;                             // the next tile's loads in flight
+            while (r0 < eo && inj[2 * (eo - r0 - 1)] == jj[0]) ++r0;
+          }
+          rk8[0] = r0;
+#pragma unroll
+          for (int k = 1; k < kLP; ++k) rk8[k] = jj[k] == jj[k - 1] ? rk8[k - 1] + 1u : 0u;
+          // length of the run from each entry to its end (the last one's may go on into the next block)
+          uint32_t ln[kLP];
+          {
+            uint32_t x = 0;
+            if (nv == (uint32_t)kLP && e0 + kLP < tcur && inj[2 * (e0 + kLP)] == jj[kLP - 1]) {
+              const uint32_t eo = o2_opaque(e0 + kLP), to = o2_opaque(tcur);
+              x = 1;
+              while (eo + x < to && inj[2 * (eo + x)] == jj[kLP - 1]) ++x;
+            }
+            ln[kLP - 1] = 1u + x;
+          }
+#pragma unroll
+          for (int k = kLP - 2; k >= 0; --k) ln[k] = 1u + ((uint32_t)(k + 1) < nv && jj[k + 1] == jj[k] ? ln[k + 1] : 0u);
+#pragma unroll
+          for (int k = 0; k < kLP; ++k)
+            if ((uint32_t)k < nv && rk8[k] == 0u) c16[jj[k] - j0] = (uint16_t)ln[k];
         }
         lds_barrier();
         SM_O2_PHASE(1);
@@ -207,20 +219,17 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
         lds_barrier();
         SM_O2_PHASE(2);
         // placement: offset of the j + rank in its run
-        uint32_t off[kLP1];
+        if (e0 < tcur) {
+          const uint32_t nv = tcur - e0 < (uint32_t)kLP ? tcur - e0 : (uint32_t)kLP;
+          uint32_t off[kLP];
 #pragma unroll
-        for (int k = 0; k < kLP1; ++k) off[k] = c16[(jj[k] - j0) & (kOT - 1)];
+          for (int k = 0; k < kLP; ++k) off[k] = c16[(jj[k] - j0) & (kOT - 1)];
+          const uint4* b4 = (const uint4*)inb + e0 / 2;
 #pragma unroll
-        for (int k = 0; k < kLP1; ++k) {
-          const uint32_t e = (uint32_t)(tid + k * kOB);
-          if (e < tcur) {
-            uint32_t rk = 0;
-            if (!((stf >> k) & 1u)) {  // inside a run: count back to its start
-              rk = 1;
-              const uint32_t eo = o2_opaque(e);
-              while (rk < eo && inj[2 * (eo - rk - 1)] == jj[k]) ++rk;
-            }
-            obuf[off[k] + rk] = inb[e];
+          for (int q = 0; q < kLP / 2; ++q) {
+            const uint4 x = b4[q];
+            if ((uint32_t)(2 * q) < nv) obuf[off[2 * q] + rk8[2 * q]] = ((uint64_t)x.y << 32) | x.x;
+            if ((uint32_t)(2 * q + 1) < nv) obuf[off[2 * q + 1] + rk8[2 * q + 1]] = ((uint64_t)x.w << 32) | x.z;
           }
         }
         lds_barrier();
@@ -264,6 +273,7 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
       // stores, so the wait does not include those), then this tile's output, and clear the counts
       if (more) land(tnext);
       mD = o2_opaque(mD);  // waited for here, with the entries, not after this tile's stores
+      SM_O2_PHASE(7);
       SM_O2_PHASE(7);
       if (!ovf)
         for (uint32_t k = tid; k < tcur; k += kOB) a.out[out + k] = obuf[k];
