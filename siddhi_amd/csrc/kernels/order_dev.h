@@ -14,7 +14,7 @@
 //     bucket has that j), block scan of the counts, placement of match e at offset(j) + (e - start of its run)
 //     into an LDS output image;
 //   * then waves 0-7 write the output image (coalesced) while waves 8-15 load the NEXT tile's segments into the
-//     input image (flat over image entries through an entry -> bucket map, so a wave instruction reads 64
+//     input image (flat over image entries through a per-entry staging index, so a wave instruction reads 64
 //     consecutive entries of about eleven segments), and the mt row of the tile after it. The loading waves never store and the
 //     storing waves never load, so neither waits for the other's memory traffic.
 // A tile with more matches than the images hold (dense matches: kOC2 per 2^kTB ordinals) takes a slower exact path:
@@ -37,9 +37,9 @@ struct OrderArgs {
 #define SM_ORDER2_GT 32  // A/B build flag: consecutive tiles per order2 workgroup (the pipeline's prologue is per group)
 #endif
 constexpr int kGT2 = SM_ORDER2_GT;
-// the two images (8-byte matches) in what the counts, the load descriptors and the scan words leave of 160 KB
-// (and the u16 entry -> bucket map)
-constexpr int kOC2 = ((160 * 1024 - kOT * 2 - 2 * kBins * 4 - 256) / 18) & ~7;
+// the two images (8-byte matches) and the next tile's staging index per entry (4 bytes) in what the counts and the
+// scan words leave of 160 KB
+constexpr int kOC2 = ((160 * 1024 - kOT * 2 - 256) / 20) & ~7;
 constexpr int kLP = (kOC2 + kOB - 1) / kOB;  // image entries per thread
 constexpr int kLP1 = kLP;
 static_assert(kOT == 8 * kOB, "eight u16 counts (one 16-byte LDS word) per thread in the scan");
@@ -80,8 +80,7 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t inb[kOC2];   // the tile's segments, bucket after bucket
   __shared__ __attribute__((aligned(16))) uint64_t obuf[kOC2];  // the tile's output
   __shared__ __attribute__((aligned(16))) uint16_t c16[kOT];    // run length of each ordinal's j, then its offset
-  __shared__ uint16_t own[kOC2];                                // the next tile to load: bucket of each image entry,
-  __shared__ uint32_t ds0[kBins], dib[kBins];                   // the bucket's source and image offset
+  __shared__ uint32_t src[kOC2];                                // the next tile to load: staging index of each entry
   __shared__ uint32_t lw[kOB / 64];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t sb = a.sbase[tid];
@@ -96,10 +95,8 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
     const uint32_t len = hi - lo;
     uint32_t tt;
     const uint32_t ib = block_excl(len, lw, &tt);
-    ds0[tid] = sb + lo;
-    dib[tid] = ib;
-    if (tt <= (uint32_t)kOC2)  // image entries -> bucket
-      for (uint32_t k = 0; k < len; ++k) own[ib + k] = (uint16_t)tid;
+    if (tt <= (uint32_t)kOC2)  // image entry -> staging index
+      for (uint32_t k = 0; k < len; ++k) src[ib + k] = sb + lo + k;
     return tt;
   };
   // the described tile's image entries tid + k kOB into registers (consecutive lanes: consecutive entries, mostly
@@ -108,14 +105,11 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
   auto issue = [&](uint32_t tt) {
     // branch-free, so that every LDS lookup is issued before the first load: an entry past the tile's end reads
     // the tile's last entry again (a cache hit) and is not landed
-    uint32_t b[kLP], e[kLP];
+    uint32_t x[kLP];
 #pragma unroll
-    for (int k = 0; k < kLP; ++k) {
-      e[k] = (uint32_t)(tid + k * kOB) < tt ? (uint32_t)(tid + k * kOB) : tt - 1u;
-      b[k] = own[e[k]];
-    }
+    for (int k = 0; k < kLP; ++k) x[k] = src[(uint32_t)(tid + k * kOB) < tt ? (uint32_t)(tid + k * kOB) : tt - 1u];
 #pragma unroll
-    for (int k = 0; k < kLP; ++k) v[k] = a.stage[ds0[b[k]] + (e[k] - dib[b[k]])];
+    for (int k = 0; k < kLP; ++k) v[k] = a.stage[x[k]];
   };
   auto land = [&](uint32_t tt) {
 #pragma unroll
