@@ -48,6 +48,10 @@ static_assert(kLP == 8 && kOC2 % kLP == 0 && kOC2 <= kLP * kOB, "a thread's bloc
 static_assert(kOC2 < 65536 && (size_t)kOT * 4 <= (size_t)kOC2 * 8, "u16 offsets; the u32 overflow counts alias the input image");
 
 __device__ __forceinline__ uint32_t o2_j(uint64_t v) { return (uint32_t)(v >> 32); }
+// LDS position of image entry e: within each 64-byte block of eight entries the four 16-byte chunks are XOR-swizzled
+// by bits 4-5 of e, so that the 16-byte reads of a thread's block (lane stride 64 bytes) fall in distinct banks,
+// while consecutive lanes landing consecutive entries still fill whole blocks
+__device__ __forceinline__ uint32_t o2_pos(uint32_t e) { return e ^ (((e >> 4) & 3u) << 1); }
 // a value the compiler cannot see through: keeps address arithmetic at its use instead of hoisted (and spilled)
 __device__ __forceinline__ uint32_t o2_opaque(uint32_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -85,7 +89,7 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t sb = a.sbase[tid];
   const int64_t T = a.ntiles;
-  const uint32_t* inj = (const uint32_t*)inb + 1;  // j of image entry e: inj[2 e]
+  const uint32_t* inj = (const uint32_t*)inb + 1;  // j of image entry e: inj[2 o2_pos(e)]
   unsigned long long o2_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, o2_last = SM_O2_CLOCK();
   // phases: 0 prologue 6 issue 1 count 2 scan 3 place 7 land 4 output writes 5 descriptor
 
@@ -115,7 +119,7 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
 #pragma unroll
     for (int k = 0; k < kLP; ++k) {
       const uint32_t e = (uint32_t)(tid + k * kOB);
-      if (e < tt) inb[e] = v[k];
+      if (e < tt) inb[o2_pos(e)] = v[k];
     }
   };
 
@@ -159,19 +163,20 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
         uint32_t jj[kLP], rk8[kLP];
         if (e0 < tcur) {
           const uint4* b4 = (const uint4*)inb + e0 / 2;
+          const int sw = (tid >> 1) & 3;  // o2_pos's chunk swizzle of this block
 #pragma unroll
           for (int q = 0; q < kLP / 2; ++q) {
-            const uint4 x = b4[q];
+            const uint4 x = b4[q ^ sw];
             jj[2 * q] = x.y;
             jj[2 * q + 1] = x.w;
           }
           const uint32_t nv = tcur - e0 < (uint32_t)kLP ? tcur - e0 : (uint32_t)kLP;  // valid entries of the block
           // rank of each entry in its run (the first one's run may come from the block before)
           uint32_t r0 = 0;
-          if (e0 > 0 && inj[2 * (e0 - 1)] == jj[0]) {
+          if (e0 > 0 && inj[2 * o2_pos(e0 - 1)] == jj[0]) {
             const uint32_t eo = o2_opaque(e0);  // no hoisted (spilled) addresses: a scratch reload would wait for
             r0 = 1;                             // the next tile's loads in flight
-            while (r0 < eo && inj[2 * (eo - r0 - 1)] == jj[0]) ++r0;
+            while (r0 < eo && inj[2 * o2_pos(eo - r0 - 1)] == jj[0]) ++r0;
           }
           rk8[0] = r0;
 #pragma unroll
@@ -180,10 +185,10 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
           uint32_t ln[kLP];
           {
             uint32_t x = 0;
-            if (nv == (uint32_t)kLP && e0 + kLP < tcur && inj[2 * (e0 + kLP)] == jj[kLP - 1]) {
+            if (nv == (uint32_t)kLP && e0 + kLP < tcur && inj[2 * o2_pos(e0 + kLP)] == jj[kLP - 1]) {
               const uint32_t eo = o2_opaque(e0 + kLP), to = o2_opaque(tcur);
               x = 1;
-              while (eo + x < to && inj[2 * (eo + x)] == jj[kLP - 1]) ++x;
+              while (eo + x < to && inj[2 * o2_pos(eo + x)] == jj[kLP - 1]) ++x;
             }
             ln[kLP - 1] = 1u + x;
           }
@@ -219,9 +224,10 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
 #pragma unroll
           for (int k = 0; k < kLP; ++k) off[k] = c16[(jj[k] - j0) & (kOT - 1)];
           const uint4* b4 = (const uint4*)inb + e0 / 2;
+          const int sw = (tid >> 1) & 3;
 #pragma unroll
           for (int q = 0; q < kLP / 2; ++q) {
-            const uint4 x = b4[q];
+            const uint4 x = b4[q ^ sw];
             if ((uint32_t)(2 * q) < nv) obuf[off[2 * q] + rk8[2 * q]] = ((uint64_t)x.y << 32) | x.x;
             if ((uint32_t)(2 * q + 1) < nv) obuf[off[2 * q + 1] + rk8[2 * q + 1]] = ((uint64_t)x.w << 32) | x.z;
           }
