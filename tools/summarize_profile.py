@@ -28,7 +28,7 @@ FAMILIES = [("walk_kernel<", "walk"), ("jt_count_kernel", "j_count"), ("jt_place
             ("upsweep_kernel<sm::(anonymous namespace)::RecDigits", "key_up"),
             ("upsweep_kernel<sm::(anonymous namespace)::PairDigits", "j_up"), ("prep_kernel", "prep"),
             ("scan_chunks_kernel", "scan"), ("digit_base_kernel", "scan"),
-            ("stack_kernel", "stack"), ("stack4_kernel", "stack"), ("order_kernel", "order"), ("stage_base_kernel", "stack_prep"),
+            ("stack_kernel", "stack"), ("stack4_kernel", "stack"), ("order_kernel", "order"), ("order2_kernel", "order"), ("stage_base_kernel", "stack_prep"),
             ("carry_in_kernel", "stack_prep"), ("merge_main_kernel", "carry_merge"),
             ("merge_carried_kernel", "carry_merge"),
             ("filter_count", "filter_count"), ("filter_write", "filter_write"), ("filter_block_scan", "filter_scan"),
