@@ -294,7 +294,8 @@ CONFIGS = {
     3: dict(app=APP3, events=1e8, ts_div=1, out="OutputStream", shards=False, scaling="weak",
             workload="config 3: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
                      "(non-partitioned; replicas only)",
-            job_bytes=lambda n, m: 16 * n + 8 * m, cpu_sample=4_000_000),
+            # the CPU sample is BASELINE configs[0], the reference's own CPU case: this query, 1e7 events
+            job_bytes=lambda n, m: 16 * n + 8 * m, cpu_sample=10_000_000),
     4: dict(app=APP, events=1e9, ts_div=10_000, out="OutputStream", shards=True, scaling="strong",
             workload="config 4: partition with (symbol of StockStream) every e1 -> e2 within 1 sec",
             job_bytes=lambda n, m: 20 * n + 8 * m, cpu_sample=4_000_000),
@@ -309,8 +310,9 @@ CONFIGS = {
 }
 
 
-def via_input_handler(cols_dev, n, expect, chunk=None):
-    """Config 4 through the unchanged reference API (VERDICT r03 missing #3): host columns (pageable numpy arrays, as a
+def via_input_handler(cols_dev, n, expect, chunk=None, app_text=APP):
+    """Config 4 (and config 3's query: BASELINE configs[0], the reference's own CPU case, is that app through
+    SiddhiManager / InputHandler) through the unchanged reference API (VERDICT r03 missing #3): host columns (pageable numpy arrays, as a
     JNI receiver would hand over the Event[] data) -> InputHandler.send(Event[]) in columnar form
     (sm_input_send_columns) -> the device-batch pipelines in chunks, the upload of chunk c + 1 overlapping chunk c ->
     every output Event delivered to a registered StreamCallback that counts them (sm_count_events_callback, the
@@ -322,7 +324,7 @@ def via_input_handler(cols_dev, n, expect, chunk=None):
     host = [c[:n].cpu().numpy() for c in cols_dev]
     ts_h, cols_h = host[4], host[:4]
     def one(columns):
-        rt = SiddhiManager().createSiddhiAppRuntime(APP)
+        rt = SiddhiManager().createSiddhiAppRuntime(app_text)
         if chunk:
             _lib.check(L.sm_app_set_option(rt._h, b"bulk_chunk", int(chunk)))
         cnt = ct.c_int64(0)
@@ -361,7 +363,7 @@ def via_input_handler(cols_dev, n, expect, chunk=None):
             "callback": "columns StreamCallback (sm_app_add_stream_columns_callback: each call's Event[] as columns)",
             "events_form": {"value": n / ev_best, "ms": ev_best * 1e3, "host_ms_last_run": ev_phases,
                             "callback": "sm_event StreamCallback (sm_app_add_stream_callback)"},
-            "note": "host columns -> sm_input_send_columns (InputHandler.send(Event[])) -> bucket-stack closed form in "
+            "note": "host columns -> sm_input_send_columns (InputHandler.send(Event[])) -> the closed form in "
                     "chunks (H2D of the next chunk overlapped) -> StreamCallback counting every output Event (value: "
                     "the columns form; events_form: Events as sm_event / sm_value records); best of 2, fresh runtime "
                     "each"}
@@ -457,10 +459,10 @@ def build_parser():
     ap.add_argument("--select5", default="select e1.timestamp as a",
                     help="config 5 diagnostic: the select clause of --query5")
     ap.add_argument("--ih-events", type=float, default=1e8,
-                    help="config 4: events of the input-handler variant (host columns through sm_input_send_columns)")
+                    help="configs 3 and 4: events of the input-handler variant (host columns through sm_input_send_columns)")
     ap.add_argument("--via-input-handler", action="store_true",
-                    help="config 4: run the input-handler variant on all --events")
-    ap.add_argument("--no-ih", action="store_true", help="config 4: skip the input-handler variant")
+                    help="configs 3 and 4: run the input-handler variant on all --events")
+    ap.add_argument("--no-ih", action="store_true", help="configs 3 and 4: skip the input-handler variant")
     ap.add_argument("--ih-chunk", type=float, default=None, help="input-handler variant: option bulk_chunk")
     ap.add_argument("--no-sparse", action="store_true", help="config 4: skip the sparse 64-bit key variant")
     ap.add_argument("--key-partitions", action="store_true",
@@ -735,7 +737,7 @@ def main():
         app_s.close()
         del key64
     ih = None
-    if args.config == 4 and world == 1 and not args.no_ih:
+    if args.config in (3, 4) and world == 1 and not args.no_ih:
         n_ih = N if args.via_input_handler else min(N, int(args.ih_events))
         log(f"input-handler variant on {n_ih} events")
         app.set_option("reset", 0)
@@ -746,7 +748,7 @@ def main():
         if vol_attr is None:  # the plan does not read volume: the host columns still carry it, as a caller's would
             vol_attr = torch.zeros(n_ih, dtype=torch.int64, device=dev)
         ih = via_input_handler([symbol, price, vol_attr, tsattr, ts], n_ih, expect,
-                               int(args.ih_chunk) if args.ih_chunk else None)
+                               int(args.ih_chunk) if args.ih_chunk else None, cfg["app"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         sample = args.cpu_sample or cfg["cpu_sample"]
