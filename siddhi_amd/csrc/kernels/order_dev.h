@@ -8,15 +8,16 @@
 // order2_kernel (round 6, the default; SM_ORDER_V1=1 builds the round-3 order_kernel of stack.hip). That kernel
 // kept the segments in registers from their load to their placement and waited, once per tile, for the segment
 // loads and (gfx9's vmcnt counts loads and stores in order) for the previous tile's output stores: one workgroup per
-// CU spent most of each tile waiting on memory. Here the segments pass through LDS and the roles split:
-//   * an LDS input image holds the tile's segments, bucket after bucket (offsets: a block scan of the lengths);
-//   * count: the first match of each j-run stores the run length in a u16 per ordinal (plain stores: no other
-//     bucket has that j), block scan of the counts, placement of match e at offset(j) + (e - start of its run)
-//     into an LDS output image;
-//   * then waves 0-7 write the output image (coalesced) while waves 8-15 load the NEXT tile's segments into the
-//     input image (flat over image entries through a per-entry staging index, so a wave instruction reads 64
-//     consecutive entries of about eleven segments), and the mt row of the tile after it. The loading waves never store and the
-//     storing waves never load, so neither waits for the other's memory traffic.
+// CU spent most of each tile waiting on memory. Here the segments pass through LDS, and the next tile's loads are in
+// flight while this tile is counted and placed:
+//   * an LDS input image holds the tile's segments, bucket after bucket (offsets: a block scan of the lengths; a
+//     staging index per image entry, written with the tile's descriptor);
+//   * at the top of each tile every thread issues the loads of the next tile's image entries (eight per thread,
+//     lane-consecutive: a wave instruction reads 64 consecutive entries of about eleven segments) and of an mt row
+//     two tiles ahead; they land in the input image after this tile's placement, before its output stores;
+//   * count: each thread takes eight consecutive image entries; the first match of each j-run stores the run length
+//     in a u16 per ordinal (plain stores: no other bucket has that j); block scan of the counts; placement of each
+//     match at offset(j) + its rank in the run into an LDS output image, written out coalesced.
 // A tile with more matches than the images hold (dense matches: kOC2 per 2^kTB ordinals) takes a slower exact path:
 // one thread per bucket, LDS atomic counts, direct placement in HBM.
 #pragma once
@@ -41,7 +42,6 @@ constexpr int kGT2 = SM_ORDER2_GT;
 // scan words leave of 160 KB
 constexpr int kOC2 = ((160 * 1024 - kOT * 2 - 256) / 20) & ~7;
 constexpr int kLP = (kOC2 + kOB - 1) / kOB;  // image entries per thread
-constexpr int kLP1 = kLP;
 static_assert(kOT == 8 * kOB, "eight u16 counts (one 16-byte LDS word) per thread in the scan");
 static_assert(kBins == kOB && kOB == 1024, "one bucket per thread");
 static_assert(kLP == 8 && kOC2 % kLP == 0 && kOC2 <= kLP * kOB, "a thread's block of the image: eight entries, whole");
@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(kOB) order2_kernel(OrderArgs a) {
       if (more) issue(tnext);
       SM_O2_PHASE(6);
       if (!ovf) {
-        // runs: thread tid takes the kLP consecutive entries [e0, e0 + kLP) (kLP1 16-byte reads); run starts, run
+        // runs: thread tid takes the kLP consecutive entries [e0, e0 + kLP) (kLP / 2 16-byte reads); run starts, run
         // lengths and ranks come from register compares, LDS only at the block's edges (a run crossing one: rare).
         // The entry before a run's first is another j: of this bucket, or of another bucket, which never has it.
         const uint32_t e0 = (uint32_t)tid * kLP;
